@@ -1,0 +1,166 @@
+/*
+ * lsr.h — C ABI of the MI355X-native language-Gaussian tile rasterizer
+ * (liblsr.so, hand-written HIP for gfx950).
+ *
+ * This is the drop-in boundary under the reference's operator surface
+ * `diff_gaussian_rasterization` (imported at gaussian_renderer/__init__.py:15,
+ * constructed :37-54, called :108-119).  Each entry point replaces one
+ * binding of the reference's (absent) torch extension `_C`
+ * (submodules/efficient-langsplat-rasterization, .gitmodules:1-3):
+ *
+ *   lsr_forward      <- _C.rasterize_gaussians           (forward of
+ *                       GaussianRasterizer.__call__, gaussian_renderer/__init__.py:108-119)
+ *   lsr_backward     <- _C.rasterize_gaussians_backward  (autograd backward,
+ *                       reached from loss.backward() at train.py:173)
+ *   lsr_mark_visible <- _C.mark_visible                  (GaussianRasterizer.markVisible)
+ *   lsr_strerror     <- the RuntimeError text the binding raises
+ *
+ * Conventions
+ *  - All tensor pointers are DEVICE pointers to contiguous fp32 (int32 for
+ *    radii) arrays with the shapes documented per field; optional inputs are
+ *    NULL.  N = number of Gaussians, H×W image, D dense language channels,
+ *    K quick entries per Gaussian, Dq quick output channels.
+ *  - Matrices are the reference's `world_view_transform` /
+ *    `full_proj_transform` tensors as stored (row-major transposed, i.e.
+ *    column-major math matrices; scene/cameras.py:55-57).
+ *  - The library never allocates device memory itself: workspaces are
+ *    requested through `alloc(ctx, bytes, which)` (torch's caching allocator
+ *    on the Python side) and returned in the out struct so the caller can
+ *    keep them for backward (the upstream geomBuffer/binningBuffer/imgBuffer
+ *    pattern).  Returned pointers must be 256-byte aligned.
+ *  - All work is enqueued on `stream` (a hipStream_t).  lsr_forward performs
+ *    exactly one host synchronisation (the num_rendered read-back that sizes
+ *    the binning workspace).
+ *  - Return value 0 = success; otherwise an LSR_E* code (lsr_strerror).
+ */
+#ifndef LSR_H
+#define LSR_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LSR_ABI_VERSION 1
+
+enum {
+    LSR_OK = 0,
+    LSR_EINVAL = 1,        /* invalid argument / shape / missing input */
+    LSR_EUNSUPPORTED = 2,  /* e.g. language dim beyond the compiled channel sets */
+    LSR_EHIP = 3,          /* HIP launch / runtime failure */
+    LSR_ENOMEM = 4,        /* alloc callback returned NULL */
+    LSR_EOVERFLOW = 5      /* num_rendered does not fit 32-bit instance indices */
+};
+
+/* GaussianRasterizationSettings (gaussian_renderer/__init__.py:37-52),
+ * field for field, plus the optional trailing quick_dim (u4). */
+typedef struct lsr_settings {
+    int image_height;
+    int image_width;
+    float tanfovx;
+    float tanfovy;
+    const float* bg;          /* (3,) device */
+    float scale_modifier;
+    const float* viewmatrix;  /* (4,4) device */
+    const float* projmatrix;  /* (4,4) device */
+    int sh_degree;            /* active SH degree (0..3) */
+    const float* campos;      /* (3,) device */
+    int prefiltered;
+    int debug;                /* sync + check after every stage */
+    int include_feature;      /* dense language channels on */
+    int quick_render;         /* sparse (weights, indices) language channels on */
+    int quick_dim;            /* Dq; 0 selects the reference default 192 */
+} lsr_settings;
+
+enum { LSR_INDEX_F32 = 0, LSR_INDEX_I32 = 1, LSR_INDEX_I64 = 2 };
+
+/* GaussianRasterizer.forward kwargs (gaussian_renderer/__init__.py:108-119). */
+typedef struct lsr_inputs {
+    int P;                          /* N */
+    int max_coeffs;                 /* shs.shape[1] (16 at degree 3) */
+    int lang_dim;                   /* D = language_feature_precomp.shape[1] */
+    int quick_k;                    /* K = language_feature_weights_quick.shape[1] */
+    int quick_index_dtype;          /* LSR_INDEX_* of language_feature_indices */
+    const float* means3D;           /* (N,3) */
+    const float* shs;               /* (N,M,3) or NULL */
+    const float* colors_precomp;    /* (N,3) or NULL (exactly one of shs/colors) */
+    const float* opacities;         /* (N,1) */
+    const float* scales;            /* (N,3) or NULL */
+    const float* rotations;         /* (N,4) wxyz or NULL (normalised by caller) */
+    const float* cov3D_precomp;     /* (N,6) or NULL (exactly one of scale+rot/cov) */
+    const float* language_feature_precomp;       /* (N,D) or NULL */
+    const float* language_feature_weights_quick; /* (N,K) or NULL */
+    const void* language_feature_indices;        /* (N,K) or NULL */
+} lsr_inputs;
+
+typedef void* (*lsr_alloc_fn)(void* ctx, size_t bytes, int which);
+enum { LSR_BUF_GEOM = 0, LSR_BUF_BINNING = 1, LSR_BUF_IMAGE = 2, LSR_BUF_GRAD = 3 };
+
+typedef struct lsr_fwd_out {
+    float* out_color;     /* (3,H,W)  caller-allocated */
+    float* out_lang;      /* (Dout,H,W) caller-allocated, Dout = D (dense), Dq (quick) or 0 */
+    int32_t* radii;       /* (N,) caller-allocated */
+    /* filled by lsr_forward: */
+    void* geom;    size_t geom_bytes;
+    void* binning; size_t binning_bytes;
+    void* image;   size_t image_bytes;
+    int64_t num_rendered;
+} lsr_fwd_out;
+
+/* _C.rasterize_gaussians: preprocess → binning (tile buckets + per-tile depth
+ * sort) → per-pixel alpha blend of RGB + language channels. */
+int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out,
+                lsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+
+typedef struct lsr_bwd_in {
+    const void* geom;
+    const void* binning;
+    const void* image;
+    int64_t num_rendered;
+    const int32_t* radii;           /* (N,) from forward */
+    const float* dL_dout_color;     /* (3,H,W) */
+    const float* dL_dout_lang;      /* (D,H,W) or NULL */
+} lsr_bwd_in;
+
+/* Gradient outputs; NULL = not requested (needs_input_grad False).  Every
+ * non-NULL array is fully written (no pre-zeroing needed). */
+typedef struct lsr_bwd_out {
+    float* dL_dmeans2D;     /* (N,3): [:, :2] = dL/d(NDC xy), [:, 2] = 0 */
+    float* dL_dcolors;      /* (N,3): dL/dcolors_precomp */
+    float* dL_dlang;        /* (N,D): dL/dlanguage_feature_precomp */
+    float* dL_dopacity;     /* (N,1) */
+    float* dL_dmeans3D;     /* (N,3) */
+    float* dL_dcov3D;       /* (N,6) */
+    float* dL_dsh;          /* (N,M,3) */
+    float* dL_dscales;      /* (N,3) */
+    float* dL_drotations;   /* (N,4) */
+} lsr_bwd_out;
+
+/* _C.rasterize_gaussians_backward. */
+int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* b,
+                 lsr_bwd_out* out, lsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+
+/* _C.mark_visible: present[i] = (view-space z of means3D[i]) > 0.2. */
+int lsr_mark_visible(int P, const float* means3D, const float* viewmatrix,
+                     const float* projmatrix, uint8_t* present, void* stream);
+
+const char* lsr_strerror(int code);
+int lsr_abi_version(void);
+
+/* Dense language channel sets compiled into this build (ascending; D is
+ * rounded up to the next set).  Returns the largest supported D. */
+int lsr_max_lang_dim(void);
+
+/* Diagnostics: per-stage HIP-event timing on the caller's stream (used by
+ * bench.py for the live roofline).  Not thread-safe; off by default.
+ * lsr_profile_query fills up to max_stages (name, total ms, call count)
+ * triples since the last reset and returns the number filled. */
+void lsr_profile_enable(int on);
+void lsr_profile_reset(void);
+int lsr_profile_query(const char** names, double* ms, int64_t* calls, int max_stages);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,170 @@
+"""ctypes binding of liblsr.so (the C ABI declared in include/lsr.h).
+
+This is the Python side of the drop-in boundary: the same role the
+reference's compiled `diff_gaussian_rasterization._C` plays
+(gaussian_renderer/__init__.py:15).  No CPU fallback exists: if the HIP
+library is missing, or tensors are not on a ROCm device, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("LSR_LIB", os.path.join(_HERE, "liblsr.so"))
+
+LSR_OK = 0
+LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_GRAD = 0, 1, 2, 3
+LSR_INDEX_F32, LSR_INDEX_I32, LSR_INDEX_I64 = 0, 1, 2
+
+_vp = ctypes.c_void_p
+
+
+class Settings(ctypes.Structure):
+    _fields_ = [
+        ("image_height", ctypes.c_int),
+        ("image_width", ctypes.c_int),
+        ("tanfovx", ctypes.c_float),
+        ("tanfovy", ctypes.c_float),
+        ("bg", _vp),
+        ("scale_modifier", ctypes.c_float),
+        ("viewmatrix", _vp),
+        ("projmatrix", _vp),
+        ("sh_degree", ctypes.c_int),
+        ("campos", _vp),
+        ("prefiltered", ctypes.c_int),
+        ("debug", ctypes.c_int),
+        ("include_feature", ctypes.c_int),
+        ("quick_render", ctypes.c_int),
+        ("quick_dim", ctypes.c_int),
+    ]
+
+
+class Inputs(ctypes.Structure):
+    _fields_ = [
+        ("P", ctypes.c_int),
+        ("max_coeffs", ctypes.c_int),
+        ("lang_dim", ctypes.c_int),
+        ("quick_k", ctypes.c_int),
+        ("quick_index_dtype", ctypes.c_int),
+        ("means3D", _vp),
+        ("shs", _vp),
+        ("colors_precomp", _vp),
+        ("opacities", _vp),
+        ("scales", _vp),
+        ("rotations", _vp),
+        ("cov3D_precomp", _vp),
+        ("language_feature_precomp", _vp),
+        ("language_feature_weights_quick", _vp),
+        ("language_feature_indices", _vp),
+    ]
+
+
+class FwdOut(ctypes.Structure):
+    _fields_ = [
+        ("out_color", _vp),
+        ("out_lang", _vp),
+        ("radii", _vp),
+        ("geom", _vp),
+        ("geom_bytes", ctypes.c_size_t),
+        ("binning", _vp),
+        ("binning_bytes", ctypes.c_size_t),
+        ("image", _vp),
+        ("image_bytes", ctypes.c_size_t),
+        ("num_rendered", ctypes.c_int64),
+    ]
+
+
+class BwdIn(ctypes.Structure):
+    _fields_ = [
+        ("geom", _vp),
+        ("binning", _vp),
+        ("image", _vp),
+        ("num_rendered", ctypes.c_int64),
+        ("radii", _vp),
+        ("dL_dout_color", _vp),
+        ("dL_dout_lang", _vp),
+    ]
+
+
+class BwdOut(ctypes.Structure):
+    _fields_ = [
+        ("dL_dmeans2D", _vp),
+        ("dL_dcolors", _vp),
+        ("dL_dlang", _vp),
+        ("dL_dopacity", _vp),
+        ("dL_dmeans3D", _vp),
+        ("dL_dcov3D", _vp),
+        ("dL_dsh", _vp),
+        ("dL_dscales", _vp),
+        ("dL_drotations", _vp),
+    ]
+
+
+ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
+
+EXPORTS = ("lsr_forward", "lsr_backward", "lsr_mark_visible", "lsr_strerror", "lsr_abi_version",
+           "lsr_max_lang_dim", "lsr_profile_enable", "lsr_profile_reset", "lsr_profile_query")
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load liblsr.so (after torch, so the HIP runtime torch already mapped is
+    the one the library binds to).  Raises if the library is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(
+            f"liblsr.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(or `make -C langsplatv2_amd/csrc`).  There is no CPU fallback.")
+    lib = ctypes.CDLL(p)
+    lib.lsr_forward.argtypes = [ctypes.POINTER(Settings), ctypes.POINTER(Inputs), ctypes.POINTER(FwdOut),
+                                ALLOC_FN, _vp, _vp]
+    lib.lsr_forward.restype = ctypes.c_int
+    lib.lsr_backward.argtypes = [ctypes.POINTER(Settings), ctypes.POINTER(Inputs), ctypes.POINTER(BwdIn),
+                                 ctypes.POINTER(BwdOut), ALLOC_FN, _vp, _vp]
+    lib.lsr_backward.restype = ctypes.c_int
+    lib.lsr_mark_visible.argtypes = [ctypes.c_int, _vp, _vp, _vp, _vp, _vp]
+    lib.lsr_mark_visible.restype = ctypes.c_int
+    lib.lsr_strerror.argtypes = [ctypes.c_int]
+    lib.lsr_strerror.restype = ctypes.c_char_p
+    lib.lsr_abi_version.restype = ctypes.c_int
+    lib.lsr_max_lang_dim.restype = ctypes.c_int
+    lib.lsr_profile_enable.argtypes = [ctypes.c_int]
+    lib.lsr_profile_enable.restype = None
+    lib.lsr_profile_reset.restype = None
+    lib.lsr_profile_query.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+    lib.lsr_profile_query.restype = ctypes.c_int
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc: int, what: str):
+    if rc != LSR_OK:
+        msg = load().lsr_strerror(rc).decode()
+        raise RuntimeError(f"{what} failed: {msg} (code {rc})")
+
+
+def profile_enable(on: bool = True):
+    load().lsr_profile_enable(1 if on else 0)
+
+
+def profile_reset():
+    load().lsr_profile_reset()
+
+
+def profile_query() -> dict:
+    """{stage: (total_ms, calls)} since the last reset (synchronises the events)."""
+    n = 16
+    names = (ctypes.c_char_p * n)()
+    ms = (ctypes.c_double * n)()
+    calls = (ctypes.c_int64 * n)()
+    k = load().lsr_profile_query(names, ms, calls, n)
+    if k < 0:
+        raise RuntimeError("lsr_profile_query failed")
+    return {names[i].decode(): (ms[i], int(calls[i])) for i in range(k)}

@@ -1,0 +1,355 @@
+// lsr_api.hip — the C ABI (include/lsr.h): host-side driver that validates
+// arguments, requests workspaces through the caller's allocator and enqueues
+// the gfx950 kernels on the caller's stream.
+//
+// Forward pipeline (one host sync, for num_rendered):
+//   preprocess -> scan(tiles_touched) -> [read M] -> duplicate (tile ranks)
+//   -> scan(tile counts) -> scatter into tile buckets -> per-tile depth sort
+//   -> render (dense or quick)
+// Backward: zero gradient rows -> render bwd (wave-reduced atomics)
+//   -> preprocess bwd (chain rule, writes every requested output).
+#include <stdio.h>
+#include <utility>
+#include <vector>
+#include "lsr_internal.h"
+
+using namespace lsr;
+
+namespace {
+
+struct Status {
+    int code = LSR_OK;
+};
+
+#define LSR_HIP(expr)                                                        \
+    do {                                                                     \
+        hipError_t _e = (expr);                                              \
+        if (_e != hipSuccess) {                                              \
+            fprintf(stderr, "[lsr] %s failed: %s (%s:%d)\n", #expr,          \
+                    hipGetErrorString(_e), __FILE__, __LINE__);              \
+            return LSR_EHIP;                                                 \
+        }                                                                    \
+    } while (0)
+
+#define LSR_DEBUG_SYNC(s, st, stage)                                         \
+    do {                                                                     \
+        if ((s)->debug) {                                                    \
+            hipError_t _e = hipStreamSynchronize(st);                        \
+            if (_e == hipSuccess) _e = hipGetLastError();                    \
+            if (_e != hipSuccess) {                                          \
+                fprintf(stderr, "[lsr] stage %s failed: %s\n", stage,        \
+                        hipGetErrorString(_e));                              \
+                return LSR_EHIP;                                             \
+            }                                                                \
+        }                                                                    \
+    } while (0)
+
+// ---------------------------------------------------------------- profiling
+// Optional per-stage HIP-event timing (diagnostics for bench.py's roofline):
+// when enabled, each stage is bracketed by two events recorded on the
+// caller's stream; lsr_profile_query sums their elapsed times.
+enum Stage { ST_PRE, ST_SCAN, ST_DUP, ST_SCAN_T, ST_SCATTER, ST_SORT, ST_RENDER, ST_GZERO, ST_RENDER_BWD,
+             ST_PRE_BWD, ST_N };
+const char* kStageNames[ST_N] = {"preprocess", "scan_tiles", "duplicate", "scan_tile_counts", "scatter",
+                                 "tile_sort", "render_fwd", "grad_zero", "render_bwd", "preprocess_bwd"};
+
+struct Prof {
+    bool on = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[ST_N];
+    size_t used[ST_N] = {};
+};
+Prof g_prof;
+
+struct StageScope {
+    Stage s;
+    hipStream_t st;
+    bool on;
+    StageScope(Stage s_, hipStream_t st_) : s(s_), st(st_), on(g_prof.on)
+    {
+        if (!on) return;
+        auto& v = g_prof.ev[s];
+        if (g_prof.used[s] == v.size()) {
+            hipEvent_t a, b;
+            if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) { on = false; return; }
+            v.push_back({a, b});
+        }
+        (void)hipEventRecord(v[g_prof.used[s]].first, st);
+    }
+    ~StageScope()
+    {
+        if (!on) return;
+        (void)hipEventRecord(g_prof.ev[s][g_prof.used[s]].second, st);
+        g_prof.used[s]++;
+    }
+};
+
+int dense_dim(const lsr_settings* s, const lsr_inputs* in)
+{
+    if (s->quick_render) return 0;
+    if (!s->include_feature) return 0;
+    return in->language_feature_precomp ? in->lang_dim : 0;
+}
+
+int quick_dim(const lsr_settings* s)
+{
+    return s->quick_dim > 0 ? s->quick_dim : 192;
+}
+
+int validate(const lsr_settings* s, const lsr_inputs* in)
+{
+    if (!s || !in) return LSR_EINVAL;
+    if (s->image_height <= 0 || s->image_width <= 0 || in->P < 0) return LSR_EINVAL;
+    if (!s->bg || !s->viewmatrix || !s->projmatrix || !s->campos) return LSR_EINVAL;
+    if (in->P > 0) {
+        if (!in->means3D || !in->opacities) return LSR_EINVAL;
+        if ((in->shs == nullptr) == (in->colors_precomp == nullptr)) return LSR_EINVAL;
+        const bool sr = in->scales && in->rotations;
+        if (sr == (in->cov3D_precomp != nullptr)) return LSR_EINVAL;
+        if (in->shs && (in->max_coeffs <= 0 || s->sh_degree < 0 || s->sh_degree > 3 ||
+                        (s->sh_degree + 1) * (s->sh_degree + 1) > in->max_coeffs))
+            return LSR_EINVAL;
+        if (in->shs && in->max_coeffs > 16) return LSR_EUNSUPPORTED;
+    }
+    if (s->quick_render) {
+        if (in->P > 0 && (!in->language_feature_weights_quick || !in->language_feature_indices || in->quick_k <= 0))
+            return LSR_EINVAL;
+        if (in->quick_index_dtype < LSR_INDEX_F32 || in->quick_index_dtype > LSR_INDEX_I64) return LSR_EINVAL;
+        if ((size_t)quick_dim(s) * 256 + 64 * (32 + 12 + 8 * (size_t)in->quick_k) > 65536) return LSR_EUNSUPPORTED;
+    } else if (s->include_feature) {
+        if (in->P > 0 && (!in->language_feature_precomp || in->lang_dim <= 0)) return LSR_EINVAL;
+        if (lang_set_for(in->lang_dim) < 0) return LSR_EUNSUPPORTED;
+    }
+    return LSR_OK;
+}
+
+Cam make_cam(const lsr_settings* s)
+{
+    Cam c;
+    c.W = s->image_width;
+    c.H = s->image_height;
+    c.gx = (c.W + LSR_TILE - 1) / LSR_TILE;
+    c.gy = (c.H + LSR_TILE - 1) / LSR_TILE;
+    c.tanfovx = s->tanfovx;
+    c.tanfovy = s->tanfovy;
+    c.fx = (float)c.W / (2.0f * s->tanfovx);
+    c.fy = (float)c.H / (2.0f * s->tanfovy);
+    c.scale_modifier = s->scale_modifier;
+    c.view = s->viewmatrix;
+    c.proj = s->projmatrix;
+    c.campos = s->campos;
+    c.bg = s->bg;
+    c.sh_degree = s->sh_degree;
+    return c;
+}
+
+RenderArgs make_render_args(const lsr_settings* s, const lsr_inputs* in, const Cam& c, const uint8_t* geom,
+                            const uint8_t* bin, const uint8_t* img, int64_t M)
+{
+    RenderArgs a;
+    const GeomLayout GL = geom_layout((size_t)in->P);
+    const int T = c.gx * c.gy;
+    const ImageLayout IL = image_layout((size_t)c.W * c.H, (size_t)T);
+    const BinLayout BL = bin_layout((size_t)M);
+    a.cam = c;
+    a.P = in->P;
+    a.splatA = (const float4*)(geom + GL.splatA);
+    a.splatB = (const float4*)(geom + GL.splatB);
+    a.rgb = in->colors_precomp ? in->colors_precomp : (const float*)(geom + GL.rgb);
+    a.D = dense_dim(s, in);
+    a.lang = a.D ? in->language_feature_precomp : nullptr;
+    a.qw = s->quick_render ? in->language_feature_weights_quick : nullptr;
+    a.qi = s->quick_render ? in->language_feature_indices : nullptr;
+    a.qidx_dtype = in->quick_index_dtype;
+    a.K = s->quick_render ? in->quick_k : 0;
+    a.Dq = s->quick_render ? quick_dim(s) : 0;
+    a.point_list = (const uint32_t*)(bin + BL.point_list);
+    a.tile_start = (const uint32_t*)(img + IL.tile_start);
+    a.final_T = (float*)(img + IL.final_T);
+    a.n_contrib = (uint32_t*)(img + IL.n_contrib);
+    a.out_color = nullptr;
+    a.out_lang = nullptr;
+    return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* lsr_strerror(int code)
+{
+    switch (code) {
+        case LSR_OK: return "success";
+        case LSR_EINVAL: return "invalid argument (shapes, missing or conflicting inputs)";
+        case LSR_EUNSUPPORTED: return "unsupported configuration (language dim / SH coefficients beyond the compiled sets)";
+        case LSR_EHIP: return "HIP runtime or kernel launch failure";
+        case LSR_ENOMEM: return "workspace allocation failed";
+        case LSR_EOVERFLOW: return "num_rendered exceeds 32-bit instance indexing";
+        default: return "unknown error";
+    }
+}
+
+int lsr_abi_version(void) { return LSR_ABI_VERSION; }
+
+int lsr_max_lang_dim(void) { return 64; }
+
+void lsr_profile_enable(int on)
+{
+    g_prof.on = on != 0;
+}
+
+void lsr_profile_reset(void)
+{
+    for (int k = 0; k < ST_N; k++) g_prof.used[k] = 0;
+}
+
+int lsr_profile_query(const char** names, double* ms, int64_t* calls, int max_stages)
+{
+    int n = 0;
+    for (int k = 0; k < ST_N && n < max_stages; k++, n++) {
+        double tot = 0.0;
+        for (size_t i = 0; i < g_prof.used[k]; i++) {
+            float e = 0.f;
+            if (hipEventSynchronize(g_prof.ev[k][i].second) != hipSuccess) return -LSR_EHIP;
+            if (hipEventElapsedTime(&e, g_prof.ev[k][i].first, g_prof.ev[k][i].second) != hipSuccess) return -LSR_EHIP;
+            tot += e;
+        }
+        if (names) names[n] = kStageNames[k];
+        if (ms) ms[n] = tot;
+        if (calls) calls[n] = (int64_t)g_prof.used[k];
+    }
+    return n;
+}
+
+int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, lsr_alloc_fn alloc, void* ctx,
+                void* stream)
+{
+    int rc = validate(s, in);
+    if (rc != LSR_OK) return rc;
+    if (!out || !alloc || !out->out_color || (in->P > 0 && !out->radii)) return LSR_EINVAL;
+    const int Dd = dense_dim(s, in);
+    if ((Dd > 0 || s->quick_render) && !out->out_lang) return LSR_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    const Cam c = make_cam(s);
+    const int P = in->P;
+    const int T = c.gx * c.gy;
+    const size_t NPIX = (size_t)c.W * c.H;
+
+    const GeomLayout GL = geom_layout((size_t)P);
+    const ImageLayout IL = image_layout(NPIX, (size_t)T);
+    uint8_t* geom = (uint8_t*)alloc(ctx, GL.total, LSR_BUF_GEOM);
+    uint8_t* img = (uint8_t*)alloc(ctx, IL.total, LSR_BUF_IMAGE);
+    if (!geom || !img) return LSR_ENOMEM;
+    out->geom = geom;
+    out->geom_bytes = GL.total;
+    out->image = img;
+    out->image_bytes = IL.total;
+
+    // 1. preprocess
+    { StageScope sc(ST_PRE, st); LSR_HIP(launch_preprocess(c, *in, geom, out->radii, st)); }
+    LSR_DEBUG_SYNC(s, st, "preprocess");
+    // 2. scan tiles_touched -> offsets ; read num_rendered
+    uint64_t* gpart = (uint64_t*)(geom + GL.scan_part);
+    const size_t gnb = scan_partials((size_t)P) - 1;
+    {
+        StageScope sc(ST_SCAN, st);
+        LSR_HIP(launch_scan_u32((const uint32_t*)(geom + GL.tiles), (uint32_t*)(geom + GL.offsets), gpart,
+                                (size_t)P, false, st));
+    }
+    uint64_t M = 0;
+    LSR_HIP(hipMemcpyAsync(&M, gpart + gnb, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    LSR_HIP(hipStreamSynchronize(st));
+    if (M >= 0xffffffffull) return LSR_EOVERFLOW;
+    out->num_rendered = (int64_t)M;
+
+    // 3. binning
+    const BinLayout BL = bin_layout((size_t)M);
+    uint8_t* bin = (uint8_t*)alloc(ctx, BL.total > 0 ? BL.total : 256, LSR_BUF_BINNING);
+    if (!bin) return LSR_ENOMEM;
+    out->binning = bin;
+    out->binning_bytes = BL.total;
+    uint32_t* tile_cnt = (uint32_t*)(img + IL.tile_cnt);
+    uint32_t* tile_start = (uint32_t*)(img + IL.tile_start);
+    uint64_t* tpart = (uint64_t*)(img + IL.tile_part);
+    {
+        StageScope sc(ST_DUP, st);
+        LSR_HIP(hipMemsetAsync(tile_cnt, 0, (size_t)T * 4, st));
+        LSR_HIP(launch_duplicate(c, P, geom, out->radii, tile_cnt, (uint32_t*)(bin + BL.rank), st));
+    }
+    LSR_DEBUG_SYNC(s, st, "duplicate");
+    {
+        StageScope sc(ST_SCAN_T, st);
+        LSR_HIP(launch_scan_u32(tile_cnt, tile_start, tpart, (size_t)T, true, st));
+        const size_t tnb = scan_partials((size_t)T) - 1;
+        LSR_HIP(hipMemcpyAsync(tile_start + T, tpart + tnb, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    }
+    {
+        StageScope sc(ST_SCATTER, st);
+        LSR_HIP(launch_scatter(c, P, geom, out->radii, tile_start, (const uint32_t*)(bin + BL.rank),
+                               (uint64_t*)(bin + BL.keys), st));
+    }
+    LSR_DEBUG_SYNC(s, st, "scatter");
+    {
+        StageScope sc(ST_SORT, st);
+        LSR_HIP(launch_tile_sort(T, tile_start, (uint64_t*)(bin + BL.keys), (uint32_t*)(bin + BL.point_list), st));
+    }
+    LSR_DEBUG_SYNC(s, st, "tile_sort");
+
+    // 4. render
+    RenderArgs ra = make_render_args(s, in, c, geom, bin, img, (int64_t)M);
+    ra.out_color = out->out_color;
+    ra.out_lang = out->out_lang;
+    { StageScope sc(ST_RENDER, st); LSR_HIP(launch_render_fwd(ra, st)); }
+    LSR_DEBUG_SYNC(s, st, "render");
+    return LSR_OK;
+}
+
+int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* b, lsr_bwd_out* out,
+                 lsr_alloc_fn alloc, void* ctx, void* stream)
+{
+    int rc = validate(s, in);
+    if (rc != LSR_OK) return rc;
+    if (!b || !out || !alloc || !b->geom || !b->image || !b->binning || !b->dL_dout_color) return LSR_EINVAL;
+    const int Dd = dense_dim(s, in);
+    if (Dd > 0 && !b->dL_dout_lang) return LSR_EINVAL;
+    if (in->P == 0) return LSR_OK;
+    if (!b->radii) return LSR_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    const Cam c = make_cam(s);
+    const int P = in->P;
+    const int VP = grad_row_width(Dd);
+    float* gacc = (float*)alloc(ctx, (size_t)P * VP * 4, LSR_BUF_GRAD);
+    if (!gacc) return LSR_ENOMEM;
+    { StageScope sc(ST_GZERO, st); LSR_HIP(hipMemsetAsync(gacc, 0, (size_t)P * VP * 4, st)); }
+
+    RenderBwdArgs rb;
+    rb.f = make_render_args(s, in, c, (const uint8_t*)b->geom, (const uint8_t*)b->binning, (const uint8_t*)b->image,
+                            b->num_rendered);
+    rb.f.qw = nullptr;  // quick language channels are not differentiated
+    rb.f.D = Dd;
+    rb.f.lang = Dd ? in->language_feature_precomp : nullptr;
+    rb.dout_color = b->dL_dout_color;
+    rb.dout_lang = Dd ? b->dL_dout_lang : nullptr;
+    rb.grad_acc = gacc;
+    rb.VP = VP;
+    { StageScope sc(ST_RENDER_BWD, st); LSR_HIP(launch_render_bwd(rb, st)); }
+    LSR_DEBUG_SYNC(s, st, "render_bwd");
+
+    lsr_inputs in2 = *in;
+    in2.lang_dim = Dd;
+    lsr_bwd_out o2 = *out;
+    if (!Dd) o2.dL_dlang = nullptr;
+    { StageScope sc(ST_PRE_BWD, st); LSR_HIP(launch_preprocess_bwd(c, in2, (const uint8_t*)b->geom, b->radii, gacc, VP, o2, st)); }
+    LSR_DEBUG_SYNC(s, st, "preprocess_bwd");
+    return LSR_OK;
+}
+
+int lsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, uint8_t* present,
+                     void* stream)
+{
+    (void)projmatrix;
+    if (P < 0 || (P > 0 && (!means3D || !viewmatrix || !present))) return LSR_EINVAL;
+    LSR_HIP(launch_mark_visible(P, means3D, viewmatrix, present, (hipStream_t)stream));
+    return LSR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,295 @@
+// lsr_device.h — device-side math and layouts of the gfx950 rasterizer.
+//
+// Floating-point contract: every .hip file is compiled with -ffp-contract=off
+// and each fused multiply-add is an explicit fmaf().  The operation sequence
+// of every function here is the one the CPU restatement (oracle/lsr_oracle.c)
+// specifies, so forward results are bit-identical to it.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define LSR_TILE 16
+#define LSR_TILE_PIX 256
+#define LSR_WAVE 64
+
+namespace lsr {
+
+// ------------------------------------------------------------------ math --
+// Deterministic exp for x <= 0: Cody-Waite reduction + degree-7 Taylor
+// (|rel err| < 2 ulp).  Replaces the CUDA reference's expf so results are
+// reproducible on the CPU bit for bit.
+__device__ __forceinline__ float expf_det(float x)
+{
+    if (x < -87.0f) return 0.0f;
+    float n = rintf(x * 1.44269504088896341f);
+    float r = fmaf(n, -0.693145751953125f, x);
+    r = fmaf(n, -1.428606765330187e-06f, r);
+    float p = 1.98412698412698413e-04f;
+    p = fmaf(p, r, 1.38888888888888889e-03f);
+    p = fmaf(p, r, 8.33333333333333333e-03f);
+    p = fmaf(p, r, 4.16666666666666667e-02f);
+    p = fmaf(p, r, 1.66666666666666667e-01f);
+    p = fmaf(p, r, 0.5f);
+    p = fmaf(p, r, 1.0f);
+    p = fmaf(p, r, 1.0f);
+    int ni = (int)n;
+    float sc = __int_as_float((ni + 127) << 23);
+    return p * sc;
+}
+
+// float -> int truncating + saturating; NaN -> 0 (matches oracle f2i).
+__device__ __forceinline__ int f2i(float v)
+{
+    if (v != v) return 0;
+    if (v >= 2147483520.0f) return 2147483647;
+    if (v <= -2147483648.0f) return (int)(-2147483647 - 1);
+    return (int)v;
+}
+
+__device__ __forceinline__ float ndc2pix(float v, int S)
+{
+    return (float)((((double)v + 1.0) * (double)S - 1.0) * 0.5);
+}
+
+__device__ __forceinline__ void get_rect(float px, float py, int r, int gx, int gy, int& x0, int& y0, int& x1, int& y1)
+{
+    x0 = min(gx, max(0, f2i((px - (float)r) / 16.0f)));
+    y0 = min(gy, max(0, f2i((py - (float)r) / 16.0f)));
+    x1 = min(gx, max(0, f2i((px + (float)r + 16.0f - 1.0f) / 16.0f)));
+    y1 = min(gy, max(0, f2i((py + (float)r + 16.0f - 1.0f) / 16.0f)));
+}
+
+// Column-major 4x4 (m[c*4+r]) point transforms.
+__device__ __forceinline__ float3 xform43(const float* m, float x, float y, float z)
+{
+    return make_float3(m[0] * x + m[4] * y + m[8] * z + m[12],
+                       m[1] * x + m[5] * y + m[9] * z + m[13],
+                       m[2] * x + m[6] * y + m[10] * z + m[14]);
+}
+__device__ __forceinline__ float4 xform44(const float* m, float x, float y, float z)
+{
+    return make_float4(m[0] * x + m[4] * y + m[8] * z + m[12],
+                       m[1] * x + m[5] * y + m[9] * z + m[13],
+                       m[2] * x + m[6] * y + m[10] * z + m[14],
+                       m[3] * x + m[7] * y + m[11] * z + m[15]);
+}
+
+// Quaternion (r,x,y,z) -> row-major R (utils/general_utils.py:90-98, no renormalisation).
+__device__ __forceinline__ void quat_to_R(float r, float x, float y, float z, float* R)
+{
+    R[0] = 1.f - 2.f * (y * y + z * z);
+    R[1] = 2.f * (x * y - r * z);
+    R[2] = 2.f * (x * z + r * y);
+    R[3] = 2.f * (x * y + r * z);
+    R[4] = 1.f - 2.f * (x * x + z * z);
+    R[5] = 2.f * (y * z - r * x);
+    R[6] = 2.f * (x * z - r * y);
+    R[7] = 2.f * (y * z + r * x);
+    R[8] = 1.f - 2.f * (x * x + y * y);
+}
+
+__device__ __forceinline__ void compute_cov3D(float s0, float s1, float s2, float mod, float4 q, float* cov)
+{
+    float R[9], Mm[9];
+    quat_to_R(q.x, q.y, q.z, q.w, R);
+    float sx = mod * s0, sy = mod * s1, sz = mod * s2;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        Mm[i * 3 + 0] = R[i * 3 + 0] * sx;
+        Mm[i * 3 + 1] = R[i * 3 + 1] * sy;
+        Mm[i * 3 + 2] = R[i * 3 + 2] * sz;
+    }
+#define LSR_SIG(i, j) (Mm[(i)*3 + 0] * Mm[(j)*3 + 0] + Mm[(i)*3 + 1] * Mm[(j)*3 + 1] + Mm[(i)*3 + 2] * Mm[(j)*3 + 2])
+    cov[0] = LSR_SIG(0, 0);
+    cov[1] = LSR_SIG(0, 1);
+    cov[2] = LSR_SIG(0, 2);
+    cov[3] = LSR_SIG(1, 1);
+    cov[4] = LSR_SIG(1, 2);
+    cov[5] = LSR_SIG(2, 2);
+#undef LSR_SIG
+}
+
+struct Ewa {
+    float tx, ty, tz;
+    bool xclamp, yclamp;
+    float J00, J02, J11, J12;
+    float T0[3], T1[3];
+};
+
+__device__ __forceinline__ void ewa_setup(const float* view, float3 pv, float fx, float fy, float tanfx, float tanfy, Ewa& e)
+{
+    const float limx = 1.3f * tanfx, limy = 1.3f * tanfy;
+    float txtz = pv.x / pv.z, tytz = pv.y / pv.z;
+    e.xclamp = (txtz < -limx) || (txtz > limx);
+    e.yclamp = (tytz < -limy) || (tytz > limy);
+    e.tz = pv.z;
+    e.tx = fminf(limx, fmaxf(-limx, txtz)) * pv.z;
+    e.ty = fminf(limy, fmaxf(-limy, tytz)) * pv.z;
+    float tz2 = e.tz * e.tz;
+    e.J00 = fx / e.tz;
+    e.J02 = -(fx * e.tx) / tz2;
+    e.J11 = fy / e.tz;
+    e.J12 = -(fy * e.ty) / tz2;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        e.T0[j] = e.J00 * view[j * 4 + 0] + e.J02 * view[j * 4 + 2];
+        e.T1[j] = e.J11 * view[j * 4 + 1] + e.J12 * view[j * 4 + 2];
+    }
+}
+
+__device__ __forceinline__ void ewa_uv(const Ewa& e, const float* c, float* u, float* v)
+{
+    u[0] = c[0] * e.T0[0] + c[1] * e.T0[1] + c[2] * e.T0[2];
+    u[1] = c[1] * e.T0[0] + c[3] * e.T0[1] + c[4] * e.T0[2];
+    u[2] = c[2] * e.T0[0] + c[4] * e.T0[1] + c[5] * e.T0[2];
+    v[0] = c[0] * e.T1[0] + c[1] * e.T1[1] + c[2] * e.T1[2];
+    v[1] = c[1] * e.T1[0] + c[3] * e.T1[1] + c[4] * e.T1[2];
+    v[2] = c[2] * e.T1[0] + c[4] * e.T1[1] + c[5] * e.T1[2];
+}
+
+__device__ __forceinline__ void ewa_cov2D(const Ewa& e, const float* c, float& a, float& b, float& cc)
+{
+    float u[3], v[3];
+    ewa_uv(e, c, u, v);
+    a = e.T0[0] * u[0] + e.T0[1] * u[1] + e.T0[2] * u[2] + 0.3f;
+    b = e.T0[0] * v[0] + e.T0[1] * v[1] + e.T0[2] * v[2];
+    cc = e.T1[0] * v[0] + e.T1[1] * v[1] + e.T1[2] * v[2] + 0.3f;
+}
+
+__constant__ static const float SH_C0 = 0.28209479177387814f;
+__constant__ static const float SH_C1 = 0.4886025119029199f;
+#define LSR_C2_0 1.0925484305920792f
+#define LSR_C2_1 (-1.0925484305920792f)
+#define LSR_C2_2 0.31539156525252005f
+#define LSR_C2_3 (-1.0925484305920792f)
+#define LSR_C2_4 0.5462742152960396f
+#define LSR_C3_0 (-0.5900435899266435f)
+#define LSR_C3_1 2.890611442640554f
+#define LSR_C3_2 (-0.4570457994644658f)
+#define LSR_C3_3 0.3731763325901154f
+#define LSR_C3_4 (-0.4570457994644658f)
+#define LSR_C3_5 1.445305721320277f
+#define LSR_C3_6 (-0.5900435899266435f)
+
+// SH -> RGB (+0.5, pre-clamp), term order of utils/sh_utils.py:57-112.
+// sh points at the Gaussian's (M,3) block.
+__device__ __forceinline__ float sh_channel(int deg, const float* sh, int ch, float x, float y, float z)
+{
+#define S(k) sh[(k)*3 + ch]
+    float r = 0.28209479177387814f * S(0);
+    if (deg > 0) {
+        const float c1 = 0.4886025119029199f;
+        r = r - c1 * y * S(1) + c1 * z * S(2) - c1 * x * S(3);
+        if (deg > 1) {
+            float xx = x * x, yy = y * y, zz = z * z;
+            float xy = x * y, yz = y * z, xz = x * z;
+            r = r + LSR_C2_0 * xy * S(4) + LSR_C2_1 * yz * S(5) + LSR_C2_2 * (2.0f * zz - xx - yy) * S(6) +
+                LSR_C2_3 * xz * S(7) + LSR_C2_4 * (xx - yy) * S(8);
+            if (deg > 2) {
+                r = r + LSR_C3_0 * y * (3.0f * xx - yy) * S(9) + LSR_C3_1 * xy * z * S(10) +
+                    LSR_C3_2 * y * (4.0f * zz - xx - yy) * S(11) +
+                    LSR_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * S(12) +
+                    LSR_C3_4 * x * (4.0f * zz - xx - yy) * S(13) + LSR_C3_5 * z * (xx - yy) * S(14) +
+                    LSR_C3_6 * x * (xx - 3.0f * yy) * S(15);
+            }
+        }
+    }
+#undef S
+    return r + 0.5f;
+}
+
+__device__ __forceinline__ void sh_dir(float mx, float my, float mz, const float* campos, float* dir, float* dor)
+{
+    dor[0] = mx - campos[0];
+    dor[1] = my - campos[1];
+    dor[2] = mz - campos[2];
+    float len = sqrtf(dor[0] * dor[0] + dor[1] * dor[1] + dor[2] * dor[2]);
+    dir[0] = dor[0] / len;
+    dir[1] = dor[1] / len;
+    dir[2] = dor[2] / len;
+}
+
+// The per-pair Gaussian exponent (A.3), shared by forward and backward.
+__device__ __forceinline__ float splat_power(float ca, float cb, float cc, float dx, float dy)
+{
+    return fmaf(-0.5f, fmaf(ca * dx, dx, (cc * dy) * dy), -((cb * dx) * dy));
+}
+
+// Conservative exponent cut: for power < cut, opacity*exp(power) < 1/255 is
+// certain, so the pair is skipped without evaluating exp.  Never changes a
+// result (the margin 0.02 dwarfs exp/log rounding); only saves work.
+__device__ __forceinline__ float power_cut(float o)
+{
+    if (!(o * 255.0f > 1.0f)) return (o == o) ? -0.02f : -INFINITY;
+    return -__logf(255.0f * o) - 0.02f;
+}
+
+// ------------------------------------------------------------- layouts --
+// Geometry workspace (per Gaussian, SoA, every section 256-B aligned).
+struct GeomLayout {
+    size_t splatA, splatB, rgb, depth, tiles, offsets, clamped, scan_part, total;
+};
+
+__host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+__host__ __device__ inline GeomLayout geom_layout(size_t N)
+{
+    GeomLayout L;
+    size_t o = 0;
+    L.splatA = o;   o += align256(N * 16);  // float4 {x, y, conic.a, conic.b}
+    L.splatB = o;   o += align256(N * 16);  // float4 {conic.c, opacity, cut, depth}
+    L.rgb = o;      o += align256(N * 12);
+    L.depth = o;    o += align256(N * 4);
+    L.tiles = o;    o += align256(N * 4);
+    L.offsets = o;  o += align256(N * 4);   // inclusive scan of tiles
+    L.clamped = o;  o += align256(N * 4);   // 3-bit mask
+    L.scan_part = o; o += align256(((N + 4095) / 4096 + 1) * 8);
+    L.total = o;
+    return L;
+}
+
+// Image workspace (per pixel + per tile).
+struct ImageLayout {
+    size_t final_T, n_contrib, tile_cnt, tile_start, tile_part, total;
+};
+
+__host__ __device__ inline ImageLayout image_layout(size_t P, size_t T)
+{
+    ImageLayout L;
+    size_t o = 0;
+    L.final_T = o;    o += align256(P * 4);
+    L.n_contrib = o;  o += align256(P * 4);
+    L.tile_cnt = o;   o += align256(T * 4);
+    L.tile_start = o; o += align256((T + 1) * 4);   // exclusive scan, [T] = num_rendered
+    L.tile_part = o;  o += align256(((T + 4095) / 4096 + 1) * 8);
+    L.total = o;
+    return L;
+}
+
+// Binning workspace (per instance).
+struct BinLayout {
+    size_t rank, keys, point_list, total;
+};
+
+__host__ __device__ inline BinLayout bin_layout(size_t M)
+{
+    BinLayout L;
+    size_t o = 0;
+    L.rank = o;       o += align256(M * 4);
+    L.keys = o;       o += align256(M * 8);
+    L.point_list = o; o += align256(M * 4);
+    L.total = o;
+    return L;
+}
+
+// XCD-aware bijective block remap: blocks b, b+8, b+16 ... (one XCD under
+// round-robin dispatch) receive consecutive work items, so neighbouring tiles
+// share an L2.  Speed only; correctness never depends on placement.
+__device__ __forceinline__ int xcd_remap(int b, int nb)
+{
+    const int q = nb / 8, r = nb % 8;
+    const int xcd = b % 8, k = b / 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+}
+
+}  // namespace lsr

@@ -1,0 +1,70 @@
+// lsr_internal.h — launcher declarations shared by the kernel translation
+// units and the C-ABI driver (lsr_api.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/lsr.h"
+#include "lsr_device.h"
+
+namespace lsr {
+
+struct Cam {
+    int W, H, gx, gy;
+    float tanfovx, tanfovy, fx, fy, scale_modifier;
+    const float* view;
+    const float* proj;
+    const float* campos;
+    const float* bg;
+    int sh_degree;
+};
+
+// preprocess.hip
+hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, int32_t* radii, hipStream_t st);
+hipError_t launch_preprocess_bwd(const Cam& c, const lsr_inputs& in, const uint8_t* geom, const int32_t* radii,
+                                 const float* grad_acc, int VP, const lsr_bwd_out& out, hipStream_t st);
+hipError_t launch_mark_visible(int P, const float* means, const float* view, uint8_t* present, hipStream_t st);
+
+// binning.hip
+// Inclusive scan of n uint32 values (in-place allowed); writes the 64-bit total
+// to part[0] (part must hold scan_partials(n) uint64 entries).
+size_t scan_partials(size_t n);
+hipError_t launch_scan_u32(const uint32_t* in, uint32_t* out, uint64_t* part, size_t n, bool exclusive, hipStream_t st);
+hipError_t launch_duplicate(const Cam& c, int P, const uint8_t* geom, const int32_t* radii, uint32_t* tile_cnt,
+                            uint32_t* rank, hipStream_t st);
+hipError_t launch_scatter(const Cam& c, int P, const uint8_t* geom, const int32_t* radii, const uint32_t* tile_start,
+                          const uint32_t* rank, uint64_t* keys, hipStream_t st);
+hipError_t launch_tile_sort(int T, const uint32_t* tile_start, uint64_t* keys, uint32_t* point_list, hipStream_t st);
+
+// render.hip
+struct RenderArgs {
+    Cam cam;
+    int P;
+    const float4* splatA;
+    const float4* splatB;
+    const float* rgb;            // (P,3): preprocess output or colors_precomp
+    const float* lang;           // (P,D) dense or NULL
+    int D;                       // dense language channels rendered (0 if off)
+    const float* qw;             // quick weights (P,K) or NULL
+    const void* qi;              // quick indices (P,K)
+    int qidx_dtype, K, Dq;
+    const uint32_t* point_list;
+    const uint32_t* tile_start;  // T+1
+    float* final_T;
+    uint32_t* n_contrib;
+    float* out_color;
+    float* out_lang;
+};
+hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st);
+
+struct RenderBwdArgs {
+    RenderArgs f;
+    const float* dout_color;
+    const float* dout_lang;
+    float* grad_acc;   // (P, VP) atomically accumulated
+    int VP;
+};
+int grad_row_width(int D);   // VP for a dense language dim
+hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t st);
+int lang_set_for(int D);     // compiled channel set >= D, or -1
+
+}  // namespace lsr

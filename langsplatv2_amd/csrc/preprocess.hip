@@ -1,0 +1,360 @@
+// preprocess.hip — per-Gaussian projection (A.1) and its chain rule (A.4).
+//
+// One thread per Gaussian, 256-thread blocks.  HBM-bound stream over N:
+// reads means/scales/rotations/opacity/SH (44 + 4*S B), writes the splat
+// records consumed by binning and render (2 x float4), rgb, depth, tile
+// counts.  Operation sequence == oracle/lsr_oracle.c lso_preprocess.
+#include "lsr_internal.h"
+
+namespace lsr {
+
+template <bool SH16>
+__global__ void __launch_bounds__(256) k_preprocess(Cam c, lsr_inputs in, uint8_t* __restrict__ geom,
+                                                    int32_t* __restrict__ radii)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int N = in.P;
+    if (i >= N) return;
+    const GeomLayout L = geom_layout(N);
+    float4* splatA = (float4*)(geom + L.splatA);
+    float4* splatB = (float4*)(geom + L.splatB);
+    float* rgbo = (float*)(geom + L.rgb);
+    float* depth = (float*)(geom + L.depth);
+    uint32_t* tiles = (uint32_t*)(geom + L.tiles);
+    uint32_t* clampm = (uint32_t*)(geom + L.clamped);
+
+    radii[i] = 0;
+    tiles[i] = 0;
+    clampm[i] = 0;
+    depth[i] = 0.f;
+    splatA[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    splatB[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (!in.colors_precomp) {
+        rgbo[3 * i + 0] = 0.f;
+        rgbo[3 * i + 1] = 0.f;
+        rgbo[3 * i + 2] = 0.f;
+    }
+
+    const float mx = in.means3D[3 * i], my = in.means3D[3 * i + 1], mz = in.means3D[3 * i + 2];
+    const float3 pv = xform43(c.view, mx, my, mz);
+    if (pv.z <= 0.2f) return;
+    const float4 ph = xform44(c.proj, mx, my, mz);
+    const float pw = 1.0f / (ph.w + 0.0000001f);
+    const float ppx = ph.x * pw, ppy = ph.y * pw;
+
+    float cov[6];
+    if (in.cov3D_precomp) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) cov[k] = in.cov3D_precomp[6 * i + k];
+    } else {
+        const float4 q = reinterpret_cast<const float4*>(in.rotations)[i];
+        compute_cov3D(in.scales[3 * i], in.scales[3 * i + 1], in.scales[3 * i + 2], c.scale_modifier, q, cov);
+    }
+    Ewa e;
+    ewa_setup(c.view, pv, c.fx, c.fy, c.tanfovx, c.tanfovy, e);
+    float a, b, cc;
+    ewa_cov2D(e, cov, a, b, cc);
+    const float det = a * cc - b * b;
+    if (det == 0.0f) return;
+    const float det_inv = 1.f / det;
+    const float mid = 0.5f * (a + cc);
+    const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float radius = ceilf(3.f * sqrtf(l1));
+    const int r = f2i(radius);
+    const float px = ndc2pix(ppx, c.W), py = ndc2pix(ppy, c.H);
+    int x0, y0, x1, y1;
+    get_rect(px, py, r, c.gx, c.gy, x0, y0, x1, y1);
+    const int area = (x1 - x0) * (y1 - y0);
+    if (area == 0 || r <= 0) return;
+
+    if (!in.colors_precomp) {
+        float dir[3], dor[3];
+        sh_dir(mx, my, mz, c.campos, dir, dor);
+        float out[3];
+        if (SH16) {
+            float sh[48];
+            const float4* src = reinterpret_cast<const float4*>(in.shs) + (size_t)i * 12;
+#pragma unroll
+            for (int k = 0; k < 12; k++) {
+                float4 v = src[k];
+                sh[4 * k] = v.x; sh[4 * k + 1] = v.y; sh[4 * k + 2] = v.z; sh[4 * k + 3] = v.w;
+            }
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) out[ch] = sh_channel(c.sh_degree, sh, ch, dir[0], dir[1], dir[2]);
+        } else {
+            const float* sh = in.shs + (size_t)i * in.max_coeffs * 3;
+            for (int ch = 0; ch < 3; ch++) out[ch] = sh_channel(c.sh_degree, sh, ch, dir[0], dir[1], dir[2]);
+        }
+        uint32_t m = 0;
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) {
+            m |= (out[ch] < 0.f ? 1u : 0u) << ch;
+            rgbo[3 * i + ch] = fmaxf(out[ch], 0.f);
+        }
+        clampm[i] = m;
+    }
+    const float o = in.opacities[i];
+    depth[i] = pv.z;
+    radii[i] = r;
+    splatA[i] = make_float4(px, py, cc * det_inv, -b * det_inv);
+    splatB[i] = make_float4(a * det_inv, o, power_cut(o), pv.z);
+    tiles[i] = (uint32_t)area;
+}
+
+hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, int32_t* radii, hipStream_t st)
+{
+    if (in.P == 0) return hipSuccess;
+    dim3 grid((in.P + 255) / 256), block(256);
+    const bool sh16 = in.shs && in.max_coeffs == 16 && ((uintptr_t)in.shs % 16 == 0);
+    if (sh16)
+        k_preprocess<true><<<grid, block, 0, st>>>(c, in, geom, radii);
+    else
+        k_preprocess<false><<<grid, block, 0, st>>>(c, in, geom, radii);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Backward: chain rule through A.1.  grad_acc row layout (VP floats):
+//   [0,1] dL/dmean2D (NDC)  [2,3,4] dL/dconic (a,b,c)  [5] dL/dopacity
+//   [6,7,8] dL/dcolor       [9, 9+D) dL/dlanguage
+__global__ void __launch_bounds__(256) k_preprocess_bwd(Cam c, lsr_inputs in, const uint8_t* __restrict__ geom,
+                                                        const int32_t* __restrict__ radii,
+                                                        const float* __restrict__ gacc, int VP, lsr_bwd_out out)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int N = in.P;
+    if (i >= N) return;
+    const GeomLayout L = geom_layout(N);
+    const uint32_t clampm = ((const uint32_t*)(geom + L.clamped))[i];
+    const float* g = gacc + (size_t)i * VP;
+    const bool vis = radii[i] > 0;
+    const int M = in.max_coeffs;
+    const int D = in.lang_dim;
+
+    if (out.dL_dmeans2D) {
+        out.dL_dmeans2D[3 * i + 0] = vis ? g[0] : 0.f;
+        out.dL_dmeans2D[3 * i + 1] = vis ? g[1] : 0.f;
+        out.dL_dmeans2D[3 * i + 2] = 0.f;
+    }
+    if (out.dL_dopacity) out.dL_dopacity[i] = vis ? g[5] : 0.f;
+    if (out.dL_dlang)
+        for (int k = 0; k < D; k++) out.dL_dlang[(size_t)i * D + k] = vis ? g[9 + k] : 0.f;
+    if (out.dL_dcolors)
+        for (int k = 0; k < 3; k++) out.dL_dcolors[3 * i + k] = vis ? g[6 + k] : 0.f;
+
+    float dm[3] = {0.f, 0.f, 0.f};
+    const bool want_sh = out.dL_dsh && in.shs && !in.colors_precomp;
+    if (!vis) {
+        if (out.dL_dmeans3D) { out.dL_dmeans3D[3 * i] = 0.f; out.dL_dmeans3D[3 * i + 1] = 0.f; out.dL_dmeans3D[3 * i + 2] = 0.f; }
+        if (want_sh) for (int k = 0; k < M * 3; k++) out.dL_dsh[(size_t)i * M * 3 + k] = 0.f;
+        if (out.dL_dscales) for (int k = 0; k < 3; k++) out.dL_dscales[3 * i + k] = 0.f;
+        if (out.dL_drotations) for (int k = 0; k < 4; k++) out.dL_drotations[4 * i + k] = 0.f;
+        if (out.dL_dcov3D) for (int k = 0; k < 6; k++) out.dL_dcov3D[6 * i + k] = 0.f;
+        return;
+    }
+    const float* V = c.view;
+    const float* P = c.proj;
+    const float mx = in.means3D[3 * i], my = in.means3D[3 * i + 1], mz = in.means3D[3 * i + 2];
+    float cov[6];
+    float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
+    float sc0 = 0.f, sc1 = 0.f, sc2 = 0.f;
+    if (in.cov3D_precomp) {
+        for (int k = 0; k < 6; k++) cov[k] = in.cov3D_precomp[6 * i + k];
+    } else {
+        q = reinterpret_cast<const float4*>(in.rotations)[i];
+        sc0 = in.scales[3 * i]; sc1 = in.scales[3 * i + 1]; sc2 = in.scales[3 * i + 2];
+        compute_cov3D(sc0, sc1, sc2, c.scale_modifier, q, cov);
+    }
+    const float3 pv = xform43(V, mx, my, mz);
+    Ewa e;
+    ewa_setup(V, pv, c.fx, c.fy, c.tanfovx, c.tanfovy, e);
+    float a, b, cc;
+    ewa_cov2D(e, cov, a, b, cc);
+    const float dA = g[2], dB = g[3], dC = g[4];
+    const float det = a * cc - b * b;
+    const float d2inv = 1.0f / ((det * det) + 0.0000001f);
+    float dLa = 0.f, dLb = 0.f, dLc = 0.f;
+    float dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (d2inv != 0.f) {
+        dLa = d2inv * (-cc * cc * dA + b * cc * dB - b * b * dC);
+        dLb = d2inv * (2.f * b * cc * dA - (det + 2.f * b * b) * dB + 2.f * a * b * dC);
+        dLc = d2inv * (-b * b * dA + a * b * dB - a * a * dC);
+        const float* T0 = e.T0;
+        const float* T1 = e.T1;
+        dcov[0] = T0[0] * T0[0] * dLa + T0[0] * T1[0] * dLb + T1[0] * T1[0] * dLc;
+        dcov[3] = T0[1] * T0[1] * dLa + T0[1] * T1[1] * dLb + T1[1] * T1[1] * dLc;
+        dcov[5] = T0[2] * T0[2] * dLa + T0[2] * T1[2] * dLb + T1[2] * T1[2] * dLc;
+        dcov[1] = 2.f * T0[0] * T0[1] * dLa + (T0[0] * T1[1] + T0[1] * T1[0]) * dLb + 2.f * T1[0] * T1[1] * dLc;
+        dcov[2] = 2.f * T0[0] * T0[2] * dLa + (T0[0] * T1[2] + T0[2] * T1[0]) * dLb + 2.f * T1[0] * T1[2] * dLc;
+        dcov[4] = 2.f * T0[1] * T0[2] * dLa + (T0[1] * T1[2] + T0[2] * T1[1]) * dLb + 2.f * T1[1] * T1[2] * dLc;
+    }
+    float u[3], v[3];
+    ewa_uv(e, cov, u, v);
+    float dT0[3], dT1[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        dT0[k] = 2.f * dLa * u[k] + dLb * v[k];
+        dT1[k] = 2.f * dLc * v[k] + dLb * u[k];
+    }
+    const float dJ00 = dT0[0] * V[0] + dT0[1] * V[4] + dT0[2] * V[8];
+    const float dJ02 = dT0[0] * V[2] + dT0[1] * V[6] + dT0[2] * V[10];
+    const float dJ11 = dT1[0] * V[1] + dT1[1] * V[5] + dT1[2] * V[9];
+    const float dJ12 = dT1[0] * V[2] + dT1[1] * V[6] + dT1[2] * V[10];
+    const float tz = 1.f / e.tz, tz2 = tz * tz, tz3 = tz2 * tz;
+    const float dtx = e.xclamp ? 0.f : -c.fx * tz2 * dJ02;
+    const float dty = e.yclamp ? 0.f : -c.fy * tz2 * dJ12;
+    const float dtz = -c.fx * tz2 * dJ00 - c.fy * tz2 * dJ11 + (2.f * c.fx * e.tx) * tz3 * dJ02 +
+                      (2.f * c.fy * e.ty) * tz3 * dJ12;
+    dm[0] = V[0] * dtx + V[1] * dty + V[2] * dtz;
+    dm[1] = V[4] * dtx + V[5] * dty + V[6] * dtz;
+    dm[2] = V[8] * dtx + V[9] * dty + V[10] * dtz;
+
+    const float4 ph = xform44(P, mx, my, mz);
+    const float mw = 1.0f / (ph.w + 0.0000001f);
+    const float mul1 = ph.x * mw * mw, mul2 = ph.y * mw * mw;
+    const float g2x = g[0], g2y = g[1];
+    dm[0] += (P[0] * mw - P[3] * mul1) * g2x + (P[1] * mw - P[3] * mul2) * g2y;
+    dm[1] += (P[4] * mw - P[7] * mul1) * g2x + (P[5] * mw - P[7] * mul2) * g2y;
+    dm[2] += (P[8] * mw - P[11] * mul1) * g2x + (P[9] * mw - P[11] * mul2) * g2y;
+
+    if (in.shs && !in.colors_precomp) {
+        float dRGB[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) dRGB[k] = ((clampm >> k) & 1u) ? 0.f : g[6 + k];
+        float dir[3], dor[3];
+        sh_dir(mx, my, mz, c.campos, dir, dor);
+        const float x = dir[0], y = dir[1], z = dir[2];
+        const float* sh = in.shs + (size_t)i * M * 3;
+        const int deg = c.sh_degree;
+        float ddx[3] = {0.f, 0.f, 0.f}, ddy[3] = {0.f, 0.f, 0.f}, ddz[3] = {0.f, 0.f, 0.f};
+        float* ds = out.dL_dsh ? out.dL_dsh + (size_t)i * M * 3 : nullptr;
+        for (int k = 0; k < M * 3; k++)
+            if (ds) ds[k] = 0.f;
+        for (int ch = 0; ch < 3; ch++) {
+#define S(k) sh[(k)*3 + ch]
+#define DS(k, val) if (ds) ds[(k)*3 + ch] = (val)
+            const float gch = dRGB[ch];
+            DS(0, 0.28209479177387814f * gch);
+            if (deg > 0) {
+                const float c1 = 0.4886025119029199f;
+                DS(1, -c1 * y * gch);
+                DS(2, c1 * z * gch);
+                DS(3, -c1 * x * gch);
+                ddx[ch] = -c1 * S(3);
+                ddy[ch] = -c1 * S(1);
+                ddz[ch] = c1 * S(2);
+                if (deg > 1) {
+                    const float xx = x * x, yy = y * y, zz = z * z;
+                    const float xy = x * y, yz = y * z, xz = x * z;
+                    DS(4, LSR_C2_0 * xy * gch);
+                    DS(5, LSR_C2_1 * yz * gch);
+                    DS(6, LSR_C2_2 * (2.f * zz - xx - yy) * gch);
+                    DS(7, LSR_C2_3 * xz * gch);
+                    DS(8, LSR_C2_4 * (xx - yy) * gch);
+                    ddx[ch] += LSR_C2_0 * y * S(4) + LSR_C2_2 * 2.f * -x * S(6) + LSR_C2_3 * z * S(7) + LSR_C2_4 * 2.f * x * S(8);
+                    ddy[ch] += LSR_C2_0 * x * S(4) + LSR_C2_1 * z * S(5) + LSR_C2_2 * 2.f * -y * S(6) + LSR_C2_4 * 2.f * -y * S(8);
+                    ddz[ch] += LSR_C2_1 * y * S(5) + LSR_C2_2 * 2.f * 2.f * z * S(6) + LSR_C2_3 * x * S(7);
+                    if (deg > 2) {
+                        DS(9, LSR_C3_0 * y * (3.f * xx - yy) * gch);
+                        DS(10, LSR_C3_1 * xy * z * gch);
+                        DS(11, LSR_C3_2 * y * (4.f * zz - xx - yy) * gch);
+                        DS(12, LSR_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy) * gch);
+                        DS(13, LSR_C3_4 * x * (4.f * zz - xx - yy) * gch);
+                        DS(14, LSR_C3_5 * z * (xx - yy) * gch);
+                        DS(15, LSR_C3_6 * x * (xx - 3.f * yy) * gch);
+                        ddx[ch] += LSR_C3_0 * S(9) * 3.f * 2.f * xy + LSR_C3_1 * S(10) * yz + LSR_C3_2 * S(11) * -2.f * xy +
+                                   LSR_C3_3 * S(12) * -3.f * 2.f * xz + LSR_C3_4 * S(13) * (-3.f * xx + 4.f * zz - yy) +
+                                   LSR_C3_5 * S(14) * 2.f * xz + LSR_C3_6 * S(15) * 3.f * (xx - yy);
+                        ddy[ch] += LSR_C3_0 * S(9) * 3.f * (xx - yy) + LSR_C3_1 * S(10) * xz +
+                                   LSR_C3_2 * S(11) * (-3.f * yy + 4.f * zz - xx) + LSR_C3_3 * S(12) * -3.f * 2.f * yz +
+                                   LSR_C3_4 * S(13) * -2.f * xy + LSR_C3_5 * S(14) * -2.f * yz +
+                                   LSR_C3_6 * S(15) * -3.f * 2.f * xy;
+                        ddz[ch] += LSR_C3_1 * S(10) * xy + LSR_C3_2 * S(11) * 4.f * 2.f * yz +
+                                   LSR_C3_3 * S(12) * 3.f * (2.f * zz - xx - yy) + LSR_C3_4 * S(13) * 4.f * 2.f * xz +
+                                   LSR_C3_5 * S(14) * (xx - yy);
+                    }
+                }
+            }
+#undef S
+#undef DS
+        }
+        float gd0 = ddx[0] * dRGB[0] + ddx[1] * dRGB[1] + ddx[2] * dRGB[2];
+        float gd1 = ddy[0] * dRGB[0] + ddy[1] * dRGB[1] + ddy[2] * dRGB[2];
+        float gd2 = ddz[0] * dRGB[0] + ddz[1] * dRGB[1] + ddz[2] * dRGB[2];
+        const float sum2 = dor[0] * dor[0] + dor[1] * dor[1] + dor[2] * dor[2];
+        const float inv32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+        dm[0] += ((sum2 - dor[0] * dor[0]) * gd0 - dor[1] * dor[0] * gd1 - dor[2] * dor[0] * gd2) * inv32;
+        dm[1] += (-dor[0] * dor[1] * gd0 + (sum2 - dor[1] * dor[1]) * gd1 - dor[2] * dor[1] * gd2) * inv32;
+        dm[2] += (-dor[0] * dor[2] * gd0 - dor[1] * dor[2] * gd1 + (sum2 - dor[2] * dor[2]) * gd2) * inv32;
+    }
+    if (out.dL_dmeans3D) {
+        out.dL_dmeans3D[3 * i] = dm[0];
+        out.dL_dmeans3D[3 * i + 1] = dm[1];
+        out.dL_dmeans3D[3 * i + 2] = dm[2];
+    }
+    if (in.cov3D_precomp) {
+        if (out.dL_dcov3D)
+            for (int k = 0; k < 6; k++) out.dL_dcov3D[6 * i + k] = dcov[k];
+    } else {
+        if (out.dL_dcov3D)
+            for (int k = 0; k < 6; k++) out.dL_dcov3D[6 * i + k] = 0.f;
+        const float mod = c.scale_modifier;
+        float R[9];
+        quat_to_R(q.x, q.y, q.z, q.w, R);
+        const float sv[3] = {mod * sc0, mod * sc1, mod * sc2};
+        const float Gm[9] = {dcov[0], 0.5f * dcov[1], 0.5f * dcov[2], 0.5f * dcov[1], dcov[3],
+                             0.5f * dcov[4], 0.5f * dcov[2], 0.5f * dcov[4], dcov[5]};
+        float Mm[9], dM[9], dR[9];
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+            for (int k = 0; k < 3; k++) Mm[r * 3 + k] = R[r * 3 + k] * sv[k];
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+            for (int k = 0; k < 3; k++)
+                dM[r * 3 + k] = 2.f * (Gm[r * 3 + 0] * Mm[0 * 3 + k] + Gm[r * 3 + 1] * Mm[1 * 3 + k] + Gm[r * 3 + 2] * Mm[2 * 3 + k]);
+        if (out.dL_dscales)
+#pragma unroll
+            for (int k = 0; k < 3; k++)
+                out.dL_dscales[3 * i + k] = mod * (dM[0 * 3 + k] * R[0 * 3 + k] + dM[1 * 3 + k] * R[1 * 3 + k] + dM[2 * 3 + k] * R[2 * 3 + k]);
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+            for (int k = 0; k < 3; k++) dR[r * 3 + k] = dM[r * 3 + k] * sv[k];
+        const float qr = q.x, qx = q.y, qy = q.z, qz = q.w;
+        if (out.dL_drotations) {
+            out.dL_drotations[4 * i + 0] = 2.f * (-qz * dR[1] + qy * dR[2] + qz * dR[3] - qx * dR[5] - qy * dR[6] + qx * dR[7]);
+            out.dL_drotations[4 * i + 1] = 2.f * (qy * dR[1] + qz * dR[2] + qy * dR[3] - qr * dR[5] + qz * dR[6] + qr * dR[7]) - 4.f * qx * (dR[4] + dR[8]);
+            out.dL_drotations[4 * i + 2] = 2.f * (qx * dR[1] + qr * dR[2] + qx * dR[3] + qz * dR[5] - qr * dR[6] + qz * dR[7]) - 4.f * qy * (dR[0] + dR[8]);
+            out.dL_drotations[4 * i + 3] = 2.f * (-qr * dR[1] + qx * dR[2] + qr * dR[3] + qy * dR[5] + qx * dR[6] + qy * dR[7]) - 4.f * qz * (dR[0] + dR[4]);
+        }
+    }
+}
+
+hipError_t launch_preprocess_bwd(const Cam& c, const lsr_inputs& in, const uint8_t* geom, const int32_t* radii,
+                                 const float* grad_acc, int VP, const lsr_bwd_out& out, hipStream_t st)
+{
+    if (in.P == 0) return hipSuccess;
+    dim3 grid((in.P + 255) / 256), block(256);
+    k_preprocess_bwd<<<grid, block, 0, st>>>(c, in, geom, radii, grad_acc, VP, out);
+    return hipGetLastError();
+}
+
+__global__ void k_mark_visible(int P, const float* __restrict__ means, const float* __restrict__ view,
+                               uint8_t* __restrict__ present)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const float3 pv = xform43(view, means[3 * i], means[3 * i + 1], means[3 * i + 2]);
+    present[i] = pv.z > 0.2f ? 1 : 0;
+}
+
+hipError_t launch_mark_visible(int P, const float* means, const float* view, uint8_t* present, hipStream_t st)
+{
+    if (P == 0) return hipSuccess;
+    k_mark_visible<<<(P + 255) / 256, 256, 0, st>>>(P, means, view, present);
+    return hipGetLastError();
+}
+
+}  // namespace lsr

@@ -1,0 +1,297 @@
+"""Host-side mirror of the reference operator `diff_gaussian_rasterization`.
+
+Surface (what gaussian_renderer/__init__.py:15,37-54,108-119 uses):
+  GaussianRasterizationSettings  NamedTuple, the 14 fields of
+                                 gaussian_renderer/__init__.py:37-52, plus an
+                                 optional trailing `language_feature_dim`
+                                 (quick-path output channels, default 192).
+  GaussianRasterizer(raster_settings)  nn.Module;
+      forward(means3D, means2D, opacities, shs=None, colors_precomp=None,
+              language_feature_precomp=None,
+              language_feature_weights_quick=None,
+              language_feature_indices=None, scales=None, rotations=None,
+              cov3D_precomp=None) -> (color (3,H,W), language map (D,H,W), radii (N,))
+      markVisible(positions) -> bool (N,)
+  rasterize_gaussians(...)       functional form (autograd).
+
+Behaviour kept from the reference:
+  - exactly one of shs / colors_precomp, exactly one of (scales, rotations) /
+    cov3D_precomp, else `Exception` before any launch;
+  - means2D receives dL/d(NDC xy) in [:, :2] (scene/gaussian_model.py:507);
+  - `debug=True`: synchronous per-stage checks in the library, and on failure
+    the inputs are dumped to snapshot_fw.dump / snapshot_bw.dump;
+  - placeholder tensors with numel <= 1 (torch.zeros((1,)),
+    gaussian_renderer/__init__.py:93,97-98,101-103) mean "absent".
+Language modes (gaussian_renderer/__init__.py:87-103):
+  include_feature=True  -> dense (N,D) coefficients, output (D,H,W);
+  quick_render=True     -> sparse (N,K) weights + (N,K) indices (fp32-encoded
+                           integers, or int32/int64), output (Dq,H,W), no grad;
+  neither               -> output (0,H,W).
+All compute runs in liblsr.so (hand-written HIP, gfx950); this module only
+moves pointers.  There is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import NamedTuple, Optional
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+
+class GaussianRasterizationSettings(NamedTuple):
+    image_height: int
+    image_width: int
+    tanfovx: float
+    tanfovy: float
+    bg: torch.Tensor
+    scale_modifier: float
+    viewmatrix: torch.Tensor
+    projmatrix: torch.Tensor
+    sh_degree: int
+    campos: torch.Tensor
+    prefiltered: bool
+    debug: bool
+    include_feature: bool = False
+    quick_render: bool = False
+    language_feature_dim: Optional[int] = None
+
+
+def _present(t: Optional[torch.Tensor]) -> bool:
+    """False for None, empty tensors and the reference's 1-element placeholders
+    (torch.zeros((1,)), gaussian_renderer/__init__.py:93,97-98,101-103)."""
+    return t is not None and t.numel() > 0 and not (t.dim() <= 1 and t.numel() <= 1)
+
+
+def _f32(t: torch.Tensor, name: str) -> torch.Tensor:
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must be a ROCm device tensor (got {t.device}); "
+                           "the rasterizer has no CPU path")
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name} must be float32 (got {t.dtype})")
+    return t.contiguous()
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+class _Alloc:
+    """Workspace allocator handed to the C ABI: torch's caching allocator."""
+
+    def __init__(self, device):
+        self.device = device
+        self.bufs = {}
+
+        def cb(_ctx, nbytes, which):
+            t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=self.device)
+            self.bufs[int(which)] = t
+            return t.data_ptr()
+
+        self.fn = _lib.ALLOC_FN(cb)
+
+
+def _settings_struct(rs: GaussianRasterizationSettings, dev) -> tuple:
+    bg = _f32(rs.bg, "bg")
+    view = _f32(rs.viewmatrix, "viewmatrix")
+    proj = _f32(rs.projmatrix, "projmatrix")
+    campos = _f32(rs.campos, "campos")
+    qdim = rs.language_feature_dim if (len(rs) > 14 and rs.language_feature_dim) else 0
+    s = _lib.Settings(int(rs.image_height), int(rs.image_width), float(rs.tanfovx), float(rs.tanfovy),
+                      bg.data_ptr(), float(rs.scale_modifier), view.data_ptr(), proj.data_ptr(),
+                      int(rs.sh_degree), campos.data_ptr(), int(bool(rs.prefiltered)), int(bool(rs.debug)),
+                      int(bool(rs.include_feature)), int(bool(rs.quick_render)), int(qdim))
+    return s, (bg, view, proj, campos)
+
+
+def _index_dtype(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return _lib.LSR_INDEX_F32
+    if t.dtype == torch.int32:
+        return _lib.LSR_INDEX_I32
+    if t.dtype == torch.int64:
+        return _lib.LSR_INDEX_I64
+    raise RuntimeError(f"language_feature_indices dtype {t.dtype} unsupported (float32/int32/int64)")
+
+
+def _stream(dev) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _dump(path, tensors):
+    try:
+        torch.save([t.detach().cpu() if isinstance(t, torch.Tensor) else t for t in tensors], path)
+        print(f"\nAn error occured in the rasterizer. Please forward {path} for debugging.")
+    except Exception:  # pragma: no cover - best effort
+        pass
+
+
+def _run_forward(means3D, sh, colors_precomp, language_feature_precomp, language_feature_weights_quick,
+                 language_feature_indices, opacities, scales, rotations, cov3Ds_precomp, rs):
+    """One lsr_forward call.  Returns (color, lang, radii, num_rendered, bufs, saved) where
+    bufs = {LSR_BUF_*: uint8 workspace tensor} and saved = contiguous inputs."""
+    dev = means3D.device
+    lib = _lib.load()
+    N = means3D.shape[0]
+    means3D_c = _f32(means3D, "means3D")
+    opac_c = _f32(opacities, "opacities")
+    sh_c = _f32(sh, "shs") if _present(sh) else None
+    col_c = _f32(colors_precomp, "colors_precomp") if _present(colors_precomp) else None
+    sc_c = _f32(scales, "scales") if _present(scales) else None
+    rot_c = _f32(rotations, "rotations") if _present(rotations) else None
+    cov_c = _f32(cov3Ds_precomp, "cov3D_precomp") if _present(cov3Ds_precomp) else None
+    quick = bool(rs.quick_render)
+    dense = bool(rs.include_feature) and not quick
+    lang_c = _f32(language_feature_precomp, "language_feature_precomp") \
+        if (dense and _present(language_feature_precomp)) else None
+    qw_c = qi_c = None
+    if quick:
+        qw_c = _f32(language_feature_weights_quick, "language_feature_weights_quick")
+        qi_c = language_feature_indices.contiguous()
+        if not qi_c.is_cuda:
+            raise RuntimeError("language_feature_indices must be a ROCm device tensor")
+    M = sh_c.shape[1] if sh_c is not None and sh_c.dim() == 3 else (
+        sh_c.shape[1] // 3 if sh_c is not None else 0)
+    D = lang_c.shape[1] if lang_c is not None else 0
+    K = qw_c.shape[1] if qw_c is not None else 0
+    Dq = (rs.language_feature_dim if (len(rs) > 14 and rs.language_feature_dim) else 192) if quick else 0
+    Dout = Dq if quick else D
+    H, W = int(rs.image_height), int(rs.image_width)
+
+    s, keep = _settings_struct(rs, dev)
+    ins = _lib.Inputs(N, M, D, K, _index_dtype(qi_c) if qi_c is not None else 0,
+                      means3D_c.data_ptr(), _ptr(sh_c), _ptr(col_c), opac_c.data_ptr(), _ptr(sc_c), _ptr(rot_c),
+                      _ptr(cov_c), _ptr(lang_c), _ptr(qw_c), _ptr(qi_c))
+    color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
+    lang_out = torch.empty((Dout, H, W), dtype=torch.float32, device=dev)
+    radii = torch.empty((N,), dtype=torch.int32, device=dev)
+    out = _lib.FwdOut(color.data_ptr(), lang_out.data_ptr() if Dout else None, radii.data_ptr())
+    alloc = _Alloc(dev)
+    rc = lib.lsr_forward(ctypes.byref(s), ctypes.byref(ins), ctypes.byref(out), alloc.fn, None, _stream(dev))
+    if rc != _lib.LSR_OK:
+        if rs.debug:
+            _dump("snapshot_fw.dump", [means3D, sh, colors_precomp, opacities, scales, rotations,
+                                       cov3Ds_precomp, language_feature_precomp, rs.viewmatrix, rs.projmatrix])
+        _lib.check(rc, "rasterize_gaussians (forward)")
+    saved = (means3D_c, opac_c, sh_c, col_c, sc_c, rot_c, cov_c, lang_c)
+    return color, lang_out, radii, int(out.num_rendered), alloc.bufs, saved, (N, M, D, K)
+
+
+class _RasterizeGaussians(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means3D, means2D, sh, colors_precomp, language_feature_precomp,
+                language_feature_weights_quick, language_feature_indices, opacities, scales, rotations,
+                cov3Ds_precomp, raster_settings):
+        color, lang_out, radii, num_rendered, bufs, saved, dims = _run_forward(
+            means3D, sh, colors_precomp, language_feature_precomp, language_feature_weights_quick,
+            language_feature_indices, opacities, scales, rotations, cov3Ds_precomp, raster_settings)
+        ctx.raster_settings = raster_settings
+        ctx.num_rendered = num_rendered
+        ctx.dims = dims
+        ctx.save_for_backward(*saved, radii, bufs[_lib.LSR_BUF_GEOM], bufs[_lib.LSR_BUF_BINNING],
+                              bufs[_lib.LSR_BUF_IMAGE])
+        ctx.mark_non_differentiable(radii)
+        return color, lang_out, radii
+
+    @staticmethod
+    def backward(ctx, grad_color, grad_lang, _grad_radii):
+        rs = ctx.raster_settings
+        (means3D, opac, sh, col, sc, rot, cov, lang, radii, geom, binning, image) = ctx.saved_tensors
+        N, M, D, K = ctx.dims
+        dev = means3D.device
+        lib = _lib.load()
+        need = ctx.needs_input_grad
+        # inputs: 0 means3D 1 means2D 2 sh 3 colors 4 lang 5 qw 6 qi 7 opac 8 scales 9 rot 10 cov 11 settings
+        grad_color = grad_color.contiguous() if grad_color is not None else torch.zeros(
+            (3, rs.image_height, rs.image_width), device=dev)
+        gl = None
+        if lang is not None:
+            gl = grad_lang.contiguous() if grad_lang is not None else torch.zeros(
+                (D, rs.image_height, rs.image_width), device=dev)
+        s, keep = _settings_struct(rs, dev)
+        ins = _lib.Inputs(N, M, D, 0, 0, means3D.data_ptr(), _ptr(sh), _ptr(col), opac.data_ptr(), _ptr(sc),
+                          _ptr(rot), _ptr(cov), _ptr(lang), None, None)
+        # quick-path language channels are not differentiated: run the backward in dense/RGB mode
+        s.quick_render = 0
+        bin_ = _lib.BwdIn(geom.data_ptr(), binning.data_ptr(), image.data_ptr(), ctx.num_rendered, radii.data_ptr(),
+                          grad_color.data_ptr(), _ptr(gl))
+
+        def mk(shape, flag):
+            return torch.empty(shape, dtype=torch.float32, device=dev) if flag else None
+
+        g_means2D = torch.empty((N, 3), dtype=torch.float32, device=dev)
+        g_means3D = mk((N, 3), True)
+        g_sh = mk(tuple(sh.shape), need[2]) if sh is not None else None
+        g_col = mk((N, 3), need[3]) if col is not None else None
+        g_lang = mk((N, D), need[4]) if lang is not None else None
+        g_opac = mk((N, 1), True)
+        g_sc = mk((N, 3), need[8]) if sc is not None else None
+        g_rot = mk((N, 4), need[9]) if rot is not None else None
+        g_cov = mk((N, 6), need[10]) if cov is not None else None
+        bout = _lib.BwdOut(_ptr(g_means2D), _ptr(g_col), _ptr(g_lang), _ptr(g_opac), _ptr(g_means3D), _ptr(g_cov),
+                           _ptr(g_sh), _ptr(g_sc), _ptr(g_rot))
+        alloc = _Alloc(dev)
+        rc = lib.lsr_backward(ctypes.byref(s), ctypes.byref(ins), ctypes.byref(bin_), ctypes.byref(bout), alloc.fn,
+                              None, _stream(dev))
+        if rc != _lib.LSR_OK:
+            if rs.debug:
+                _dump("snapshot_bw.dump", [grad_color, gl, means3D, sh, col, opac, sc, rot, cov, lang])
+            _lib.check(rc, "rasterize_gaussians_backward")
+        return (g_means3D if need[0] else None, g_means2D if need[1] else None, g_sh, g_col, g_lang, None, None,
+                g_opac if need[7] else None, g_sc, g_rot, g_cov, None)
+
+
+def rasterize_gaussians(means3D, means2D, sh, colors_precomp, language_feature_precomp,
+                        language_feature_weights_quick, language_feature_indices, opacities, scales, rotations,
+                        cov3Ds_precomp, raster_settings):
+    return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, language_feature_precomp,
+                                     language_feature_weights_quick, language_feature_indices, opacities, scales,
+                                     rotations, cov3Ds_precomp, raster_settings)
+
+
+class GaussianRasterizer(nn.Module):
+    def __init__(self, raster_settings: GaussianRasterizationSettings):
+        super().__init__()
+        self.raster_settings = raster_settings
+
+    def markVisible(self, positions: torch.Tensor) -> torch.Tensor:
+        with torch.no_grad():
+            rs = self.raster_settings
+            pos = _f32(positions, "positions")
+            view = _f32(rs.viewmatrix, "viewmatrix")
+            proj = _f32(rs.projmatrix, "projmatrix")
+            out = torch.empty((pos.shape[0],), dtype=torch.bool, device=pos.device)
+            rc = _lib.load().lsr_mark_visible(int(pos.shape[0]), pos.data_ptr(), view.data_ptr(), proj.data_ptr(),
+                                              out.data_ptr(), _stream(pos.device))
+            _lib.check(rc, "mark_visible")
+        return out
+
+    def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, language_feature_precomp=None,
+                language_feature_weights_quick=None, language_feature_indices=None, scales=None, rotations=None,
+                cov3D_precomp=None):
+        rs = self.raster_settings
+        if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
+            raise Exception('Please provide excatly one of either SHs or precomputed colors!')
+        if ((scales is None or rotations is None) and cov3D_precomp is None) or \
+                ((scales is not None or rotations is not None) and cov3D_precomp is not None):
+            raise Exception('Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!')
+        empty = torch.empty(0, device=means3D.device)
+        shs = empty if shs is None else shs
+        colors_precomp = empty if colors_precomp is None else colors_precomp
+        scales = empty if scales is None else scales
+        rotations = empty if rotations is None else rotations
+        cov3D_precomp = empty if cov3D_precomp is None else cov3D_precomp
+        if language_feature_precomp is None:
+            language_feature_precomp = empty
+        if language_feature_weights_quick is None:
+            language_feature_weights_quick = empty
+        if language_feature_indices is None:
+            language_feature_indices = empty
+        if rs.quick_render and not (_present(language_feature_weights_quick) and
+                                    _present(language_feature_indices)):
+            raise Exception('quick_render requires language_feature_weights_quick and language_feature_indices!')
+        return rasterize_gaussians(means3D, means2D, shs, colors_precomp, language_feature_precomp,
+                                   language_feature_weights_quick, language_feature_indices, opacities, scales,
+                                   rotations, cov3D_precomp, rs)

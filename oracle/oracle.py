@@ -1,0 +1,211 @@
+"""numpy/ctypes wrapper of the CPU restatement (oracle/lsr_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg — never by the product path.  See lsr_oracle.h
+for the parity status (pinned by the reference's importable Python on the
+path's edges; against the absent CUDA kernels: parity unpinned).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "_build", "liblsr_oracle.so")
+_vp = ctypes.c_void_p
+
+
+class _Settings(ctypes.Structure):
+    _fields_ = [("W", ctypes.c_int), ("H", ctypes.c_int), ("tanfovx", ctypes.c_float), ("tanfovy", ctypes.c_float),
+                ("bg", _vp), ("scale_modifier", ctypes.c_float), ("viewmatrix", _vp), ("projmatrix", _vp),
+                ("sh_degree", ctypes.c_int), ("campos", _vp), ("include_feature", ctypes.c_int),
+                ("quick_render", ctypes.c_int), ("quick_dim", ctypes.c_int)]
+
+
+class _Inputs(ctypes.Structure):
+    _fields_ = [("N", ctypes.c_int), ("M", ctypes.c_int), ("D", ctypes.c_int), ("K", ctypes.c_int),
+                ("means3D", _vp), ("shs", _vp), ("colors_precomp", _vp), ("opacities", _vp), ("scales", _vp),
+                ("rotations", _vp), ("cov3D_precomp", _vp), ("lang", _vp), ("qweights", _vp), ("qindices", _vp)]
+
+
+class _Geom(ctypes.Structure):
+    _fields_ = [("depth", _vp), ("radii", _vp), ("xy", _vp), ("conic_opacity", _vp), ("rgb", _vp),
+                ("clamped", _vp), ("cov3D", _vp), ("tiles_touched", _vp)]
+
+
+class _RGrads(ctypes.Structure):
+    _fields_ = [("dmean2D", _vp), ("dconic", _vp), ("dopacity", _vp), ("dcolor", _vp), ("dlang", _vp)]
+
+
+class _PGrads(ctypes.Structure):
+    _fields_ = [("dmeans3D", _vp), ("dsh", _vp), ("dcolors", _vp), ("dscales", _vp), ("drot", _vp),
+                ("dcov3D", _vp)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        lib = ctypes.CDLL(_SO)
+        lib.lso_num_rendered.restype = ctypes.c_int64
+        lib.lso_num_rendered.argtypes = [ctypes.c_int, _vp]
+        lib.lso_expf.restype = ctypes.c_float
+        lib.lso_expf.argtypes = [ctypes.c_float]
+        _lib = lib
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(_vp)
+
+
+def _np(t, dtype=np.float32):
+    if t is None:
+        return None
+    if hasattr(t, "detach"):
+        t = t.detach().cpu().numpy()
+    return np.ascontiguousarray(t, dtype=dtype)
+
+
+class Problem:
+    """Host copies of one rasterizer call (settings + inputs), fp32/C-contiguous."""
+
+    def __init__(self, cam: dict, g: dict, bg=(0.0, 0.0, 0.0), scale_modifier=1.0, include_feature=None,
+                 quick=False, sh_degree=None):
+        self.W, self.H = int(cam["W"]), int(cam["H"])
+        self.tanfovx, self.tanfovy = float(cam["tanfovx"]), float(cam["tanfovy"])
+        self.view = _np(cam["viewmatrix"])
+        self.proj = _np(cam["projmatrix"])
+        self.campos = _np(cam["campos"])
+        self.bg = np.asarray(bg, dtype=np.float32)
+        self.scale_modifier = float(scale_modifier)
+        self.means3D = _np(g["means3D"])
+        self.N = self.means3D.shape[0]
+        self.shs = _np(g.get("shs"))
+        self.colors = _np(g.get("colors_precomp"))
+        self.opac = _np(g["opacities"])
+        self.scales = _np(g.get("scales"))
+        self.rot = _np(g.get("rotations"))
+        self.cov3D = _np(g.get("cov3D_precomp"))
+        if self.cov3D is not None:
+            self.scales = self.rot = None
+        self.lang = _np(g.get("language_feature_precomp"))
+        self.include_feature = (self.lang is not None) if include_feature is None else include_feature
+        self.quick = quick
+        self.qw = _np(g.get("language_feature_weights_quick")) if quick else None
+        self.qi = _np(g.get("language_feature_indices")) if quick else None
+        self.quick_dim = int(g.get("quick_dim", 192)) if quick else 0
+        self.sh_degree = int(g.get("sh_degree", 0) if sh_degree is None else sh_degree)
+        self.M = self.shs.shape[1] if self.shs is not None else 0
+        self.D = self.lang.shape[1] if (self.lang is not None and self.include_feature and not quick) else 0
+        self.K = self.qw.shape[1] if self.qw is not None else 0
+        self.gx, self.gy = (self.W + 15) // 16, (self.H + 15) // 16
+
+    def _structs(self):
+        s = _Settings(self.W, self.H, self.tanfovx, self.tanfovy, _p(self.bg), self.scale_modifier, _p(self.view),
+                      _p(self.proj), self.sh_degree, _p(self.campos), int(self.D > 0), int(self.quick),
+                      self.quick_dim)
+        i = _Inputs(self.N, self.M, self.D, self.K, _p(self.means3D), _p(self.shs), _p(self.colors), _p(self.opac),
+                    _p(self.scales), _p(self.rot), _p(self.cov3D), _p(self.lang) if self.D else None, _p(self.qw),
+                    _p(self.qi))
+        return s, i
+
+
+def forward(pb: Problem, nthreads: int = 1, tiles=None) -> dict:
+    """Full oracle forward; returns geometry, binning and image outputs.
+    `tiles`: optional subset of tile ids to render (others left zero)."""
+    lib = load()
+    N = pb.N
+    g = dict(depth=np.zeros(N, np.float32), radii=np.zeros(N, np.int32), xy=np.zeros((N, 2), np.float32),
+             conic_opacity=np.zeros((N, 4), np.float32), rgb=np.zeros((N, 3), np.float32),
+             clamped=np.zeros((N, 3), np.uint8), cov3D=np.zeros((N, 6), np.float32),
+             tiles_touched=np.zeros(N, np.uint32))
+    geom = _Geom(*[_p(g[k]) for k in ("depth", "radii", "xy", "conic_opacity", "rgb", "clamped", "cov3D",
+                                     "tiles_touched")])
+    s, i = pb._structs()
+    lib.lso_preprocess(ctypes.byref(s), ctypes.byref(i), ctypes.byref(geom))
+    M = int(lib.lso_num_rendered(N, _p(g["tiles_touched"])))
+    T = pb.gx * pb.gy
+    point_list = np.zeros(max(M, 1), np.uint32)
+    ranges = np.zeros((T, 2), np.uint32)
+    lib.lso_binning(ctypes.byref(s), N, ctypes.byref(geom), _p(point_list), _p(ranges))
+    Dout = pb.quick_dim if pb.quick else pb.D
+    H, W = pb.H, pb.W
+    color = np.zeros((3, H, W), np.float32)
+    lang = np.zeros((Dout, H, W), np.float32)
+    final_T = np.zeros((H, W), np.float32)
+    n_contrib = np.zeros((H, W), np.uint32)
+    if tiles is None:
+        lib.lso_render_fwd(ctypes.byref(s), ctypes.byref(i), ctypes.byref(geom), _p(point_list), _p(ranges),
+                           _p(color), _p(lang) if Dout else None, _p(final_T), _p(n_contrib), int(nthreads))
+    else:
+        tl = np.ascontiguousarray(tiles, dtype=np.int32)
+        lib.lso_render_fwd_tiles(ctypes.byref(s), ctypes.byref(i), ctypes.byref(geom), _p(point_list), _p(ranges),
+                                 _p(tl), len(tl), _p(color), _p(lang) if Dout else None, _p(final_T), _p(n_contrib),
+                                 int(nthreads))
+    out = dict(g)
+    out.update(num_rendered=M, point_list=point_list[:M], ranges=ranges, color=color, lang=lang, final_T=final_T,
+               n_contrib=n_contrib)
+    out["_keep"] = (g, geom)
+    return out
+
+
+def backward(pb: Problem, fwd: dict, dout_color: np.ndarray, dout_lang: np.ndarray | None = None, tiles=None) -> dict:
+    lib = load()
+    N, D = pb.N, pb.D
+    g, geom = fwd["_keep"]
+    s, i = pb._structs()
+    if pb.quick:
+        # quick-path language channels are not differentiated (as the GPU path)
+        s.quick_render = 0
+        s.include_feature = 0
+        i.D = 0
+        i.lang = None
+        D = 0
+    dcol = _np(dout_color)
+    dlang = _np(dout_lang) if (D and dout_lang is not None) else None
+    rg = dict(dmean2D=np.zeros((N, 3), np.float32), dconic=np.zeros((N, 3), np.float32),
+              dopacity=np.zeros(N, np.float32), dcolor=np.zeros((N, 3), np.float32),
+              dlang=np.zeros((N, max(D, 1)), np.float32))
+    rgs = _RGrads(_p(rg["dmean2D"]), _p(rg["dconic"]), _p(rg["dopacity"]), _p(rg["dcolor"]),
+                  _p(rg["dlang"]) if D else None)
+    pl = fwd["point_list"] if fwd["num_rendered"] > 0 else np.zeros(1, np.uint32)
+    pl = np.ascontiguousarray(pl)
+    if tiles is None:
+        lib.lso_render_bwd(ctypes.byref(s), ctypes.byref(i), ctypes.byref(geom), _p(pl), _p(fwd["ranges"]),
+                           _p(fwd["final_T"]), _p(fwd["n_contrib"]), _p(dcol), _p(dlang), ctypes.byref(rgs))
+    else:
+        tl = np.ascontiguousarray(tiles, dtype=np.int32)
+        lib.lso_render_bwd_tiles(ctypes.byref(s), ctypes.byref(i), ctypes.byref(geom), _p(pl), _p(fwd["ranges"]),
+                                 _p(tl), len(tl), _p(fwd["final_T"]), _p(fwd["n_contrib"]), _p(dcol), _p(dlang),
+                                 ctypes.byref(rgs))
+    pgd = dict(dmeans3D=np.zeros((N, 3), np.float32), dcolors=np.zeros((N, 3), np.float32))
+    if pb.shs is not None:
+        pgd["dsh"] = np.zeros_like(pb.shs)
+    if pb.scales is not None:
+        pgd["dscales"] = np.zeros((N, 3), np.float32)
+        pgd["drot"] = np.zeros((N, 4), np.float32)
+    if pb.cov3D is not None:
+        pgd["dcov3D"] = np.zeros((N, 6), np.float32)
+    pgs = _PGrads(_p(pgd["dmeans3D"]), _p(pgd.get("dsh")), _p(pgd["dcolors"]), _p(pgd.get("dscales")),
+                  _p(pgd.get("drot")), _p(pgd.get("dcov3D")))
+    lib.lso_preprocess_bwd(ctypes.byref(s), ctypes.byref(i), ctypes.byref(geom), ctypes.byref(rgs), ctypes.byref(pgs))
+    out = dict(rg)
+    out["dlang"] = rg["dlang"][:, :D] if D else None
+    out.update(pgd)
+    return out
+
+
+def expf(x: float) -> float:
+    return float(load().lso_expf(ctypes.c_float(x)))
