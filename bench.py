@@ -73,13 +73,15 @@ def algorithmic_bytes(g, rs, D, S):
     T = gx * gy
     C = 3 + D
     inst = 4 + 32 + 4 * C     # point_list id + splat record + feature row
-    VP = ((9 + D) + 31) // 32 * 32
+    VP = ((12 + D) + 31) // 32 * 32
+    chunk = max(1024, (N + 511) // 512)
+    chunk = (chunk + 255) // 256 * 256
+    B = (N + chunk - 1) // chunk
     b = {
         "preprocess": N * (12 + 12 + 16 + 4 + 4 * S) + N * (16 + 16 + 12 + 4 + 4 + 4 + 4),
-        "scan_tiles": N * 12,
-        "duplicate": vis * (16 + 4 + 4 + 4) + M * 4,
+        "bin_count": N * 4 + vis * 16 + B * T * 4 * 3 + T * 4,
         "scan_tile_counts": T * 12,
-        "scatter": vis * (16 + 4 + 4 + 4 + 4) + M * (4 + 8),
+        "bin_scatter": N * 4 + vis * (16 + 4) + B * T * 4 + T * 4 + M * 8,
         "tile_sort": M * (8 + 4),
         "render_fwd": staged_f * inst + T * 8 + P * (4 * C + 8),
         "grad_zero": N * VP * 4,
@@ -222,7 +224,7 @@ def main():
             gd = {k: v.detach() for k, v in g.items()}
             bytes_, info = algorithmic_bytes(gd, rs, D, 48)
         per_stage = {k: dict(ms_per_launch=(ms / calls if calls else 0.0), launches=calls)
-                     for k, (ms, calls) in stages.items()}
+                     for k, (ms, calls) in stages.items() if calls}
         dom = max(per_stage, key=lambda k: per_stage[k]["ms_per_launch"])
         dom_ms = per_stage[dom]["ms_per_launch"]
         dom_gbps = bytes_[dom] / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0

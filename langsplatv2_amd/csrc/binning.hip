@@ -1,14 +1,19 @@
-// binning.hip — tile binning (A.2): scan of tiles_touched, duplicate with
-// per-tile counting ranks, scatter into tile buckets, per-tile depth sort.
+// binning.hip — tile binning (A.2): per-tile instance counts, scatter into
+// tile buckets, per-tile depth sort.
 //
 // MI355X design (vs the reference's global 64-bit radix sort over
-// 32 + log2(T) bits of M keys): the tile is the bucket.  duplicate takes a
-// per-tile rank with one L2 atomic per instance, scatter places each
-// instance's key (depth bits << 32 | gaussian id) in its tile bucket, and one
-// 256-thread workgroup per tile sorts its bucket in LDS (flip-bitonic on
-// unique u64 keys).  The result equals a stable sort by
-// (tile, depth bits) with ties broken by Gaussian id — the order of the
-// reference's stable radix sort over duplicates emitted in Gaussian order.
+// 32 + log2(T) bits of M keys): the tile is the bucket.
+//  - count/scatter (k_bin_count / k_bin_table / k_bin_scatter): per-block
+//    tile histograms in LDS, a B x T column scan for block bases, LDS-atomic
+//    ranks inside the block: no global atomics at all.  (The older
+//    k_duplicate / k_scatter pair with one global atomic per instance remains
+//    as the fallback when T does not fit LDS.)
+//  - per-tile sort of the bucket's unique u64 keys (depth bits << 32 | id):
+//    one wave per tile with the keys in registers (k_tile_sort_wave, n <= 2048);
+//    a workgroup in LDS for n <= 4096, chunked LDS + global merge above.
+// The result equals a stable sort by (tile, depth bits) with ties broken by
+// Gaussian id — the order of the reference's stable radix sort over
+// duplicates emitted in Gaussian order.
 #include "lsr_internal.h"
 
 namespace lsr {
@@ -162,6 +167,147 @@ hipError_t launch_scatter(const Cam& c, int P, const uint8_t* geom, const int32_
     return hipGetLastError();
 }
 
+// --------------------------------------------- privatised count / scatter --
+// Block b owns Gaussians [b*chunk, (b+1)*chunk).  k_bin_count builds the
+// block's tile histogram with LDS atomics and writes it as row b of the
+// B x T table; k_bin_table scans each column (tile) over blocks; k_bin_scatter
+// re-walks the chunk and places every instance at tile_start + block base +
+// LDS-atomic rank.  No global atomics; the in-bucket order is arbitrary and
+// fixed by the per-tile sort.
+#define BIN_BLOCK 256
+
+__device__ __forceinline__ void bin_rect(const Cam& c, const uint8_t* geom, int P, int i, int r, int& x0, int& y0,
+                                         int& x1, int& y1)
+{
+    const GeomLayout L = geom_layout(P);
+    const float4 A = ((const float4*)(geom + L.splatA))[i];
+    get_rect(A.x, A.y, r, c.gx, c.gy, x0, y0, x1, y1);
+}
+
+__global__ void __launch_bounds__(BIN_BLOCK) k_bin_count(Cam c, int P, int chunk, const uint8_t* __restrict__ geom,
+                                                         const int32_t* __restrict__ radii, uint32_t* __restrict__ table)
+{
+    extern __shared__ uint32_t hist[];
+    const int T = c.gx * c.gy;
+    for (int k = threadIdx.x; k < T; k += BIN_BLOCK) hist[k] = 0;
+    __syncthreads();
+    const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
+    for (int i = g0 + threadIdx.x; i < g1; i += BIN_BLOCK) {
+        const int r = radii[i];
+        if (r <= 0) continue;
+        int x0, y0, x1, y1;
+        bin_rect(c, geom, P, i, r, x0, y0, x1, y1);
+        for (int y = y0; y < y1; y++)
+            for (int x = x0; x < x1; x++) atomicAdd(&hist[y * c.gx + x], 1u);
+    }
+    __syncthreads();
+    uint32_t* row = table + (size_t)blockIdx.x * T;
+    for (int k = threadIdx.x; k < T; k += BIN_BLOCK) row[k] = hist[k];
+}
+
+// Column scan: table[b][t] <- sum_{b' < b} table[b'][t]; tile_cnt[t] <- total.
+// A 256-thread block owns 32 tiles x 8 row segments: each thread sums its
+// segment (8 independent loads in flight), the 8 segment sums are scanned in
+// LDS, then each thread rewrites its segment with running bases.
+#define TBL_COLS 32
+#define TBL_SEGS 8
+__global__ void __launch_bounds__(256) k_bin_table(int T, int B, uint32_t* __restrict__ table,
+                                                   uint32_t* __restrict__ tile_cnt)
+{
+    __shared__ uint32_t seg_sum[TBL_SEGS][TBL_COLS];
+    const int col = threadIdx.x % TBL_COLS, seg = threadIdx.x / TBL_COLS;
+    const int t = blockIdx.x * TBL_COLS + col;
+    const int rows = (B + TBL_SEGS - 1) / TBL_SEGS;
+    const int b0 = seg * rows, b1 = min(B, b0 + rows);
+    uint32_t sum = 0;
+    if (t < T) {
+        int b = b0;
+        for (; b + 8 <= b1; b += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) v[k] = table[(size_t)(b + k) * T + t];
+#pragma unroll
+            for (int k = 0; k < 8; k++) sum += v[k];
+        }
+        for (; b < b1; b++) sum += table[(size_t)b * T + t];
+    }
+    seg_sum[seg][col] = sum;
+    __syncthreads();
+    uint32_t run = 0, tot = 0;
+    for (int k = 0; k < TBL_SEGS; k++) {
+        const uint32_t x = seg_sum[k][col];
+        run += (k < seg) ? x : 0u;
+        tot += x;
+    }
+    if (t >= T) return;
+    if (seg == 0) tile_cnt[t] = tot;
+    for (int b = b0; b < b1; b++) {
+        const uint32_t v = table[(size_t)b * T + t];
+        table[(size_t)b * T + t] = run;
+        run += v;
+    }
+}
+
+__global__ void __launch_bounds__(BIN_BLOCK) k_bin_scatter(Cam c, int P, int chunk, const uint8_t* __restrict__ geom,
+                                                           const int32_t* __restrict__ radii,
+                                                           const uint32_t* __restrict__ table,
+                                                           const uint32_t* __restrict__ tile_start,
+                                                           uint64_t* __restrict__ keys)
+{
+    extern __shared__ uint32_t base[];
+    const int T = c.gx * c.gy;
+    const uint32_t* row = table + (size_t)blockIdx.x * T;
+    for (int k = threadIdx.x; k < T; k += BIN_BLOCK) base[k] = tile_start[k] + row[k];
+    __syncthreads();
+    const GeomLayout L = geom_layout(P);
+    const float* depth = (const float*)(geom + L.depth);
+    const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
+    for (int i = g0 + threadIdx.x; i < g1; i += BIN_BLOCK) {
+        const int r = radii[i];
+        if (r <= 0) continue;
+        int x0, y0, x1, y1;
+        bin_rect(c, geom, P, i, r, x0, y0, x1, y1);
+        const uint64_t key = ((uint64_t)__float_as_uint(depth[i]) << 32) | (uint32_t)i;
+        for (int y = y0; y < y1; y++)
+            for (int x = x0; x < x1; x++) keys[atomicAdd(&base[y * c.gx + x], 1u)] = key;
+    }
+}
+
+int bin_blocks(int P, int T, int& chunk)
+{
+    // ~512 blocks (2 per CU) of >= 1024 Gaussians; the B x T table stays small
+    chunk = max(1024, (P + 511) / 512);
+    chunk = (chunk + BIN_BLOCK - 1) / BIN_BLOCK * BIN_BLOCK;
+    return (P + chunk - 1) / chunk;
+}
+
+bool bin_privatised_ok(int T) { return (size_t)T * 4 <= 150 * 1024; }
+
+hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t* geom, const int32_t* radii,
+                            uint32_t* table, uint32_t* tile_cnt, hipStream_t st)
+{
+    const int T = c.gx * c.gy;
+    if ((size_t)T * 4 > 65536) {
+        (void)hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize, T * 4);
+        (void)hipFuncSetAttribute((const void*)k_bin_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, T * 4);
+    }
+    if (B > 0) {
+        k_bin_count<<<B, BIN_BLOCK, (size_t)T * 4, st>>>(c, P, chunk, geom, radii, table);
+        k_bin_table<<<(T + TBL_COLS - 1) / TBL_COLS, 256, 0, st>>>(T, B, table, tile_cnt);
+    } else {
+        (void)hipMemsetAsync(tile_cnt, 0, (size_t)T * 4, st);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_bin_scatter(const Cam& c, int P, int chunk, int B, const uint8_t* geom, const int32_t* radii,
+                              const uint32_t* table, const uint32_t* tile_start, uint64_t* keys, hipStream_t st)
+{
+    const int T = c.gx * c.gy;
+    if (B > 0) k_bin_scatter<<<B, BIN_BLOCK, (size_t)T * 4, st>>>(c, P, chunk, geom, radii, table, tile_start, keys);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------ tile sort ---
 // Ascending flip-bitonic network over n keys with virtual +inf padding to the
 // next power of two: every compare-exchange puts the minimum at the lower
@@ -216,14 +362,15 @@ __device__ __forceinline__ int next_pow2(int n)
 }
 
 __global__ void __launch_bounds__(SORT_BLOCK) k_tile_sort(int T, const uint32_t* __restrict__ tile_start,
-                                                          uint64_t* __restrict__ keys, uint32_t* __restrict__ point_list)
+                                                          uint64_t* __restrict__ keys, uint32_t* __restrict__ point_list,
+                                                          int min_n)
 {
     __shared__ uint64_t buf[SORT_CHUNK];
     const int t = xcd_remap(blockIdx.x, gridDim.x);
     if (t >= T) return;
     const uint32_t s0 = tile_start[t], s1 = tile_start[t + 1];
     const int n = (int)(s1 - s0);
-    if (n == 0) return;
+    if (n == 0 || n < min_n) return;
     uint64_t* g = keys + s0;
     if (n <= SORT_CHUNK) {
         for (int k = threadIdx.x; k < n; k += SORT_BLOCK) buf[k] = g[k];
@@ -271,10 +418,93 @@ __global__ void __launch_bounds__(SORT_BLOCK) k_tile_sort(int T, const uint32_t*
     for (int k = threadIdx.x; k < n; k += SORT_BLOCK) point_list[s0 + k] = (uint32_t)g[k];
 }
 
+// Wave-level register bitonic sort for tiles of n <= 64*KPL keys: lane l
+// holds elements [l*KPL, l*KPL + KPL) (padding = UINT64_MAX).  Steps whose
+// partner distance j < KPL run inside the lane's registers; the others pair
+// lane l with lane l ^ (j / KPL) through shuffles.  No LDS, no barriers.
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m)
+{
+    const uint32_t lo = __shfl_xor((uint32_t)v, m, 64);
+    const uint32_t hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <int KPL>
+__device__ __forceinline__ void wave_sort_tile(uint64_t* __restrict__ g, uint32_t* __restrict__ out, int n)
+{
+    const int lane = threadIdx.x & 63;
+    uint64_t v[KPL];
+#pragma unroll
+    for (int r = 0; r < KPL; r++) {
+        const int e = lane * KPL + r;
+        v[r] = e < n ? g[e] : ~0ull;
+    }
+#pragma unroll
+    for (int k = 2; k <= 64 * KPL; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j >= 1; j >>= 1) {
+            if (j < KPL) {
+#pragma unroll
+                for (int r = 0; r < KPL; r++) {
+                    if (r & j) continue;
+                    const int e = lane * KPL + r;
+                    const bool asc = (e & k) == 0;
+                    const uint64_t a = v[r], b = v[r | j];
+                    const bool sw = asc ? (a > b) : (a < b);
+                    v[r] = sw ? b : a;
+                    v[r | j] = sw ? a : b;
+                }
+            } else {
+                const int m = j / KPL;
+                const bool lower = (lane & m) == 0;
+#pragma unroll
+                for (int r = 0; r < KPL; r++) {
+                    const int e = lane * KPL + r;
+                    const bool asc = (e & k) == 0;
+                    const uint64_t o = shfl_xor_u64(v[r], m);
+                    const bool take_min = (lower == asc);
+                    const uint64_t mn = v[r] < o ? v[r] : o, mx = v[r] < o ? o : v[r];
+                    v[r] = take_min ? mn : mx;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < KPL; r++) {
+        const int e = lane * KPL + r;
+        if (e < n) out[e] = (uint32_t)v[r];
+    }
+}
+
+// One wave per tile (4 tiles per 256-thread block).  Tiles above 2048 keys are
+// left to k_tile_sort_big.
+__global__ void __launch_bounds__(256) k_tile_sort_wave(int T, const uint32_t* __restrict__ tile_start,
+                                                        uint64_t* __restrict__ keys, uint32_t* __restrict__ point_list)
+{
+    const int w = threadIdx.x >> 6;
+    const int t = xcd_remap(blockIdx.x, gridDim.x) * 4 + w;
+    if (t >= T) return;
+    const uint32_t s0 = tile_start[t];
+    const int n = (int)(tile_start[t + 1] - s0);
+    if (n <= 1) {
+        if (n == 1 && (threadIdx.x & 63) == 0) point_list[s0] = (uint32_t)keys[s0];
+        return;
+    }
+    uint64_t* g = keys + s0;
+    uint32_t* o = point_list + s0;
+    if (n <= 64) wave_sort_tile<1>(g, o, n);
+    else if (n <= 128) wave_sort_tile<2>(g, o, n);
+    else if (n <= 256) wave_sort_tile<4>(g, o, n);
+    else if (n <= 512) wave_sort_tile<8>(g, o, n);
+    else if (n <= 1024) wave_sort_tile<16>(g, o, n);
+    else if (n <= 2048) wave_sort_tile<32>(g, o, n);
+}
+
 hipError_t launch_tile_sort(int T, const uint32_t* tile_start, uint64_t* keys, uint32_t* point_list, hipStream_t st)
 {
     if (T == 0) return hipSuccess;
-    k_tile_sort<<<T, SORT_BLOCK, 0, st>>>(T, tile_start, keys, point_list);
+    k_tile_sort_wave<<<(T + 3) / 4, 256, 0, st>>>(T, tile_start, keys, point_list);
+    k_tile_sort<<<T, SORT_BLOCK, 0, st>>>(T, tile_start, keys, point_list, 2049);
     return hipGetLastError();
 }
 

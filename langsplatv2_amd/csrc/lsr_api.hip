@@ -50,7 +50,7 @@ struct Status {
 // caller's stream; lsr_profile_query sums their elapsed times.
 enum Stage { ST_PRE, ST_SCAN, ST_DUP, ST_SCAN_T, ST_SCATTER, ST_SORT, ST_RENDER, ST_GZERO, ST_RENDER_BWD,
              ST_PRE_BWD, ST_N };
-const char* kStageNames[ST_N] = {"preprocess", "scan_tiles", "duplicate", "scan_tile_counts", "scatter",
+const char* kStageNames[ST_N] = {"preprocess", "scan_tiles", "bin_count", "scan_tile_counts", "bin_scatter",
                                  "tile_sort", "render_fwd", "grad_zero", "render_bwd", "preprocess_bwd"};
 
 struct Prof {
@@ -236,53 +236,74 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
 
     const GeomLayout GL = geom_layout((size_t)P);
     const ImageLayout IL = image_layout(NPIX, (size_t)T);
+    // privatised binning needs a B x T table (tail of the image workspace)
+    const bool priv = P > 0 && bin_privatised_ok(T);
+    int chunk = 0;
+    const int B = priv ? bin_blocks(P, T, chunk) : 0;
+    const size_t table_bytes = priv ? align256((size_t)B * T * 4) : 0;
     uint8_t* geom = (uint8_t*)alloc(ctx, GL.total, LSR_BUF_GEOM);
-    uint8_t* img = (uint8_t*)alloc(ctx, IL.total, LSR_BUF_IMAGE);
+    uint8_t* img = (uint8_t*)alloc(ctx, IL.total + table_bytes, LSR_BUF_IMAGE);
     if (!geom || !img) return LSR_ENOMEM;
     out->geom = geom;
     out->geom_bytes = GL.total;
     out->image = img;
-    out->image_bytes = IL.total;
+    out->image_bytes = IL.total + table_bytes;
+    uint32_t* table = (uint32_t*)(img + IL.total);
+    uint32_t* tile_cnt = (uint32_t*)(img + IL.tile_cnt);
+    uint32_t* tile_start = (uint32_t*)(img + IL.tile_start);
+    uint64_t* tpart = (uint64_t*)(img + IL.tile_part);
+    const size_t tnb = scan_partials((size_t)T) - 1;
 
     // 1. preprocess
     { StageScope sc(ST_PRE, st); LSR_HIP(launch_preprocess(c, *in, geom, out->radii, st)); }
     LSR_DEBUG_SYNC(s, st, "preprocess");
-    // 2. scan tiles_touched -> offsets ; read num_rendered
-    uint64_t* gpart = (uint64_t*)(geom + GL.scan_part);
-    const size_t gnb = scan_partials((size_t)P) - 1;
-    {
+    uint64_t M = 0;
+    if (priv) {
+        // 2. per-block tile histograms -> column scan -> tile starts; M = total
+        {
+            StageScope sc(ST_DUP, st);
+            LSR_HIP(launch_bin_count(c, P, chunk, B, geom, out->radii, table, tile_cnt, st));
+        }
+        {
+            StageScope sc(ST_SCAN_T, st);
+            LSR_HIP(launch_scan_u32(tile_cnt, tile_start, tpart, (size_t)T, true, st));
+            LSR_HIP(hipMemcpyAsync(tile_start + T, tpart + tnb, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+        }
+        LSR_HIP(hipMemcpyAsync(&M, tpart + tnb, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    } else {
+        uint64_t* gpart = (uint64_t*)(geom + GL.scan_part);
+        const size_t gnb = scan_partials((size_t)P) - 1;
         StageScope sc(ST_SCAN, st);
         LSR_HIP(launch_scan_u32((const uint32_t*)(geom + GL.tiles), (uint32_t*)(geom + GL.offsets), gpart,
                                 (size_t)P, false, st));
+        LSR_HIP(hipMemcpyAsync(&M, gpart + gnb, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     }
-    uint64_t M = 0;
-    LSR_HIP(hipMemcpyAsync(&M, gpart + gnb, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     LSR_HIP(hipStreamSynchronize(st));
+    LSR_DEBUG_SYNC(s, st, "count");
     if (M >= 0xffffffffull) return LSR_EOVERFLOW;
     out->num_rendered = (int64_t)M;
 
-    // 3. binning
+    // 3. binning workspace + scatter into tile buckets
     const BinLayout BL = bin_layout((size_t)M);
     uint8_t* bin = (uint8_t*)alloc(ctx, BL.total > 0 ? BL.total : 256, LSR_BUF_BINNING);
     if (!bin) return LSR_ENOMEM;
     out->binning = bin;
     out->binning_bytes = BL.total;
-    uint32_t* tile_cnt = (uint32_t*)(img + IL.tile_cnt);
-    uint32_t* tile_start = (uint32_t*)(img + IL.tile_start);
-    uint64_t* tpart = (uint64_t*)(img + IL.tile_part);
-    {
-        StageScope sc(ST_DUP, st);
-        LSR_HIP(hipMemsetAsync(tile_cnt, 0, (size_t)T * 4, st));
-        LSR_HIP(launch_duplicate(c, P, geom, out->radii, tile_cnt, (uint32_t*)(bin + BL.rank), st));
-    }
-    LSR_DEBUG_SYNC(s, st, "duplicate");
-    {
-        StageScope sc(ST_SCAN_T, st);
-        LSR_HIP(launch_scan_u32(tile_cnt, tile_start, tpart, (size_t)T, true, st));
-        const size_t tnb = scan_partials((size_t)T) - 1;
-        LSR_HIP(hipMemcpyAsync(tile_start + T, tpart + tnb, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-    }
-    {
+    if (priv) {
+        StageScope sc(ST_SCATTER, st);
+        LSR_HIP(launch_bin_scatter(c, P, chunk, B, geom, out->radii, table, tile_start, (uint64_t*)(bin + BL.keys),
+                                   st));
+    } else {
+        {
+            StageScope sc(ST_DUP, st);
+            LSR_HIP(hipMemsetAsync(tile_cnt, 0, (size_t)T * 4, st));
+            LSR_HIP(launch_duplicate(c, P, geom, out->radii, tile_cnt, (uint32_t*)(bin + BL.rank), st));
+        }
+        {
+            StageScope sc(ST_SCAN_T, st);
+            LSR_HIP(launch_scan_u32(tile_cnt, tile_start, tpart, (size_t)T, true, st));
+            LSR_HIP(hipMemcpyAsync(tile_start + T, tpart + tnb, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+        }
         StageScope sc(ST_SCATTER, st);
         LSR_HIP(launch_scatter(c, P, geom, out->radii, tile_start, (const uint32_t*)(bin + BL.rank),
                                (uint64_t*)(bin + BL.keys), st));

@@ -11,6 +11,9 @@
 #define LSR_TILE 16
 #define LSR_TILE_PIX 256
 #define LSR_WAVE 64
+// Gradient row layout (floats): [0,1] dL/dmean2D  [2,3,4] dL/dconic
+// [5] dL/dopacity  [6,7,8] dL/dcolor  [12, 12+D) dL/dlanguage (16-B aligned)
+#define LSR_GROW_LANG 12
 
 namespace lsr {
 
@@ -224,10 +227,36 @@ __device__ __forceinline__ float power_cut(float o)
     return -__logf(255.0f * o) - 0.02f;
 }
 
+// Conservative half-extents (pixels) of the region where power >= cut, i.e.
+// where a pair can contribute: the cut ellipse Q(d) <= 2|cut| has bounding
+// half-widths sqrt(2|cut| * cov2D.xx) and sqrt(2|cut| * cov2D.yy) (the conic
+// is the inverse 2D covariance).  +2 px margin; packed as two u16 into the
+// splat record's last word.  Anything degenerate gets the no-skip maximum.
+__device__ __forceinline__ uint32_t cut_extent(float cut, float a, float c, float det)
+{
+    uint32_t hx = 65535u, hy = 65535u;
+    if (det > 0.f && cut > -3.0e38f && cut <= 0.f) {
+        const float r2 = -2.f * cut;
+        const float ex = sqrtf(r2 * a), ey = sqrtf(r2 * c);
+        if (ex < 65000.f) hx = (uint32_t)ceilf(ex) + 2u;
+        if (ey < 65000.f) hy = (uint32_t)ceilf(ey) + 2u;
+    }
+    return hx | (hy << 16);
+}
+
+// Does the Gaussian (center x,y; packed extents) possibly touch the 8x8 pixel
+// block whose top-left pixel is (bx, by)?
+__device__ __forceinline__ bool block_overlap(float x, float y, uint32_t ext, int bx, int by)
+{
+    const float hx = (float)(ext & 0xffffu), hy = (float)(ext >> 16);
+    return (x + hx >= (float)bx) && (x - hx <= (float)(bx + 7)) && (y + hy >= (float)by) && (y - hy <= (float)(by + 7));
+}
+
 // ------------------------------------------------------------- layouts --
 // Geometry workspace (per Gaussian, SoA, every section 256-B aligned).
 struct GeomLayout {
     size_t splatA, splatB, rgb, depth, tiles, offsets, clamped, scan_part, total;
+    // splatA = {x, y, conic.a, conic.b}; splatB = {conic.c, opacity, cut, extent bits}
 };
 
 __host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -237,7 +266,7 @@ __host__ __device__ inline GeomLayout geom_layout(size_t N)
     GeomLayout L;
     size_t o = 0;
     L.splatA = o;   o += align256(N * 16);  // float4 {x, y, conic.a, conic.b}
-    L.splatB = o;   o += align256(N * 16);  // float4 {conic.c, opacity, cut, depth}
+    L.splatB = o;   o += align256(N * 16);  // float4 {conic.c, opacity, cut, u16x2 cut extents}
     L.rgb = o;      o += align256(N * 12);
     L.depth = o;    o += align256(N * 4);
     L.tiles = o;    o += align256(N * 4);

@@ -33,6 +33,12 @@ hipError_t launch_duplicate(const Cam& c, int P, const uint8_t* geom, const int3
                             uint32_t* rank, hipStream_t st);
 hipError_t launch_scatter(const Cam& c, int P, const uint8_t* geom, const int32_t* radii, const uint32_t* tile_start,
                           const uint32_t* rank, uint64_t* keys, hipStream_t st);
+int bin_blocks(int P, int T, int& chunk);
+bool bin_privatised_ok(int T);
+hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t* geom, const int32_t* radii,
+                            uint32_t* table, uint32_t* tile_cnt, hipStream_t st);
+hipError_t launch_bin_scatter(const Cam& c, int P, int chunk, int B, const uint8_t* geom, const int32_t* radii,
+                              const uint32_t* table, const uint32_t* tile_start, uint64_t* keys, hipStream_t st);
 hipError_t launch_tile_sort(int T, const uint32_t* tile_start, uint64_t* keys, uint32_t* point_list, hipStream_t st);
 
 // render.hip

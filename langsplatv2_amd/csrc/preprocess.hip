@@ -97,7 +97,8 @@ __global__ void __launch_bounds__(256) k_preprocess(Cam c, lsr_inputs in, uint8_
     depth[i] = pv.z;
     radii[i] = r;
     splatA[i] = make_float4(px, py, cc * det_inv, -b * det_inv);
-    splatB[i] = make_float4(a * det_inv, o, power_cut(o), pv.z);
+    const float cut = power_cut(o);
+    splatB[i] = make_float4(a * det_inv, o, cut, __uint_as_float(cut_extent(cut, a, cc, det)));
     tiles[i] = (uint32_t)area;
 }
 
@@ -114,9 +115,11 @@ hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, 
 }
 
 // ---------------------------------------------------------------------------
-// Backward: chain rule through A.1.  grad_acc row layout (VP floats):
-//   [0,1] dL/dmean2D (NDC)  [2,3,4] dL/dconic (a,b,c)  [5] dL/dopacity
-//   [6,7,8] dL/dcolor       [9, 9+D) dL/dlanguage
+// Backward: chain rule through A.1.  Gradient row layout: lsr_device.h
+// (LSR_GROW_LANG).  Rows are read as float4; the SH gradient is written as
+// 12 float4 per Gaussian (basis(k) * dRGB(ch)), the language gradient as
+// float4 when D % 4 == 0.
+template <bool SH16>
 __global__ void __launch_bounds__(256) k_preprocess_bwd(Cam c, lsr_inputs in, const uint8_t* __restrict__ geom,
                                                         const int32_t* __restrict__ radii,
                                                         const float* __restrict__ gacc, int VP, lsr_bwd_out out)
@@ -125,33 +128,56 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(Cam c, lsr_inputs in, co
     const int N = in.P;
     if (i >= N) return;
     const GeomLayout L = geom_layout(N);
-    const uint32_t clampm = ((const uint32_t*)(geom + L.clamped))[i];
-    const float* g = gacc + (size_t)i * VP;
     const bool vis = radii[i] > 0;
     const int M = in.max_coeffs;
     const int D = in.lang_dim;
+    const float4* g4 = reinterpret_cast<const float4*>(gacc + (size_t)i * VP);
+    float4 g0 = make_float4(0.f, 0.f, 0.f, 0.f), g1 = g0, g2 = g0;
+    if (vis) {
+        g0 = g4[0];
+        g1 = g4[1];
+        g2 = g4[2];
+    }
+    const float gm2x = g0.x, gm2y = g0.y, dA = g0.z, dB = g0.w;
+    const float dC = g1.x, gop = g1.y;
+    const float gcol[3] = {g1.z, g1.w, g2.x};
 
     if (out.dL_dmeans2D) {
-        out.dL_dmeans2D[3 * i + 0] = vis ? g[0] : 0.f;
-        out.dL_dmeans2D[3 * i + 1] = vis ? g[1] : 0.f;
+        out.dL_dmeans2D[3 * i + 0] = gm2x;
+        out.dL_dmeans2D[3 * i + 1] = gm2y;
         out.dL_dmeans2D[3 * i + 2] = 0.f;
     }
-    if (out.dL_dopacity) out.dL_dopacity[i] = vis ? g[5] : 0.f;
-    if (out.dL_dlang)
-        for (int k = 0; k < D; k++) out.dL_dlang[(size_t)i * D + k] = vis ? g[9 + k] : 0.f;
+    if (out.dL_dopacity) out.dL_dopacity[i] = gop;
+    if (out.dL_dlang) {
+        if ((D & 3) == 0) {
+            float4* dl = reinterpret_cast<float4*>(out.dL_dlang + (size_t)i * D);
+            for (int q = 0; q < D / 4; q++) dl[q] = vis ? g4[LSR_GROW_LANG / 4 + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+            const float* g = gacc + (size_t)i * VP + LSR_GROW_LANG;
+            for (int k = 0; k < D; k++) out.dL_dlang[(size_t)i * D + k] = vis ? g[k] : 0.f;
+        }
+    }
     if (out.dL_dcolors)
-        for (int k = 0; k < 3; k++) out.dL_dcolors[3 * i + k] = vis ? g[6 + k] : 0.f;
+        for (int k = 0; k < 3; k++) out.dL_dcolors[3 * i + k] = gcol[k];
 
-    float dm[3] = {0.f, 0.f, 0.f};
     const bool want_sh = out.dL_dsh && in.shs && !in.colors_precomp;
     if (!vis) {
         if (out.dL_dmeans3D) { out.dL_dmeans3D[3 * i] = 0.f; out.dL_dmeans3D[3 * i + 1] = 0.f; out.dL_dmeans3D[3 * i + 2] = 0.f; }
-        if (want_sh) for (int k = 0; k < M * 3; k++) out.dL_dsh[(size_t)i * M * 3 + k] = 0.f;
+        if (want_sh) {
+            if (SH16) {
+                float4* d4 = reinterpret_cast<float4*>(out.dL_dsh) + (size_t)i * 12;
+#pragma unroll
+                for (int k = 0; k < 12; k++) d4[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            } else {
+                for (int k = 0; k < M * 3; k++) out.dL_dsh[(size_t)i * M * 3 + k] = 0.f;
+            }
+        }
         if (out.dL_dscales) for (int k = 0; k < 3; k++) out.dL_dscales[3 * i + k] = 0.f;
-        if (out.dL_drotations) for (int k = 0; k < 4; k++) out.dL_drotations[4 * i + k] = 0.f;
+        if (out.dL_drotations) reinterpret_cast<float4*>(out.dL_drotations)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (out.dL_dcov3D) for (int k = 0; k < 6; k++) out.dL_dcov3D[6 * i + k] = 0.f;
         return;
     }
+    (void)L;
     const float* V = c.view;
     const float* P = c.proj;
     const float mx = in.means3D[3 * i], my = in.means3D[3 * i + 1], mz = in.means3D[3 * i + 2];
@@ -170,7 +196,6 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(Cam c, lsr_inputs in, co
     ewa_setup(V, pv, c.fx, c.fy, c.tanfovx, c.tanfovy, e);
     float a, b, cc;
     ewa_cov2D(e, cov, a, b, cc);
-    const float dA = g[2], dB = g[3], dC = g[4];
     const float det = a * cc - b * b;
     const float d2inv = 1.0f / ((det * det) + 0.0000001f);
     float dLa = 0.f, dLb = 0.f, dLc = 0.f;
@@ -205,6 +230,7 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(Cam c, lsr_inputs in, co
     const float dty = e.yclamp ? 0.f : -c.fy * tz2 * dJ12;
     const float dtz = -c.fx * tz2 * dJ00 - c.fy * tz2 * dJ11 + (2.f * c.fx * e.tx) * tz3 * dJ02 +
                       (2.f * c.fy * e.ty) * tz3 * dJ12;
+    float dm[3];
     dm[0] = V[0] * dtx + V[1] * dty + V[2] * dtz;
     dm[1] = V[4] * dtx + V[5] * dty + V[6] * dtz;
     dm[2] = V[8] * dtx + V[9] * dty + V[10] * dtz;
@@ -212,56 +238,74 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(Cam c, lsr_inputs in, co
     const float4 ph = xform44(P, mx, my, mz);
     const float mw = 1.0f / (ph.w + 0.0000001f);
     const float mul1 = ph.x * mw * mw, mul2 = ph.y * mw * mw;
-    const float g2x = g[0], g2y = g[1];
-    dm[0] += (P[0] * mw - P[3] * mul1) * g2x + (P[1] * mw - P[3] * mul2) * g2y;
-    dm[1] += (P[4] * mw - P[7] * mul1) * g2x + (P[5] * mw - P[7] * mul2) * g2y;
-    dm[2] += (P[8] * mw - P[11] * mul1) * g2x + (P[9] * mw - P[11] * mul2) * g2y;
+    dm[0] += (P[0] * mw - P[3] * mul1) * gm2x + (P[1] * mw - P[3] * mul2) * gm2y;
+    dm[1] += (P[4] * mw - P[7] * mul1) * gm2x + (P[5] * mw - P[7] * mul2) * gm2y;
+    dm[2] += (P[8] * mw - P[11] * mul1) * gm2x + (P[9] * mw - P[11] * mul2) * gm2y;
 
     if (in.shs && !in.colors_precomp) {
+        const uint32_t clampm = ((const uint32_t*)(geom + L.clamped))[i];
         float dRGB[3];
 #pragma unroll
-        for (int k = 0; k < 3; k++) dRGB[k] = ((clampm >> k) & 1u) ? 0.f : g[6 + k];
+        for (int k = 0; k < 3; k++) dRGB[k] = ((clampm >> k) & 1u) ? 0.f : gcol[k];
         float dir[3], dor[3];
         sh_dir(mx, my, mz, c.campos, dir, dor);
         const float x = dir[0], y = dir[1], z = dir[2];
-        const float* sh = in.shs + (size_t)i * M * 3;
         const int deg = c.sh_degree;
+        float sh[48];
+        if (SH16) {
+            const float4* src = reinterpret_cast<const float4*>(in.shs) + (size_t)i * 12;
+#pragma unroll
+            for (int k = 0; k < 12; k++) {
+                const float4 t4 = src[k];
+                sh[4 * k] = t4.x; sh[4 * k + 1] = t4.y; sh[4 * k + 2] = t4.z; sh[4 * k + 3] = t4.w;
+            }
+        } else {
+            const float* src = in.shs + (size_t)i * M * 3;
+#pragma unroll
+            for (int k = 0; k < 48; k++) sh[k] = (k < M * 3) ? src[k] : 0.f;
+        }
+        // basis functions (dRGB/dsh_k), term order of the forward
+        float bk[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) bk[k] = 0.f;
+        bk[0] = 0.28209479177387814f;
         float ddx[3] = {0.f, 0.f, 0.f}, ddy[3] = {0.f, 0.f, 0.f}, ddz[3] = {0.f, 0.f, 0.f};
-        float* ds = out.dL_dsh ? out.dL_dsh + (size_t)i * M * 3 : nullptr;
-        for (int k = 0; k < M * 3; k++)
-            if (ds) ds[k] = 0.f;
-        for (int ch = 0; ch < 3; ch++) {
 #define S(k) sh[(k)*3 + ch]
-#define DS(k, val) if (ds) ds[(k)*3 + ch] = (val)
-            const float gch = dRGB[ch];
-            DS(0, 0.28209479177387814f * gch);
-            if (deg > 0) {
-                const float c1 = 0.4886025119029199f;
-                DS(1, -c1 * y * gch);
-                DS(2, c1 * z * gch);
-                DS(3, -c1 * x * gch);
+        if (deg > 0) {
+            const float c1 = 0.4886025119029199f;
+            bk[1] = -c1 * y;
+            bk[2] = c1 * z;
+            bk[3] = -c1 * x;
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) {
                 ddx[ch] = -c1 * S(3);
                 ddy[ch] = -c1 * S(1);
                 ddz[ch] = c1 * S(2);
-                if (deg > 1) {
-                    const float xx = x * x, yy = y * y, zz = z * z;
-                    const float xy = x * y, yz = y * z, xz = x * z;
-                    DS(4, LSR_C2_0 * xy * gch);
-                    DS(5, LSR_C2_1 * yz * gch);
-                    DS(6, LSR_C2_2 * (2.f * zz - xx - yy) * gch);
-                    DS(7, LSR_C2_3 * xz * gch);
-                    DS(8, LSR_C2_4 * (xx - yy) * gch);
+            }
+            if (deg > 1) {
+                const float xx = x * x, yy = y * y, zz = z * z;
+                const float xy = x * y, yz = y * z, xz = x * z;
+                bk[4] = LSR_C2_0 * xy;
+                bk[5] = LSR_C2_1 * yz;
+                bk[6] = LSR_C2_2 * (2.f * zz - xx - yy);
+                bk[7] = LSR_C2_3 * xz;
+                bk[8] = LSR_C2_4 * (xx - yy);
+#pragma unroll
+                for (int ch = 0; ch < 3; ch++) {
                     ddx[ch] += LSR_C2_0 * y * S(4) + LSR_C2_2 * 2.f * -x * S(6) + LSR_C2_3 * z * S(7) + LSR_C2_4 * 2.f * x * S(8);
                     ddy[ch] += LSR_C2_0 * x * S(4) + LSR_C2_1 * z * S(5) + LSR_C2_2 * 2.f * -y * S(6) + LSR_C2_4 * 2.f * -y * S(8);
                     ddz[ch] += LSR_C2_1 * y * S(5) + LSR_C2_2 * 2.f * 2.f * z * S(6) + LSR_C2_3 * x * S(7);
-                    if (deg > 2) {
-                        DS(9, LSR_C3_0 * y * (3.f * xx - yy) * gch);
-                        DS(10, LSR_C3_1 * xy * z * gch);
-                        DS(11, LSR_C3_2 * y * (4.f * zz - xx - yy) * gch);
-                        DS(12, LSR_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy) * gch);
-                        DS(13, LSR_C3_4 * x * (4.f * zz - xx - yy) * gch);
-                        DS(14, LSR_C3_5 * z * (xx - yy) * gch);
-                        DS(15, LSR_C3_6 * x * (xx - 3.f * yy) * gch);
+                }
+                if (deg > 2) {
+                    bk[9] = LSR_C3_0 * y * (3.f * xx - yy);
+                    bk[10] = LSR_C3_1 * xy * z;
+                    bk[11] = LSR_C3_2 * y * (4.f * zz - xx - yy);
+                    bk[12] = LSR_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                    bk[13] = LSR_C3_4 * x * (4.f * zz - xx - yy);
+                    bk[14] = LSR_C3_5 * z * (xx - yy);
+                    bk[15] = LSR_C3_6 * x * (xx - 3.f * yy);
+#pragma unroll
+                    for (int ch = 0; ch < 3; ch++) {
                         ddx[ch] += LSR_C3_0 * S(9) * 3.f * 2.f * xy + LSR_C3_1 * S(10) * yz + LSR_C3_2 * S(11) * -2.f * xy +
                                    LSR_C3_3 * S(12) * -3.f * 2.f * xz + LSR_C3_4 * S(13) * (-3.f * xx + 4.f * zz - yy) +
                                    LSR_C3_5 * S(14) * 2.f * xz + LSR_C3_6 * S(15) * 3.f * (xx - yy);
@@ -275,12 +319,29 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(Cam c, lsr_inputs in, co
                     }
                 }
             }
-#undef S
-#undef DS
         }
-        float gd0 = ddx[0] * dRGB[0] + ddx[1] * dRGB[1] + ddx[2] * dRGB[2];
-        float gd1 = ddy[0] * dRGB[0] + ddy[1] * dRGB[1] + ddy[2] * dRGB[2];
-        float gd2 = ddz[0] * dRGB[0] + ddz[1] * dRGB[1] + ddz[2] * dRGB[2];
+#undef S
+        if (want_sh) {
+            if (SH16) {
+                float4* d4 = reinterpret_cast<float4*>(out.dL_dsh) + (size_t)i * 12;
+#pragma unroll
+                for (int k4 = 0; k4 < 12; k4++) {
+                    float e4[4];
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int el = 4 * k4 + r;
+                        e4[r] = bk[el / 3] * dRGB[el % 3];
+                    }
+                    d4[k4] = make_float4(e4[0], e4[1], e4[2], e4[3]);
+                }
+            } else {
+                float* ds = out.dL_dsh + (size_t)i * M * 3;
+                for (int k = 0; k < M * 3; k++) ds[k] = (k < 48) ? bk[k / 3] * dRGB[k % 3] : 0.f;
+            }
+        }
+        const float gd0 = ddx[0] * dRGB[0] + ddx[1] * dRGB[1] + ddx[2] * dRGB[2];
+        const float gd1 = ddy[0] * dRGB[0] + ddy[1] * dRGB[1] + ddy[2] * dRGB[2];
+        const float gd2 = ddz[0] * dRGB[0] + ddz[1] * dRGB[1] + ddz[2] * dRGB[2];
         const float sum2 = dor[0] * dor[0] + dor[1] * dor[1] + dor[2] * dor[2];
         const float inv32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
         dm[0] += ((sum2 - dor[0] * dor[0]) * gd0 - dor[1] * dor[0] * gd1 - dor[2] * dor[0] * gd2) * inv32;
@@ -324,10 +385,12 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(Cam c, lsr_inputs in, co
             for (int k = 0; k < 3; k++) dR[r * 3 + k] = dM[r * 3 + k] * sv[k];
         const float qr = q.x, qx = q.y, qy = q.z, qz = q.w;
         if (out.dL_drotations) {
-            out.dL_drotations[4 * i + 0] = 2.f * (-qz * dR[1] + qy * dR[2] + qz * dR[3] - qx * dR[5] - qy * dR[6] + qx * dR[7]);
-            out.dL_drotations[4 * i + 1] = 2.f * (qy * dR[1] + qz * dR[2] + qy * dR[3] - qr * dR[5] + qz * dR[6] + qr * dR[7]) - 4.f * qx * (dR[4] + dR[8]);
-            out.dL_drotations[4 * i + 2] = 2.f * (qx * dR[1] + qr * dR[2] + qx * dR[3] + qz * dR[5] - qr * dR[6] + qz * dR[7]) - 4.f * qy * (dR[0] + dR[8]);
-            out.dL_drotations[4 * i + 3] = 2.f * (-qr * dR[1] + qx * dR[2] + qr * dR[3] + qy * dR[5] + qx * dR[6] + qy * dR[7]) - 4.f * qz * (dR[0] + dR[4]);
+            float4 gq;
+            gq.x = 2.f * (-qz * dR[1] + qy * dR[2] + qz * dR[3] - qx * dR[5] - qy * dR[6] + qx * dR[7]);
+            gq.y = 2.f * (qy * dR[1] + qz * dR[2] + qy * dR[3] - qr * dR[5] + qz * dR[6] + qr * dR[7]) - 4.f * qx * (dR[4] + dR[8]);
+            gq.z = 2.f * (qx * dR[1] + qr * dR[2] + qx * dR[3] + qz * dR[5] - qr * dR[6] + qz * dR[7]) - 4.f * qy * (dR[0] + dR[8]);
+            gq.w = 2.f * (-qr * dR[1] + qx * dR[2] + qr * dR[3] + qy * dR[5] + qx * dR[6] + qy * dR[7]) - 4.f * qz * (dR[0] + dR[4]);
+            reinterpret_cast<float4*>(out.dL_drotations)[i] = gq;
         }
     }
 }
@@ -337,7 +400,12 @@ hipError_t launch_preprocess_bwd(const Cam& c, const lsr_inputs& in, const uint8
 {
     if (in.P == 0) return hipSuccess;
     dim3 grid((in.P + 255) / 256), block(256);
-    k_preprocess_bwd<<<grid, block, 0, st>>>(c, in, geom, radii, grad_acc, VP, out);
+    const bool sh16 = in.shs && in.max_coeffs == 16 && ((uintptr_t)in.shs % 16 == 0) &&
+                      (!out.dL_dsh || (uintptr_t)out.dL_dsh % 16 == 0);
+    if (sh16)
+        k_preprocess_bwd<true><<<grid, block, 0, st>>>(c, in, geom, radii, grad_acc, VP, out);
+    else
+        k_preprocess_bwd<false><<<grid, block, 0, st>>>(c, in, geom, radii, grad_acc, VP, out);
     return hipGetLastError();
 }
 

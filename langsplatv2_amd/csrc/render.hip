@@ -77,6 +77,41 @@ __device__ __forceinline__ float wave_reduce32(float (&v)[32])
     return v[0];
 }
 
+// Reduce 16 per-lane values across the wave; on return lane l holds the
+// wave-wide sum of value ((l >> 2) & 15).
+__device__ __forceinline__ float wave_reduce16(float (&v)[16])
+{
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[k]), __float_as_uint(v[k + 8]), false, false);
+        v[k] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[k]), __float_as_uint(v[k + 4]), false, false);
+        v[k] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+    {
+        const bool hi = lane & 8;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            float keep = hi ? v[k + 2] : v[k];
+            float send = hi ? v[k] : v[k + 2];
+            v[k] = keep + dpp<0x128>(send);
+        }
+    }
+    {
+        const bool hi = lane & 4;
+        float keep = hi ? v[1] : v[0];
+        float send = hi ? v[0] : v[1];
+        v[0] = keep + dpp<0x141>(send);
+    }
+    v[0] = v[0] + dpp<0x4E>(v[0]);
+    v[0] = v[0] + dpp<0xB1>(v[0]);
+    return v[0];
+}
+
 __device__ __forceinline__ int wave_max_i(int v)
 {
 #pragma unroll
@@ -85,6 +120,60 @@ __device__ __forceinline__ int wave_max_i(int v)
 }
 
 // ---------------------------------------------------------- forward -------
+// Lane -> pixel mapping: wave w of the tile owns the 8x8 block
+// (w & 1, w >> 1); lane l owns pixel (l & 7, l >> 3) of it.
+struct PixMap {
+    int bx, by, px, py;
+    __device__ PixMap(const Cam& c, int tile, int t)
+    {
+        const int tx = tile % c.gx, ty = tile / c.gx;
+        const int w = t >> 6, l = t & 63;
+        bx = tx * LSR_TILE + (w & 1) * 8;
+        by = ty * LSR_TILE + (w >> 1) * 8;
+        px = bx + (l & 7);
+        py = by + (l >> 3);
+    }
+};
+
+// Stage one instance's feature row (rgb + dense language) into LDS.
+template <int NL, int F4>
+__device__ __forceinline__ void stage_features(float4* dst, const float* rgb, const float* lang, int D, uint32_t gid)
+{
+    float row[F4 * 4];
+    row[0] = rgb[3 * gid];
+    row[1] = rgb[3 * gid + 1];
+    row[2] = rgb[3 * gid + 2];
+    if (NL > 0 && D == NL && (NL % 4) == 0) {
+        const float4* src = reinterpret_cast<const float4*>(lang + (size_t)gid * NL);
+#pragma unroll
+        for (int q = 0; q < NL / 4; q++) {
+            const float4 v = src[q];
+            row[3 + 4 * q] = v.x; row[4 + 4 * q] = v.y; row[5 + 4 * q] = v.z; row[6 + 4 * q] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < NL; k++) row[3 + k] = (k < D) ? lang[(size_t)gid * D + k] : 0.f;
+    }
+#pragma unroll
+    for (int k = 3 + NL; k < F4 * 4; k++) row[k] = 0.f;
+#pragma unroll
+    for (int q = 0; q < F4; q++) dst[q] = make_float4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
+}
+
+// Mask of instances [q, q+64) of a staged batch that may touch this wave's
+// 8x8 block (one ballot; the result lives in SGPRs and is walked with s_ff1).
+__device__ __forceinline__ uint64_t sub_mask(const float4* sA, const float4* sB, int q, int n, int bx, int by)
+{
+    const int j = q + (threadIdx.x & 63);
+    bool ok = false;
+    if (j < n) {
+        const float4 A = sA[j];
+        const float4 B = sB[j];
+        ok = block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by);
+    }
+    return __ballot(ok);
+}
+
 template <int NL>
 __global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a)
 {
@@ -96,11 +185,10 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a)
 
     const Cam& c = a.cam;
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int tx = tile % c.gx, ty = tile / c.gx;
     const int t = threadIdx.x;
-    const int px = tx * LSR_TILE + (t & 15), py = ty * LSR_TILE + (t >> 4);
-    const bool inside = px < c.W && py < c.H;
-    const float pfx = (float)px, pfy = (float)py;
+    const PixMap pm(c, tile, t);
+    const bool inside = pm.px < c.W && pm.py < c.H;
+    const float pfx = (float)pm.px, pfy = (float)pm.py;
     const uint32_t rs = a.tile_start[tile], re = a.tile_start[tile + 1];
     const int D = a.D;
 
@@ -108,7 +196,7 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a)
     float acc[F4 * 4];
 #pragma unroll
     for (int k = 0; k < F4 * 4; k++) acc[k] = 0.f;
-    uint32_t contributor = 0, last = 0;
+    uint32_t last = 0;
     bool done = !inside;
 
     for (uint32_t base = rs; base < re; base += 256) {
@@ -118,50 +206,80 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a)
             const uint32_t gid = a.point_list[idx];
             sA[t] = a.splatA[gid];
             sB[t] = a.splatB[gid];
-            float row[F4 * 4];
-            row[0] = a.rgb[3 * gid];
-            row[1] = a.rgb[3 * gid + 1];
-            row[2] = a.rgb[3 * gid + 2];
-#pragma unroll
-            for (int k = 0; k < NL; k++) row[3 + k] = (k < D) ? a.lang[(size_t)gid * D + k] : 0.f;
-#pragma unroll
-            for (int k = 3 + NL; k < F4 * 4; k++) row[k] = 0.f;
-#pragma unroll
-            for (int q = 0; q < F4; q++) sF[t * F4 + q] = make_float4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
+            stage_features<NL, F4>(&sF[t * F4], a.rgb, a.lang, D, gid);
         }
         __syncthreads();
         const int n = (int)min(256u, re - base);
-        for (int j = 0; !done && j < n; j++) {
-            contributor++;
-            const float4 A = sA[j];
-            const float4 B = sB[j];
-            const float dx = A.x - pfx, dy = A.y - pfy;
-            const float power = splat_power(A.z, A.w, B.x, dx, dy);
-            if (power > 0.0f || power < B.z) continue;
-            const float G = expf_det(power);
-            const float alpha = fminf(0.99f, B.y * G);
-            if (alpha < 1.0f / 255.0f) continue;
-            const float test_T = T * (1.0f - alpha);
-            if (test_T < 0.0001f) {
-                done = true;
-                continue;
-            }
-            const float aT = alpha * T;
+        const uint32_t pos0 = base - rs + 1;   // contributor index of instance j is pos0 + j
+#pragma unroll 1
+        for (int q = 0; q < n; q += 64) {
+            uint64_t bits = sub_mask(sA, sB, q, n, pm.bx, pm.by);
+            // Two instances per iteration, branch-free per lane: a lane that
+            // skips an instance (exponent cut, alpha < 1/255, saturated or
+            // done) blends it with weight 0 and keeps T.  The two exp chains
+            // are independent (ILP); only T carries from the first to the
+            // second, exactly as in the sequential per-pixel order.
+            while (bits) {
+                if (__ballot(!done) == 0) break;
+                const int j0 = q + (int)__builtin_ctzll(bits);
+                bits &= bits - 1;
+                const bool two = bits != 0;
+                const int j1 = two ? q + (int)__builtin_ctzll(bits) : j0;
+                bits &= bits - 1;
+                const float4 A0 = sA[j0], B0 = sB[j0];
+                const float4 A1 = sA[j1], B1 = sB[j1];
+                const float p0 = splat_power(A0.z, A0.w, B0.x, A0.x - pfx, A0.y - pfy);
+                const float p1 = splat_power(A1.z, A1.w, B1.x, A1.x - pfx, A1.y - pfy);
+                bool ok0 = !done && !(p0 > 0.0f || p0 < B0.z);
+                bool ok1 = two && !done && !(p1 > 0.0f || p1 < B1.z);
+                if (!__any(ok0 || ok1)) continue;
+                const float al0 = fminf(0.99f, B0.y * expf_det(p0));
+                const float al1 = fminf(0.99f, B1.y * expf_det(p1));
+                ok0 = ok0 && !(al0 < 1.0f / 255.0f);
+                ok1 = ok1 && !(al1 < 1.0f / 255.0f);
+                // instance j0
+                {
+                    const float test_T = T * (1.0f - al0);
+                    const bool term = ok0 && (test_T < 0.0001f);
+                    done = done || term;
+                    ok0 = ok0 && !term;
+                    ok1 = ok1 && !term;
+                    const float aT = ok0 ? al0 * T : 0.f;
 #pragma unroll
-            for (int q = 0; q < F4; q++) {
-                const float4 f = sF[j * F4 + q];
-                acc[4 * q + 0] = fmaf(f.x, aT, acc[4 * q + 0]);
-                acc[4 * q + 1] = fmaf(f.y, aT, acc[4 * q + 1]);
-                acc[4 * q + 2] = fmaf(f.z, aT, acc[4 * q + 2]);
-                acc[4 * q + 3] = fmaf(f.w, aT, acc[4 * q + 3]);
+                    for (int f = 0; f < F4; f++) {
+                        const float4 v = sF[j0 * F4 + f];
+                        acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
+                        acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
+                        acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
+                        acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
+                    }
+                    T = ok0 ? test_T : T;
+                    last = ok0 ? pos0 + j0 : last;
+                }
+                // instance j1
+                if (__any(ok1)) {
+                    const float test_T = T * (1.0f - al1);
+                    const bool term = ok1 && (test_T < 0.0001f);
+                    done = done || term;
+                    ok1 = ok1 && !term;
+                    const float aT = ok1 ? al1 * T : 0.f;
+#pragma unroll
+                    for (int f = 0; f < F4; f++) {
+                        const float4 v = sF[j1 * F4 + f];
+                        acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
+                        acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
+                        acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
+                        acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
+                    }
+                    T = ok1 ? test_T : T;
+                    last = ok1 ? pos0 + j1 : last;
+                }
             }
-            T = test_T;
-            last = contributor;
         }
     }
     if (inside) {
         const size_t HW = (size_t)c.H * c.W;
-        const size_t pix = (size_t)py * c.W + px;
+        const size_t pix = (size_t)pm.py * c.W + pm.px;
         a.final_T[pix] = T;
         a.n_contrib[pix] = last;
 #pragma unroll
@@ -173,7 +291,7 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a)
 }
 
 // Sparse "quick" language path: Dq output channels, K (weight, index) pairs
-// per Gaussian.  One wave per 16x4 pixel strip; per-pixel accumulators in LDS
+// per Gaussian.  One wave per 8x8 pixel block; per-pixel accumulators in LDS
 // laid out [channel][lane] (conflict-free: the channel index is wave-uniform
 // because every lane processes the same Gaussian).
 __global__ void __launch_bounds__(64) k_render_fwd_quick(RenderArgs a)
@@ -189,17 +307,15 @@ __global__ void __launch_bounds__(64) k_render_fwd_quick(RenderArgs a)
 
     const Cam& c = a.cam;
     const int tile = xcd_remap(blockIdx.x >> 2, gridDim.x >> 2);
-    const int strip = blockIdx.x & 3;
-    const int tx = tile % c.gx, ty = tile / c.gx;
     const int t = threadIdx.x;
-    const int px = tx * LSR_TILE + (t & 15), py = ty * LSR_TILE + strip * 4 + (t >> 4);
-    const bool inside = px < c.W && py < c.H;
-    const float pfx = (float)px, pfy = (float)py;
+    const PixMap pm(c, tile, t + ((blockIdx.x & 3) << 6));
+    const bool inside = pm.px < c.W && pm.py < c.H;
+    const float pfx = (float)pm.px, pfy = (float)pm.py;
     const uint32_t rs = a.tile_start[tile], re = a.tile_start[tile + 1];
     for (int q = 0; q < Dq; q++) acc[q * 64 + t] = 0.f;
 
     float T = 1.0f, cr = 0.f, cg = 0.f, cb = 0.f;
-    uint32_t contributor = 0, last = 0;
+    uint32_t last = 0;
     bool done = !inside;
     for (uint32_t base = rs; base < re; base += 64) {
         if (__syncthreads_count(done) == 64) break;
@@ -225,8 +341,15 @@ __global__ void __launch_bounds__(64) k_render_fwd_quick(RenderArgs a)
         }
         __syncthreads();
         const int n = (int)min(64u, re - base);
-        for (int j = 0; !done && j < n; j++) {
-            contributor++;
+        const uint32_t pos0 = base - rs + 1;
+        bool ok = false;
+        if (t < n) ok = block_overlap(sA[t].x, sA[t].y, __float_as_uint(sB[t].w), pm.bx, pm.by);
+        uint64_t bits = __ballot(ok);
+        while (bits) {
+            if (__ballot(!done) == 0) break;
+            const int j = __builtin_ctzll(bits);
+            bits &= bits - 1;
+            if (done) continue;
             const float4 A = sA[j];
             const float4 B = sB[j];
             const float dx = A.x - pfx, dy = A.y - pfy;
@@ -249,12 +372,12 @@ __global__ void __launch_bounds__(64) k_render_fwd_quick(RenderArgs a)
                 if (q >= 0) acc[q * 64 + t] = fmaf(sW[j * K + k], aT, acc[q * 64 + t]);
             }
             T = test_T;
-            last = contributor;
+            last = pos0 + j;
         }
     }
     if (inside) {
         const size_t HW = (size_t)c.H * c.W;
-        const size_t pix = (size_t)py * c.W + px;
+        const size_t pix = (size_t)pm.py * c.W + pm.px;
         a.final_T[pix] = T;
         a.n_contrib[pix] = last;
         a.out_color[pix] = fmaf(T, c.bg[0], cr);
@@ -302,8 +425,42 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
 int grad_row_width(int D)
 {
     const int nl = lang_set_for(D);
-    const int nv = 9 + (nl > 0 ? nl : 0);
+    const int nv = LSR_GROW_LANG + (nl > 0 ? nl : 0);
     return (nv + 31) / 32 * 32;
+}
+
+// Language-channel gradients on the matrix cores: grad[j][ch] = sum_p aT[j][p] *
+// dL/dout_lang[ch][p] for the 64 pixels p of a wave is a (16 instances x 64
+// pixels) x (64 pixels x 16 channels) product per flush: 16 exact-f32
+// v_mfma_f32_16x16x4_f32 per 16-channel block.  aT rows are staged in LDS
+// (row stride 66 floats: conflict-free A-fragment reads), the dout fragments
+// (B operand) are loaded once per wave into registers.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+#define SLOT_STRIDE 66
+
+template <int NB>
+__device__ __forceinline__ void flush_lang(const float* __restrict__ sw, const uint32_t* __restrict__ sg, int cnt,
+                                           const float (&bf)[NB][16], float* __restrict__ grad, int VP, int D)
+{
+    const int lane = threadIdx.x & 63;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float a[16];
+#pragma unroll
+    for (int t = 0; t < 16; t++) a[t] = sw[(lane & 15) * SLOT_STRIDE + 4 * t + (lane >> 4)];
+#pragma unroll
+    for (int nb = 0; nb < NB; nb++) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 16; t++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], bf[nb][t], acc, 0, 0, 0);
+        const int ch = nb * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int row = 4 * (lane >> 4) + r;
+            const float v = acc[r];
+            if (row < cnt && ch < D && v != 0.f) atomicAdd(grad + (size_t)sg[row] * VP + LSR_GROW_LANG + ch, v);
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 template <int NL>
@@ -311,26 +468,30 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs b)
 {
     constexpr int C = 3 + NL;
     constexpr int F4 = (C + 3) / 4;
-    constexpr int NV = 9 + NL;
+    constexpr bool MF = NL >= 16;               // language grads on MFMA
+    constexpr int NB = MF ? NL / 16 : 1;        // 16-channel blocks
+    constexpr int NV = MF ? 9 : LSR_GROW_LANG + NL;   // values through the wave reduction
     constexpr int NG = (NV + 31) / 32;
     __shared__ float4 sA[256];
     __shared__ float4 sB[256];
     __shared__ float4 sF[256 * F4];
     __shared__ uint32_t sId[256];
+    __shared__ float sW[MF ? 4 : 1][MF ? 16 * SLOT_STRIDE : 1];
+    __shared__ uint32_t sG[MF ? 4 : 1][16];
     __shared__ int sMax;
 
     const RenderArgs& a = b.f;
     const Cam& c = a.cam;
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int tx = tile % c.gx, ty = tile / c.gx;
     const int t = threadIdx.x;
     const int lane = t & 63;
-    const int px = tx * LSR_TILE + (t & 15), py = ty * LSR_TILE + (t >> 4);
-    const bool inside = px < c.W && py < c.H;
-    const float pfx = (float)px, pfy = (float)py;
+    const int w = t >> 6;
+    const PixMap pm(c, tile, t);
+    const bool inside = pm.px < c.W && pm.py < c.H;
+    const float pfx = (float)pm.px, pfy = (float)pm.py;
     const uint32_t rs = a.tile_start[tile];
     const size_t HW = (size_t)c.H * c.W;
-    const size_t pix = (size_t)py * c.W + px;
+    const size_t pix = (size_t)pm.py * c.W + pm.px;
     const int D = a.D;
     const int VP = b.VP;
     const float ddelx_dx = 0.5f * (float)c.W, ddely_dy = 0.5f * (float)c.H;
@@ -348,7 +509,24 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs b)
         for (int k = 0; k < NL; k++)
             if (k < D) Gd[3 + k] = b.dout_lang[k * HW + pix];
     }
-    const float bg_dot = c.bg[0] * Gd[0] + c.bg[1] * Gd[1] + c.bg[2] * Gd[2];
+    // B fragments: lane l holds dout_lang[nb*16 + (l&15)] at block pixel 4t + (l>>4)
+    float bf[NB][16];
+    if (MF) {
+#pragma unroll
+        for (int t4 = 0; t4 < 16; t4++) {
+            const int p = 4 * t4 + (lane >> 4);
+            const int qx = pm.bx + (p & 7), qy = pm.by + (p >> 3);
+            const bool in = qx < c.W && qy < c.H;
+#pragma unroll
+            for (int nb = 0; nb < NB; nb++) {
+                const int ch = nb * 16 + (lane & 15);
+                bf[nb][t4] = (in && ch < D) ? b.dout_lang[(size_t)ch * HW + (size_t)qy * c.W + qx] : 0.f;
+            }
+        }
+    }
+    const float bg0 = c.bg[0], bg1 = c.bg[1], bg2 = c.bg[2];
+    const bool has_bg = (bg0 != 0.f) || (bg1 != 0.f) || (bg2 != 0.f);   // uniform
+    const float bg_dot = bg0 * Gd[0] + bg1 * Gd[1] + bg2 * Gd[2];
 
     if (t == 0) sMax = 0;
     __syncthreads();
@@ -359,6 +537,7 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs b)
 
     float T = T_final;
     float last_alpha = 0.f, last_dot = 0.f, rec = 0.f;
+    int nslot = 0;   // wave-uniform
 
     for (int bs = 0; bs < hi; bs += 256) {
         __syncthreads();
@@ -369,79 +548,119 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs b)
                 sId[t] = gid;
                 sA[t] = a.splatA[gid];
                 sB[t] = a.splatB[gid];
-                float row[F4 * 4];
-                row[0] = a.rgb[3 * gid];
-                row[1] = a.rgb[3 * gid + 1];
-                row[2] = a.rgb[3 * gid + 2];
-#pragma unroll
-                for (int k = 0; k < NL; k++) row[3 + k] = (k < D) ? a.lang[(size_t)gid * D + k] : 0.f;
-#pragma unroll
-                for (int k = 3 + NL; k < F4 * 4; k++) row[k] = 0.f;
-#pragma unroll
-                for (int q = 0; q < F4; q++) sF[t * F4 + q] = make_float4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
+                stage_features<NL, F4>(&sF[t * F4], a.rgb, a.lang, D, gid);
             }
         }
         __syncthreads();
+        // instances j of this batch sit at positions hi-1-(bs+j): only
+        // j >= hi-bs-wmax can be below this wave's largest n_contrib.
         const int n = min(256, hi - bs);
-        for (int j = 0; j < n; j++) {
-            const int p = hi - 1 - (bs + j);   // wave-uniform position
-            if (p >= wmax) continue;
-            const float4 A = sA[j];
-            const float4 B = sB[j];
-            const float dx = A.x - pfx, dy = A.y - pfy;
-            const float power = splat_power(A.z, A.w, B.x, dx, dy);
-            bool contrib = (p < last) && !(power > 0.0f || power < B.z);
-            float G = 0.f, alpha = 0.f;
-            if (contrib) {
-                G = expf_det(power);
-                alpha = fminf(0.99f, B.y * G);
-                contrib = alpha >= 1.0f / 255.0f;
-            }
-            if (!__any(contrib)) continue;
-            float vals[NG * 32];
-#pragma unroll
-            for (int k = 0; k < NG * 32; k++) vals[k] = 0.f;
-            if (contrib) {
-                T = T / (1.f - alpha);
+        const int jmin = max(0, hi - bs - wmax);
+#pragma unroll 1
+        for (int q = jmin & ~63; q < n; q += 64) {
+            uint64_t bits = sub_mask(sA, sB, q, n, pm.bx, pm.by);
+            if (jmin > q) bits &= ~0ull << (jmin - q);
+            while (bits) {
+                const int j = q + (int)__builtin_ctzll(bits);
+                bits &= bits - 1;
+                const int p = hi - 1 - (bs + j);
+                const float4 A = sA[j];
+                const float4 B = sB[j];
+                const float dx = A.x - pfx, dy = A.y - pfy;
+                const float power = splat_power(A.z, A.w, B.x, dx, dy);
+                bool contrib = (p < last) && !(power > 0.0f || power < B.z);
+                float G = 0.f, alpha = 0.f;
+                if (contrib) {
+                    G = expf_det(power);
+                    alpha = fminf(0.99f, B.y * G);
+                    contrib = alpha >= 1.0f / 255.0f;
+                }
+                if (!__any(contrib)) continue;
+                // Branch-free from here: a non-contributing lane carries
+                // alpha = G = 0, so every value it contributes is 0 and its
+                // running state is left unchanged.
+                alpha = contrib ? alpha : 0.f;
+                G = contrib ? G : 0.f;
+                const float one_m = 1.f - alpha;
+                T = T / one_m;
                 const float aT = alpha * T;
                 float f[F4 * 4];
 #pragma unroll
-                for (int q = 0; q < F4; q++) {
-                    const float4 v = sF[j * F4 + q];
-                    f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
+                for (int q4 = 0; q4 < F4; q4++) {
+                    const float4 v = sF[j * F4 + q4];
+                    f[4 * q4] = v.x; f[4 * q4 + 1] = v.y; f[4 * q4 + 2] = v.z; f[4 * q4 + 3] = v.w;
                 }
                 float dot = f[0] * Gd[0];
 #pragma unroll
                 for (int k = 1; k < C; k++) dot = fmaf(f[k], Gd[k], dot);
-                rec = fmaf(last_alpha, last_dot, (1.f - last_alpha) * rec);
-                float dL_dalpha = (dot - rec) * T;
-                dL_dalpha = fmaf(-T_final / (1.f - alpha), bg_dot, dL_dalpha);
-                last_alpha = alpha;
-                last_dot = dot;
+                const float rec_new = fmaf(last_alpha, last_dot, (1.f - last_alpha) * rec);
+                float dL_dalpha = (dot - rec_new) * T;
+                if (has_bg) dL_dalpha = fmaf(-T_final / one_m, bg_dot, dL_dalpha);
+                dL_dalpha = contrib ? dL_dalpha : 0.f;
+                rec = contrib ? rec_new : rec;
+                last_alpha = contrib ? alpha : last_alpha;
+                last_dot = contrib ? dot : last_dot;
                 const float dL_dG = B.y * dL_dalpha;
                 const float gdx = G * dx, gdy = G * dy;
                 const float dG_ddelx = -gdx * A.z - gdy * A.w;
                 const float dG_ddely = -gdy * B.x - gdx * A.w;
-                vals[0] = dL_dG * dG_ddelx * ddelx_dx;
-                vals[1] = dL_dG * dG_ddely * ddely_dy;
-                vals[2] = -0.5f * gdx * dx * dL_dG;
-                vals[3] = -gdx * dy * dL_dG;
-                vals[4] = -0.5f * gdy * dy * dL_dG;
-                vals[5] = G * dL_dalpha;
+                const uint32_t gid = sId[j];
+                float* row = b.grad_acc + (size_t)gid * VP;
+                if (MF) {
+                    float v16[16];
+                    v16[0] = dL_dG * dG_ddelx * ddelx_dx;
+                    v16[1] = dL_dG * dG_ddely * ddely_dy;
+                    v16[2] = -0.5f * gdx * dx * dL_dG;
+                    v16[3] = -gdx * dy * dL_dG;
+                    v16[4] = -0.5f * gdy * dy * dL_dG;
+                    v16[5] = G * dL_dalpha;
+                    v16[6] = aT * Gd[0];
+                    v16[7] = aT * Gd[1];
+                    v16[8] = aT * Gd[2];
 #pragma unroll
-                for (int k = 0; k < C; k++) vals[6 + k] = aT * Gd[k];
-            }
-            float* row = b.grad_acc + (size_t)sId[j] * VP;
+                    for (int k = 9; k < 16; k++) v16[k] = 0.f;
+                    const float sum = wave_reduce16(v16);
+                    const int vi = (lane >> 2) & 15;
+                    if (!(lane & 3) && vi < 9 && sum != 0.f) atomicAdd(row + vi, sum);
+                    // stage this instance's aT column for the MFMA language product
+                    sW[w][nslot * SLOT_STRIDE + lane] = aT;
+                    if (lane == 0) sG[w][nslot] = gid;
+                    if (++nslot == 16) {
+                        flush_lang<NB>(sW[w], sG[w], 16, bf, b.grad_acc, VP, D);
+                        nslot = 0;
+                    }
+                } else {
+                    float vals[NG * 32];
+                    vals[0] = dL_dG * dG_ddelx * ddelx_dx;
+                    vals[1] = dL_dG * dG_ddely * ddely_dy;
+                    vals[2] = -0.5f * gdx * dx * dL_dG;
+                    vals[3] = -gdx * dy * dL_dG;
+                    vals[4] = -0.5f * gdy * dy * dL_dG;
+                    vals[5] = G * dL_dalpha;
+                    vals[6] = aT * Gd[0];
+                    vals[7] = aT * Gd[1];
+                    vals[8] = aT * Gd[2];
 #pragma unroll
-            for (int g = 0; g < NG; g++) {
-                float v32[32];
+                    for (int k = 9; k < NG * 32; k++) vals[k] = 0.f;
 #pragma unroll
-                for (int k = 0; k < 32; k++) v32[k] = vals[g * 32 + k];
-                const float s = wave_reduce32(v32);
-                const int vi = g * 32 + (lane >> 1);
-                if (!(lane & 1) && vi < 9 + D && s != 0.f) atomicAdd(row + vi, s);
+                    for (int k = 0; k < NL; k++) vals[LSR_GROW_LANG + k] = aT * Gd[3 + k];
+#pragma unroll
+                    for (int g = 0; g < NG; g++) {
+                        float v32[32];
+#pragma unroll
+                        for (int k = 0; k < 32; k++) v32[k] = vals[g * 32 + k];
+                        const float sum = wave_reduce32(v32);
+                        const int vi = g * 32 + (lane >> 1);
+                        if (!(lane & 1) && vi < LSR_GROW_LANG + D && sum != 0.f) atomicAdd(row + vi, sum);
+                    }
+                }
             }
         }
+    }
+    if (MF && nslot > 0) {
+        // zero the unused slot rows so stale aT values never enter the product
+        for (int sl = nslot; sl < 16; sl++) sW[w][sl * SLOT_STRIDE + lane] = 0.f;
+        flush_lang<NB>(sW[w], sG[w], nslot, bf, b.grad_acc, VP, D);
     }
 }
 
