@@ -19,6 +19,13 @@
 // (wave, instance) instead of (9 + D) atomics per contributing pixel.
 #include "lsr_internal.h"
 
+#ifndef LSR_BWD_PIPE
+#define LSR_BWD_PIPE 0
+#endif
+#ifndef LSR_BF_REGS
+#define LSR_BF_REGS 1
+#endif
+
 namespace lsr {
 
 // ----------------------------------------------------------- reductions --
@@ -174,22 +181,74 @@ __device__ __forceinline__ uint64_t sub_mask(const float4* sA, const float4* sB,
     return __ballot(ok);
 }
 
+// Work-item mapping for the wave-independent render kernels: one 64-thread
+// workgroup (one wave) per 8x8 block; the four blocks of a tile get
+// consecutive indices inside one XCD's range (xcd_remap), so they share an L2.
+struct WaveTile {
+    int tile, sub;
+    __device__ WaveTile()
+    {
+        const int o = xcd_remap(blockIdx.x, gridDim.x);
+        tile = o >> 2;
+        sub = o & 3;
+    }
+};
+
+// Per-wave LDS staging of one chunk of up to 64 candidate instances.
+template <int F4>
+struct WaveStage {
+    float4 A[64];
+    float4 B[64];
+    float4 F[64 * F4];
+    uint32_t gid[64];
+    int pos[64];
+};
+
+__device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Stage the candidates of one chunk: lane l holds instance (gid, A, B, pos) if
+// valid; instances that may touch the wave's 8x8 block are compacted (order
+// preserved: rank = popcount of lower candidate lanes) into LDS together with
+// their feature rows.  Returns the candidate count (wave-uniform).
+template <int NL, int F4>
+__device__ __forceinline__ int stage_candidates(WaveStage<F4>& st, bool valid, uint32_t gid, int pos, int bx, int by,
+                                                const float4* __restrict__ splatA, const float4* __restrict__ splatB,
+                                                const float* __restrict__ rgb, const float* __restrict__ lang, int D)
+{
+    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+    if (valid) {
+        A = splatA[gid];
+        B = splatB[gid];
+    }
+    const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by);
+    const uint64_t m = __ballot(ok);
+    const int cnt = __popcll(m);
+    if (ok) {
+        const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        st.A[r] = A;
+        st.B[r] = B;
+        st.gid[r] = gid;
+        st.pos[r] = pos;
+        stage_features<NL, F4>(&st.F[r * F4], rgb, lang, D, gid);
+    }
+    wave_lds_fence();
+    return cnt;
+}
+
 template <int NL>
-__global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a)
+__global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
 {
     constexpr int C = 3 + NL;
     constexpr int F4 = (C + 3) / 4;  // float4 per feature row
-    __shared__ float4 sA[256];
-    __shared__ float4 sB[256];
-    __shared__ float4 sF[256 * F4];
+    __shared__ WaveStage<F4> st;
 
     const Cam& c = a.cam;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int t = threadIdx.x;
-    const PixMap pm(c, tile, t);
+    const WaveTile wt;
+    const int lane = threadIdx.x;
+    const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
     const bool inside = pm.px < c.W && pm.py < c.H;
     const float pfx = (float)pm.px, pfy = (float)pm.py;
-    const uint32_t rs = a.tile_start[tile], re = a.tile_start[tile + 1];
+    const uint32_t rs = a.tile_start[wt.tile], re = a.tile_start[wt.tile + 1];
     const int D = a.D;
 
     float T = 1.0f;
@@ -199,83 +258,72 @@ __global__ void __launch_bounds__(256) k_render_fwd(RenderArgs a)
     uint32_t last = 0;
     bool done = !inside;
 
-    for (uint32_t base = rs; base < re; base += 256) {
-        if (__syncthreads_count(done) == 256) break;
-        const uint32_t idx = base + t;
-        if (idx < re) {
-            const uint32_t gid = a.point_list[idx];
-            sA[t] = a.splatA[gid];
-            sB[t] = a.splatB[gid];
-            stage_features<NL, F4>(&sF[t * F4], a.rgb, a.lang, D, gid);
-        }
-        __syncthreads();
-        const int n = (int)min(256u, re - base);
-        const uint32_t pos0 = base - rs + 1;   // contributor index of instance j is pos0 + j
-#pragma unroll 1
-        for (int q = 0; q < n; q += 64) {
-            uint64_t bits = sub_mask(sA, sB, q, n, pm.bx, pm.by);
-            // Two instances per iteration, branch-free per lane: a lane that
-            // skips an instance (exponent cut, alpha < 1/255, saturated or
-            // done) blends it with weight 0 and keeps T.  The two exp chains
-            // are independent (ILP); only T carries from the first to the
-            // second, exactly as in the sequential per-pixel order.
-            while (bits) {
-                if (__ballot(!done) == 0) break;
-                const int j0 = q + (int)__builtin_ctzll(bits);
-                bits &= bits - 1;
-                const bool two = bits != 0;
-                const int j1 = two ? q + (int)__builtin_ctzll(bits) : j0;
-                bits &= bits - 1;
-                const float4 A0 = sA[j0], B0 = sB[j0];
-                const float4 A1 = sA[j1], B1 = sB[j1];
-                const float p0 = splat_power(A0.z, A0.w, B0.x, A0.x - pfx, A0.y - pfy);
-                const float p1 = splat_power(A1.z, A1.w, B1.x, A1.x - pfx, A1.y - pfy);
-                bool ok0 = !done && !(p0 > 0.0f || p0 < B0.z);
-                bool ok1 = two && !done && !(p1 > 0.0f || p1 < B1.z);
-                if (!__any(ok0 || ok1)) continue;
-                const float al0 = fminf(0.99f, B0.y * expf_det(p0));
-                const float al1 = fminf(0.99f, B1.y * expf_det(p1));
-                ok0 = ok0 && !(al0 < 1.0f / 255.0f);
-                ok1 = ok1 && !(al1 < 1.0f / 255.0f);
-                // instance j0
-                {
-                    const float test_T = T * (1.0f - al0);
-                    const bool term = ok0 && (test_T < 0.0001f);
-                    done = done || term;
-                    ok0 = ok0 && !term;
-                    ok1 = ok1 && !term;
-                    const float aT = ok0 ? al0 * T : 0.f;
+    uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
+    for (uint32_t base = rs; base < re; base += 64) {
+        if (__ballot(!done) == 0) break;
+        const uint32_t idx = base + lane;
+        const bool valid = idx < re;
+        const uint32_t gid = next_gid;
+        next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;   // prefetch the next chunk's ids
+        const int n = stage_candidates<NL, F4>(st, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, a.splatA, a.splatB,
+                                               a.rgb, a.lang, D);
+        // Two instances per iteration, branch-free per lane: a lane that
+        // skips an instance (exponent cut, alpha < 1/255, saturated or done)
+        // blends it with weight 0 and keeps T.  The two exp chains are
+        // independent (ILP); T carries from the first to the second exactly
+        // as in the sequential per-pixel order.
+        for (int j0 = 0; j0 < n; j0 += 2) {
+            if (__ballot(!done) == 0) break;
+            const bool two = j0 + 1 < n;
+            const int j1 = two ? j0 + 1 : j0;
+            const float4 A0 = st.A[j0], B0 = st.B[j0];
+            const float4 A1 = st.A[j1], B1 = st.B[j1];
+            const float p0 = splat_power(A0.z, A0.w, B0.x, A0.x - pfx, A0.y - pfy);
+            const float p1 = splat_power(A1.z, A1.w, B1.x, A1.x - pfx, A1.y - pfy);
+            bool ok0 = !done && !(p0 > 0.0f || p0 < B0.z);
+            bool ok1 = two && !done && !(p1 > 0.0f || p1 < B1.z);
+            if (!__any(ok0 || ok1)) continue;
+            const float al0 = fminf(0.99f, B0.y * expf_det(p0));
+            const float al1 = fminf(0.99f, B1.y * expf_det(p1));
+            ok0 = ok0 && !(al0 < 1.0f / 255.0f);
+            ok1 = ok1 && !(al1 < 1.0f / 255.0f);
+            {
+                const float test_T = T * (1.0f - al0);
+                const bool term = ok0 && (test_T < 0.0001f);
+                done = done || term;
+                ok0 = ok0 && !term;
+                ok1 = ok1 && !term;
+                const float aT = ok0 ? al0 * T : 0.f;
 #pragma unroll
-                    for (int f = 0; f < F4; f++) {
-                        const float4 v = sF[j0 * F4 + f];
-                        acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
-                        acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
-                        acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
-                        acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
-                    }
-                    T = ok0 ? test_T : T;
-                    last = ok0 ? pos0 + j0 : last;
+                for (int f = 0; f < F4; f++) {
+                    const float4 v = st.F[j0 * F4 + f];
+                    acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
+                    acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
+                    acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
+                    acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
                 }
-                // instance j1
-                if (__any(ok1)) {
-                    const float test_T = T * (1.0f - al1);
-                    const bool term = ok1 && (test_T < 0.0001f);
-                    done = done || term;
-                    ok1 = ok1 && !term;
-                    const float aT = ok1 ? al1 * T : 0.f;
+                T = ok0 ? test_T : T;
+                last = ok0 ? (uint32_t)st.pos[j0] : last;
+            }
+            if (__any(ok1)) {
+                const float test_T = T * (1.0f - al1);
+                const bool term = ok1 && (test_T < 0.0001f);
+                done = done || term;
+                ok1 = ok1 && !term;
+                const float aT = ok1 ? al1 * T : 0.f;
 #pragma unroll
-                    for (int f = 0; f < F4; f++) {
-                        const float4 v = sF[j1 * F4 + f];
-                        acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
-                        acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
-                        acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
-                        acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
-                    }
-                    T = ok1 ? test_T : T;
-                    last = ok1 ? pos0 + j1 : last;
+                for (int f = 0; f < F4; f++) {
+                    const float4 v = st.F[j1 * F4 + f];
+                    acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
+                    acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
+                    acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
+                    acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
                 }
+                T = ok1 ? test_T : T;
+                last = ok1 ? (uint32_t)st.pos[j1] : last;
             }
         }
+        wave_lds_fence();
     }
     if (inside) {
         const size_t HW = (size_t)c.H * c.W;
@@ -408,12 +456,12 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
         return hipGetLastError();
     }
     switch (lang_set_for(a.D)) {
-        case 0: k_render_fwd<0><<<T, 256, 0, st>>>(a); break;
-        case 4: k_render_fwd<4><<<T, 256, 0, st>>>(a); break;
-        case 8: k_render_fwd<8><<<T, 256, 0, st>>>(a); break;
-        case 16: k_render_fwd<16><<<T, 256, 0, st>>>(a); break;
-        case 32: k_render_fwd<32><<<T, 256, 0, st>>>(a); break;
-        case 64: k_render_fwd<64><<<T, 256, 0, st>>>(a); break;
+        case 0: k_render_fwd<0><<<4 * T, 64, 0, st>>>(a); break;
+        case 4: k_render_fwd<4><<<4 * T, 64, 0, st>>>(a); break;
+        case 8: k_render_fwd<8><<<4 * T, 64, 0, st>>>(a); break;
+        case 16: k_render_fwd<16><<<4 * T, 64, 0, st>>>(a); break;
+        case 32: k_render_fwd<32><<<4 * T, 64, 0, st>>>(a); break;
+        case 64: k_render_fwd<64><<<4 * T, 64, 0, st>>>(a); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -463,8 +511,69 @@ __device__ __forceinline__ void flush_lang(const float* __restrict__ sw, const u
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+// sbf: the wave's dout_lang block in LDS, [channel][pixel] with row stride
+// SLOT_STRIDE; the B fragment of K-step t for lane l is
+// sbf[(nb*16 + (l&15)) * SLOT_STRIDE + 4t + (l>>4)].
+template <int NB>
+__device__ __forceinline__ void flush_lang(const float* __restrict__ sw, const uint32_t* __restrict__ sg, int cnt,
+                                           const float* __restrict__ sbf, float* __restrict__ grad, int VP, int D)
+{
+    const int lane = threadIdx.x & 63;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float a[16];
+#pragma unroll
+    for (int t = 0; t < 16; t++) a[t] = sw[(lane & 15) * SLOT_STRIDE + 4 * t + (lane >> 4)];
+#pragma unroll
+    for (int nb = 0; nb < NB; nb++) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        const float* bb = sbf + (nb * 16 + (lane & 15)) * SLOT_STRIDE + (lane >> 4);
+#pragma unroll
+        for (int t = 0; t < 16; t++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], bb[4 * t], acc, 0, 0, 0);
+        const int ch = nb * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int row = 4 * (lane >> 4) + r;
+            const float v = acc[r];
+            if (row < cnt && ch < D && v != 0.f) atomicAdd(grad + (size_t)sg[row] * VP + LSR_GROW_LANG + ch, v);
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// Reduce one instance's 9 geometric + colour values (v16) over the wave and
+// add them to its gradient row (lanes 4v hold value v).
+__device__ __forceinline__ void reduce_geom(float (&v16)[16], float* __restrict__ row)
+{
+    const int lane = threadIdx.x & 63;
+    const float sum = wave_reduce16(v16);
+    const int vi = (lane >> 2) & 15;
+    if (!(lane & 3) && vi < 9 && sum != 0.f) atomicAdd(row + vi, sum);
+}
+
+// Per-lane gradient values [0,9) of one (pixel, instance) pair (row layout of
+// lsr_device.h); dL/dalpha, G and aT are 0 for a non-contributing lane.
+__device__ __forceinline__ void geom_values(float (&v)[16], float dL_dalpha, float G, float aT, float4 A, float4 B,
+                                            float dx, float dy, float ddelx_dx, float ddely_dy, const float* Gd)
+{
+    const float dL_dG = B.y * dL_dalpha;
+    const float gdx = G * dx, gdy = G * dy;
+    const float dG_ddelx = -gdx * A.z - gdy * A.w;
+    const float dG_ddely = -gdy * B.x - gdx * A.w;
+    v[0] = dL_dG * dG_ddelx * ddelx_dx;
+    v[1] = dL_dG * dG_ddely * ddely_dy;
+    v[2] = -0.5f * gdx * dx * dL_dG;
+    v[3] = -gdx * dy * dL_dG;
+    v[4] = -0.5f * gdy * dy * dL_dG;
+    v[5] = G * dL_dalpha;
+    v[6] = aT * Gd[0];
+    v[7] = aT * Gd[1];
+    v[8] = aT * Gd[2];
+#pragma unroll
+    for (int k = 9; k < 16; k++) v[k] = 0.f;
+}
+
 template <int NL>
-__global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs b)
+__global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs b)
 {
     constexpr int C = 3 + NL;
     constexpr int F4 = (C + 3) / 4;
@@ -472,24 +581,19 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs b)
     constexpr int NB = MF ? NL / 16 : 1;        // 16-channel blocks
     constexpr int NV = MF ? 9 : LSR_GROW_LANG + NL;   // values through the wave reduction
     constexpr int NG = (NV + 31) / 32;
-    __shared__ float4 sA[256];
-    __shared__ float4 sB[256];
-    __shared__ float4 sF[256 * F4];
-    __shared__ uint32_t sId[256];
-    __shared__ float sW[MF ? 4 : 1][MF ? 16 * SLOT_STRIDE : 1];
-    __shared__ uint32_t sG[MF ? 4 : 1][16];
-    __shared__ int sMax;
+    __shared__ WaveStage<F4> st;
+    __shared__ float sW[MF ? 16 * SLOT_STRIDE : 1];
+    __shared__ float sbf[(MF && !LSR_BF_REGS) ? NL * SLOT_STRIDE : 1];
+    __shared__ uint32_t sG[16];
 
     const RenderArgs& a = b.f;
     const Cam& c = a.cam;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int t = threadIdx.x;
-    const int lane = t & 63;
-    const int w = t >> 6;
-    const PixMap pm(c, tile, t);
+    const WaveTile wt;
+    const int lane = threadIdx.x;
+    const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
     const bool inside = pm.px < c.W && pm.py < c.H;
     const float pfx = (float)pm.px, pfy = (float)pm.py;
-    const uint32_t rs = a.tile_start[tile];
+    const uint32_t rs = a.tile_start[wt.tile];
     const size_t HW = (size_t)c.H * c.W;
     const size_t pix = (size_t)pm.py * c.W + pm.px;
     const int D = a.D;
@@ -498,6 +602,8 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs b)
 
     const float T_final = inside ? a.final_T[pix] : 0.f;
     const int last = inside ? (int)a.n_contrib[pix] : 0;
+    const int wmax = wave_max_i(last);
+    if (wmax == 0) return;
     float Gd[F4 * 4];
 #pragma unroll
     for (int k = 0; k < F4 * 4; k++) Gd[k] = 0.f;
@@ -509,7 +615,9 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs b)
         for (int k = 0; k < NL; k++)
             if (k < D) Gd[3 + k] = b.dout_lang[k * HW + pix];
     }
-    // B fragments: lane l holds dout_lang[nb*16 + (l&15)] at block pixel 4t + (l>>4)
+#if LSR_BF_REGS
+    // the MFMA B operand in registers: lane l holds dout_lang[nb*16 + (l&15)]
+    // at block pixel 4t + (l>>4)
     float bf[NB][16];
     if (MF) {
 #pragma unroll
@@ -524,143 +632,130 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs b)
             }
         }
     }
+#define LSR_BFRAG bf
+#else
+    // the MFMA B operand: this wave's dout_lang block in LDS, [channel][pixel]
+    if (MF) {
+#pragma unroll
+        for (int k = 0; k < NL; k++) sbf[k * SLOT_STRIDE + lane] = Gd[3 + k];
+    }
+#define LSR_BFRAG sbf
+#endif
     const float bg0 = c.bg[0], bg1 = c.bg[1], bg2 = c.bg[2];
     const bool has_bg = (bg0 != 0.f) || (bg1 != 0.f) || (bg2 != 0.f);   // uniform
     const float bg_dot = bg0 * Gd[0] + bg1 * Gd[1] + bg2 * Gd[2];
-
-    if (t == 0) sMax = 0;
-    __syncthreads();
-    const int wmax = wave_max_i(last);
-    if (lane == 0) atomicMax(&sMax, wmax);
-    __syncthreads();
-    const int hi = sMax;
 
     float T = T_final;
     float last_alpha = 0.f, last_dot = 0.f, rec = 0.f;
     int nslot = 0;   // wave-uniform
 
-    for (int bs = 0; bs < hi; bs += 256) {
-        __syncthreads();
-        {
-            const int p = hi - 1 - (bs + t);
-            if (p >= 0) {
-                const uint32_t gid = a.point_list[rs + p];
-                sId[t] = gid;
-                sA[t] = a.splatA[gid];
-                sB[t] = a.splatB[gid];
-                stage_features<NL, F4>(&sF[t * F4], a.rgb, a.lang, D, gid);
+    // positions [0, wmax) back to front, 64 per chunk
+    uint32_t next_gid = (wmax - 1 - lane >= 0) ? a.point_list[rs + wmax - 1 - lane] : 0u;
+    for (int c0 = 0; c0 < wmax; c0 += 64) {
+        const int p = wmax - 1 - (c0 + lane);
+        const bool valid = p >= 0;
+        const uint32_t gid = next_gid;
+        next_gid = (p - 64 >= 0) ? a.point_list[rs + p - 64] : 0u;
+        const int n = stage_candidates<NL, F4>(st, valid, gid, p, pm.bx, pm.by, a.splatA, a.splatB, a.rgb, a.lang, D);
+#if LSR_BWD_PIPE
+        // software-pipelined LDS reads: instance j+1's record is in flight
+        // while j is processed
+        float4 An = st.A[0], Bn = st.B[0];
+        int posn = st.pos[0];
+#endif
+        for (int j = 0; j < n; j++) {
+#if LSR_BWD_PIPE
+            const float4 A = An;
+            const float4 B = Bn;
+            const int posj = posn;
+            const int jn = j + 1 < n ? j + 1 : j;
+            An = st.A[jn];
+            Bn = st.B[jn];
+            posn = st.pos[jn];
+            float4 fr[F4];
+#pragma unroll
+            for (int q4 = 0; q4 < F4; q4++) fr[q4] = st.F[j * F4 + q4];
+#else
+            const float4 A = st.A[j];
+            const float4 B = st.B[j];
+            const int posj = st.pos[j];
+#endif
+            const float dx = A.x - pfx, dy = A.y - pfy;
+            const float power = splat_power(A.z, A.w, B.x, dx, dy);
+            bool contrib = (posj < last) && !(power > 0.0f || power < B.z);
+            float G = 0.f, alpha = 0.f;
+            if (contrib) {
+                G = expf_det(power);
+                alpha = fminf(0.99f, B.y * G);
+                contrib = alpha >= 1.0f / 255.0f;
             }
-        }
-        __syncthreads();
-        // instances j of this batch sit at positions hi-1-(bs+j): only
-        // j >= hi-bs-wmax can be below this wave's largest n_contrib.
-        const int n = min(256, hi - bs);
-        const int jmin = max(0, hi - bs - wmax);
-#pragma unroll 1
-        for (int q = jmin & ~63; q < n; q += 64) {
-            uint64_t bits = sub_mask(sA, sB, q, n, pm.bx, pm.by);
-            if (jmin > q) bits &= ~0ull << (jmin - q);
-            while (bits) {
-                const int j = q + (int)__builtin_ctzll(bits);
-                bits &= bits - 1;
-                const int p = hi - 1 - (bs + j);
-                const float4 A = sA[j];
-                const float4 B = sB[j];
-                const float dx = A.x - pfx, dy = A.y - pfy;
-                const float power = splat_power(A.z, A.w, B.x, dx, dy);
-                bool contrib = (p < last) && !(power > 0.0f || power < B.z);
-                float G = 0.f, alpha = 0.f;
-                if (contrib) {
-                    G = expf_det(power);
-                    alpha = fminf(0.99f, B.y * G);
-                    contrib = alpha >= 1.0f / 255.0f;
+            if (!__any(contrib)) continue;
+            // Branch-free from here: a non-contributing lane carries
+            // alpha = G = 0, so every value it contributes is 0 and its
+            // running state is left unchanged.
+            alpha = contrib ? alpha : 0.f;
+            G = contrib ? G : 0.f;
+            const float one_m = 1.f - alpha;
+            T = T / one_m;
+            const float aT = alpha * T;
+            float f[F4 * 4];
+#pragma unroll
+            for (int q4 = 0; q4 < F4; q4++) {
+#if LSR_BWD_PIPE
+                const float4 v = fr[q4];
+#else
+                const float4 v = st.F[j * F4 + q4];
+#endif
+                f[4 * q4] = v.x; f[4 * q4 + 1] = v.y; f[4 * q4 + 2] = v.z; f[4 * q4 + 3] = v.w;
+            }
+            float dot = f[0] * Gd[0];
+#pragma unroll
+            for (int k = 1; k < C; k++) dot = fmaf(f[k], Gd[k], dot);
+            const float rec_new = fmaf(last_alpha, last_dot, (1.f - last_alpha) * rec);
+            float dL_dalpha = (dot - rec_new) * T;
+            if (has_bg) dL_dalpha = fmaf(-T_final / one_m, bg_dot, dL_dalpha);
+            dL_dalpha = contrib ? dL_dalpha : 0.f;
+            rec = contrib ? rec_new : rec;
+            last_alpha = contrib ? alpha : last_alpha;
+            last_dot = contrib ? dot : last_dot;
+            const uint32_t gidj = st.gid[j];
+            float* row = b.grad_acc + (size_t)gidj * VP;
+            float v16[16];
+            geom_values(v16, dL_dalpha, G, aT, A, B, dx, dy, ddelx_dx, ddely_dy, Gd);
+            if (MF) {
+                reduce_geom(v16, row);
+                // stage this instance's aT column for the MFMA language product
+                sW[nslot * SLOT_STRIDE + lane] = aT;
+                if (lane == 0) sG[nslot] = gidj;
+                if (++nslot == 16) {
+                    flush_lang<NB>(sW, sG, 16, LSR_BFRAG, b.grad_acc, VP, D);
+                    nslot = 0;
                 }
-                if (!__any(contrib)) continue;
-                // Branch-free from here: a non-contributing lane carries
-                // alpha = G = 0, so every value it contributes is 0 and its
-                // running state is left unchanged.
-                alpha = contrib ? alpha : 0.f;
-                G = contrib ? G : 0.f;
-                const float one_m = 1.f - alpha;
-                T = T / one_m;
-                const float aT = alpha * T;
-                float f[F4 * 4];
+            } else {
+                float vals[NG * 32];
 #pragma unroll
-                for (int q4 = 0; q4 < F4; q4++) {
-                    const float4 v = sF[j * F4 + q4];
-                    f[4 * q4] = v.x; f[4 * q4 + 1] = v.y; f[4 * q4 + 2] = v.z; f[4 * q4 + 3] = v.w;
-                }
-                float dot = f[0] * Gd[0];
+                for (int k = 0; k < 9; k++) vals[k] = v16[k];
 #pragma unroll
-                for (int k = 1; k < C; k++) dot = fmaf(f[k], Gd[k], dot);
-                const float rec_new = fmaf(last_alpha, last_dot, (1.f - last_alpha) * rec);
-                float dL_dalpha = (dot - rec_new) * T;
-                if (has_bg) dL_dalpha = fmaf(-T_final / one_m, bg_dot, dL_dalpha);
-                dL_dalpha = contrib ? dL_dalpha : 0.f;
-                rec = contrib ? rec_new : rec;
-                last_alpha = contrib ? alpha : last_alpha;
-                last_dot = contrib ? dot : last_dot;
-                const float dL_dG = B.y * dL_dalpha;
-                const float gdx = G * dx, gdy = G * dy;
-                const float dG_ddelx = -gdx * A.z - gdy * A.w;
-                const float dG_ddely = -gdy * B.x - gdx * A.w;
-                const uint32_t gid = sId[j];
-                float* row = b.grad_acc + (size_t)gid * VP;
-                if (MF) {
-                    float v16[16];
-                    v16[0] = dL_dG * dG_ddelx * ddelx_dx;
-                    v16[1] = dL_dG * dG_ddely * ddely_dy;
-                    v16[2] = -0.5f * gdx * dx * dL_dG;
-                    v16[3] = -gdx * dy * dL_dG;
-                    v16[4] = -0.5f * gdy * dy * dL_dG;
-                    v16[5] = G * dL_dalpha;
-                    v16[6] = aT * Gd[0];
-                    v16[7] = aT * Gd[1];
-                    v16[8] = aT * Gd[2];
+                for (int k = 9; k < NG * 32; k++) vals[k] = 0.f;
 #pragma unroll
-                    for (int k = 9; k < 16; k++) v16[k] = 0.f;
-                    const float sum = wave_reduce16(v16);
-                    const int vi = (lane >> 2) & 15;
-                    if (!(lane & 3) && vi < 9 && sum != 0.f) atomicAdd(row + vi, sum);
-                    // stage this instance's aT column for the MFMA language product
-                    sW[w][nslot * SLOT_STRIDE + lane] = aT;
-                    if (lane == 0) sG[w][nslot] = gid;
-                    if (++nslot == 16) {
-                        flush_lang<NB>(sW[w], sG[w], 16, bf, b.grad_acc, VP, D);
-                        nslot = 0;
-                    }
-                } else {
-                    float vals[NG * 32];
-                    vals[0] = dL_dG * dG_ddelx * ddelx_dx;
-                    vals[1] = dL_dG * dG_ddely * ddely_dy;
-                    vals[2] = -0.5f * gdx * dx * dL_dG;
-                    vals[3] = -gdx * dy * dL_dG;
-                    vals[4] = -0.5f * gdy * dy * dL_dG;
-                    vals[5] = G * dL_dalpha;
-                    vals[6] = aT * Gd[0];
-                    vals[7] = aT * Gd[1];
-                    vals[8] = aT * Gd[2];
+                for (int k = 0; k < NL; k++) vals[LSR_GROW_LANG + k] = aT * Gd[3 + k];
 #pragma unroll
-                    for (int k = 9; k < NG * 32; k++) vals[k] = 0.f;
+                for (int g = 0; g < NG; g++) {
+                    float v32[32];
 #pragma unroll
-                    for (int k = 0; k < NL; k++) vals[LSR_GROW_LANG + k] = aT * Gd[3 + k];
-#pragma unroll
-                    for (int g = 0; g < NG; g++) {
-                        float v32[32];
-#pragma unroll
-                        for (int k = 0; k < 32; k++) v32[k] = vals[g * 32 + k];
-                        const float sum = wave_reduce32(v32);
-                        const int vi = g * 32 + (lane >> 1);
-                        if (!(lane & 1) && vi < LSR_GROW_LANG + D && sum != 0.f) atomicAdd(row + vi, sum);
-                    }
+                    for (int k = 0; k < 32; k++) v32[k] = vals[g * 32 + k];
+                    const float sum = wave_reduce32(v32);
+                    const int vi = g * 32 + (lane >> 1);
+                    if (!(lane & 1) && vi < LSR_GROW_LANG + D && sum != 0.f) atomicAdd(row + vi, sum);
                 }
             }
         }
+        wave_lds_fence();
     }
     if (MF && nslot > 0) {
         // zero the unused slot rows so stale aT values never enter the product
-        for (int sl = nslot; sl < 16; sl++) sW[w][sl * SLOT_STRIDE + lane] = 0.f;
-        flush_lang<NB>(sW[w], sG[w], nslot, bf, b.grad_acc, VP, D);
+        for (int sl = nslot; sl < 16; sl++) sW[sl * SLOT_STRIDE + lane] = 0.f;
+        flush_lang<NB>(sW, sG, nslot, LSR_BFRAG, b.grad_acc, VP, D);
     }
 }
 
@@ -669,12 +764,12 @@ hipError_t launch_render_bwd(const RenderBwdArgs& b, hipStream_t st)
     const int T = b.f.cam.gx * b.f.cam.gy;
     if (T == 0) return hipSuccess;
     switch (lang_set_for(b.f.D)) {
-        case 0: k_render_bwd<0><<<T, 256, 0, st>>>(b); break;
-        case 4: k_render_bwd<4><<<T, 256, 0, st>>>(b); break;
-        case 8: k_render_bwd<8><<<T, 256, 0, st>>>(b); break;
-        case 16: k_render_bwd<16><<<T, 256, 0, st>>>(b); break;
-        case 32: k_render_bwd<32><<<T, 256, 0, st>>>(b); break;
-        case 64: k_render_bwd<64><<<T, 256, 0, st>>>(b); break;
+        case 0: k_render_bwd<0><<<4 * T, 64, 0, st>>>(b); break;
+        case 4: k_render_bwd<4><<<4 * T, 64, 0, st>>>(b); break;
+        case 8: k_render_bwd<8><<<4 * T, 64, 0, st>>>(b); break;
+        case 16: k_render_bwd<16><<<4 * T, 64, 0, st>>>(b); break;
+        case 32: k_render_bwd<32><<<4 * T, 64, 0, st>>>(b); break;
+        case 64: k_render_bwd<64><<<4 * T, 64, 0, st>>>(b); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

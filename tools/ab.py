@@ -1,0 +1,57 @@
+"""A/B timing of liblsr variants in ONE process: each variant's library is
+loaded under its own name and the cfg3 fwd+bwd stage times are measured in
+interleaved rounds (cdna guide §5.4 rule 24).  Usage: python tools/ab.py name=path.so ..."""
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from diff_gaussian_rasterization import GaussianRasterizer  # noqa: E402
+from langsplatv2_amd import _lib  # noqa: E402
+from langsplatv2_amd.scenes import CONFIGS, make_camera, make_gaussians  # noqa: E402
+import bench  # noqa: E402
+
+variants = [a.split("=", 1) for a in sys.argv[1:]]
+libs = {name: _lib.load(path) for name, path in variants}
+cfg = CONFIGS[3]
+D = int(os.environ.get("LSR_D", cfg["lang_dim"]))
+dev = torch.device("cuda:0")
+cam = make_camera(cfg["W"], cfg["H"])
+g0 = make_gaussians(cfg["N"], cam, seed=0, sh_degree=3, lang_dim=D)
+keys = ("means3D", "shs", "opacities", "scales", "rotations", "language_feature_precomp")
+g = {k: g0[k].to(dev).requires_grad_(True) for k in keys}
+g["means2D"] = torch.zeros_like(g["means3D"], requires_grad=True)
+r = GaussianRasterizer(bench.settings(cam, dev, 3, True))
+dc = torch.randn(3, cfg["H"], cfg["W"], device=dev)
+dl = torch.randn(D, cfg["H"], cfg["W"], device=dev)
+
+
+def run(lib, steps):
+    _lib._lib = lib
+    lib.lsr_profile_reset()
+    lib.lsr_profile_enable(1)
+    for _ in range(steps):
+        for p in g.values():
+            p.grad = None
+        c, l, _ = r(means3D=g["means3D"], means2D=g["means2D"], opacities=g["opacities"], shs=g["shs"],
+                    language_feature_precomp=g["language_feature_precomp"], scales=g["scales"],
+                    rotations=g["rotations"])
+        torch.autograd.backward([c, l], [dc, dl])
+    torch.cuda.synchronize()
+    lib.lsr_profile_enable(0)
+    q = _lib.profile_query()
+    return {k: ms / n for k, (ms, n) in q.items() if n}
+
+
+res = {name: [] for name, _ in variants}
+for name, _ in variants:
+    run(libs[name], 3)
+for rnd in range(5):
+    for name, _ in variants:
+        res[name].append(run(libs[name], 5))
+for name, _ in variants:
+    stages = res[name][0].keys()
+    med = {k: statistics.median(x[k] for x in res[name]) for k in stages}
+    print(name, " ".join(f"{k}={v:.4f}" for k, v in med.items()), f"SUM={sum(med.values()):.4f}")
