@@ -34,7 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer  # noqa: E402
-from langsplatv2_amd import _lib, layout, rasterizer  # noqa: E402
+from langsplatv2_amd import _lib, dp, layout, rasterizer  # noqa: E402
 from langsplatv2_amd.scenes import CONFIGS, make_camera, make_gaussians  # noqa: E402
 
 METRIC = "frames/s fwd+bwd @ 1M Gaussians 1080p 3+16ch; achieved HBM GB/s"
@@ -167,7 +167,7 @@ def main():
     cfg = CONFIGS[args.config]
     N, W, H, D, deg = cfg["N"], cfg["W"], cfg["H"], cfg["lang_dim"], cfg["sh_degree"]
     # one view per rank: yaw offsets within +-20 degrees, Gaussians replicated (seed 0)
-    yaw = 0.0 if world == 1 else -20.0 + 40.0 * rank / max(world - 1, 1)
+    yaw = dp.rank_yaw(rank, world)
     cam0 = make_camera(W, H)
     cam = make_camera(W, H, yaw_deg=yaw)
     gcpu = make_gaussians(N, cam0, seed=0, sh_degree=deg, lang_dim=D)
@@ -180,18 +180,19 @@ def main():
     dlang = torch.randn((D, H, W), generator=gen).to(dev)
     rs = settings(cam, dev, deg, True)
     rast = GaussianRasterizer(rs)
+    leaves = [g[k] for k in leaf_keys]
+    exch = dp.ViewShardedExchange(leaves, with_stats=True) if world > 1 else None
 
     def step():
         for p in params:
             p.grad = None
-        color, lang, _ = rast(means3D=g["means3D"], means2D=g["means2D"], opacities=g["opacities"], shs=g["shs"],
-                              language_feature_precomp=g["language_feature_precomp"], scales=g["scales"],
-                              rotations=g["rotations"])
+        color, lang, radii = rast(means3D=g["means3D"], means2D=g["means2D"], opacities=g["opacities"],
+                                  shs=g["shs"], language_feature_precomp=g["language_feature_precomp"],
+                                  scales=g["scales"], rotations=g["rotations"])
         torch.autograd.backward([color, lang], [dcolor, dlang])
-        if world > 1:
-            works = [dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, async_op=True) for p in params]
-            for w_ in works:
-                w_.wait()
+        if exch is not None:
+            # one flat all-reduce(SUM) of every gradient + densification stats, one MAX of radii
+            exch.exchange([p.grad for p in leaves], g["means2D"].grad, radii)
 
     for _ in range(args.warmup):
         step()
@@ -251,6 +252,8 @@ def main():
                 "global_batch": world, "parallelism": f"dp{world} (views sharded, RCCL all-reduce of grads)"
                 if world > 1 else "single GPU",
             },
+            "exchange": ({"bucket_bytes": exch.bucket.nbytes, **dp.allreduce_bound_ms(exch.bucket.nbytes, world)}
+                         if exch is not None else None),
             "roofline": {
                 "bound": "hbm",
                 "kernel": dom,

@@ -174,7 +174,14 @@ static void ewa_cov2D(const ewa_t* e, const float* c, float* a, float* b, float*
 }
 
 /* SH → RGB, term order of utils/sh_utils.py:57-112 (degrees 0..3). */
+static void sh_eval(int deg, const float* sh /* M*3 */, const float* dir, float* out);
 static void sh_to_rgb(int deg, const float* sh /* M*3 */, const float* dir, float* out)
+{
+    sh_eval(deg, sh, dir, out);
+    for (int ch = 0; ch < 3; ch++) out[ch] = out[ch] + 0.5f;
+}
+
+static void sh_eval(int deg, const float* sh /* M*3 */, const float* dir, float* out)
 {
     float x = dir[0], y = dir[1], z = dir[2];
     for (int ch = 0; ch < 3; ch++) {
@@ -197,8 +204,25 @@ static void sh_to_rgb(int deg, const float* sh /* M*3 */, const float* dir, floa
             }
         }
 #undef S
-        out[ch] = r + 0.5f;
+        out[ch] = r;
     }
+}
+
+/* Primitive entry points (golden-vector tests against the reference's own
+ * eval_sh / build_rotation / build_scaling_rotation). */
+void lso_sh_eval(int deg, int N, int M, const float* sh, const float* dirs, float* out)
+{
+    for (int i = 0; i < N; i++) sh_eval(deg, sh + (size_t)i * M * 3, dirs + 3 * i, out + 3 * i);
+}
+
+void lso_quat_to_R(int N, const float* q, float* R)
+{
+    for (int i = 0; i < N; i++) quat_to_R(q + 4 * i, R + 9 * i);
+}
+
+void lso_cov3D(int N, const float* s, float mod, const float* q, float* cov)
+{
+    for (int i = 0; i < N; i++) compute_cov3D(s + 3 * i, mod, q + 4 * i, cov + 6 * i);
 }
 
 static inline void sh_dir(const float* mean, const float* campos, float* dir, float* dir_orig)

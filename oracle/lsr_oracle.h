@@ -138,6 +138,12 @@ void lso_preprocess_bwd(const lso_settings* s, const lso_inputs* in, const lso_g
  * kernels: Cody-Waite reduction + degree-7 Taylor in fmaf. */
 float lso_expf(float x);
 
+/* Primitives: SH evaluation (sh: N*M*3, no +0.5), quaternion -> row-major R,
+ * packed covariance (R S)(R S)^T with S = diag(mod * s). */
+void lso_sh_eval(int deg, int N, int M, const float* sh, const float* dirs, float* out);
+void lso_quat_to_R(int N, const float* q, float* R);
+void lso_cov3D(int N, const float* s, float mod, const float* q, float* cov);
+
 #ifdef __cplusplus
 }
 #endif

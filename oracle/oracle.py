@@ -209,3 +209,26 @@ def backward(pb: Problem, fwd: dict, dout_color: np.ndarray, dout_lang: np.ndarr
 
 def expf(x: float) -> float:
     return float(load().lso_expf(ctypes.c_float(x)))
+
+
+def sh_eval(deg: int, sh_nm3: np.ndarray, dirs: np.ndarray) -> np.ndarray:
+    sh = np.ascontiguousarray(sh_nm3, np.float32)
+    d = np.ascontiguousarray(dirs, np.float32)
+    out = np.zeros((sh.shape[0], 3), np.float32)
+    load().lso_sh_eval(int(deg), sh.shape[0], sh.shape[1], _p(sh), _p(d), _p(out))
+    return out
+
+
+def quat_to_R(q: np.ndarray) -> np.ndarray:
+    q = np.ascontiguousarray(q, np.float32)
+    R = np.zeros((q.shape[0], 3, 3), np.float32)
+    load().lso_quat_to_R(q.shape[0], _p(q), _p(R))
+    return R
+
+
+def cov3D(s: np.ndarray, q: np.ndarray, mod: float = 1.0) -> np.ndarray:
+    s = np.ascontiguousarray(s, np.float32)
+    q = np.ascontiguousarray(q, np.float32)
+    out = np.zeros((s.shape[0], 6), np.float32)
+    load().lso_cov3D(s.shape[0], _p(s), ctypes.c_float(mod), _p(q), _p(out))
+    return out

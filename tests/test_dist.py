@@ -1,0 +1,113 @@
+"""world_size-2 gloo tests of the view-sharded data-parallel exchange
+(langsplatv2_amd/dp.py) on CPU.  Each rank's per-view
+gradients come from the oracle (the checker), so the test covers exactly the
+exchange logic bench.py runs over RCCL on GPUs."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from langsplatv2_amd import dp
+
+PARAM_KEYS = ("means3D", "shs", "opacities", "scales", "rotations", "language_feature_precomp")
+GRAD_KEYS = {"means3D": "dmeans3D", "shs": "dsh", "opacities": "dopacity", "scales": "dscales",
+             "rotations": "drot", "language_feature_precomp": "dlang"}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _view_grads(rank, world):
+    """Oracle forward+backward of rank's view of the shared (seed 0) cloud."""
+    from harness import make_case
+    from oracle import oracle as O
+    case = make_case(300, 64, 48, seed=0, sh_degree=3, lang_dim=4, yaw=dp.rank_yaw(rank, world))
+    for k in ("scales",):
+        case["g"][k] = case["g"][k] * 5
+    pb = O.Problem(case["cam"], case["g"], bg=case["bg"])
+    fwd = O.forward(pb)
+    rng = np.random.default_rng(1 + rank)
+    dC = rng.standard_normal((3, 48, 64)).astype(np.float32)
+    dL = rng.standard_normal((4, 48, 64)).astype(np.float32)
+    bwd = O.backward(pb, fwd, dC, dL)
+    grads = []
+    for k in PARAM_KEYS:
+        v = torch.from_numpy(np.ascontiguousarray(bwd[GRAD_KEYS[k]]))
+        grads.append(v.view(case["g"][k].shape))
+    return case, grads, torch.from_numpy(bwd["dmean2D"]), torch.from_numpy(fwd["radii"])
+
+
+def _worker(rank, world, port, tests_dir):
+    import sys
+    sys.path.insert(0, tests_dir)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        case, grads, m2d, radii = _view_grads(rank, world)
+        params = [case["g"][k] for k in PARAM_KEYS]
+        ex = dp.ViewShardedExchange(params, with_stats=True)
+        red, stats, max_r = ex.exchange(grads, m2d, radii)
+
+        # expected: every rank's view, summed in rank order (= accum_iter=world on one GPU)
+        views = [_view_grads(r, world) for r in range(world)]
+        for i, k in enumerate(PARAM_KEYS):
+            exp = views[0][1][i].clone()
+            for r in range(1, world):
+                exp = exp + views[r][1][i]
+            assert torch.equal(red[i], exp), k
+            assert red[i].shape == params[i].shape
+        exp_stats = sum(dp.densify_increment(v[2], v[3]) for v in views)
+        assert torch.equal(stats, exp_stats)
+        exp_r = views[0][3].clone()
+        for v in views[1:]:
+            exp_r = torch.maximum(exp_r, v[3])
+        assert torch.equal(max_r, exp_r)
+        # both views are non-trivial and differ (the shards really are different views)
+        assert not torch.equal(views[0][1][0], views[1][1][0])
+        assert float(stats[:, 1].max()) == world
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_view_sharded_exchange_gloo_world2(oracle_lib):
+    tests_dir = os.path.dirname(os.path.abspath(__file__))
+    mp.spawn(_worker, args=(2, _free_port(), tests_dir), nprocs=2, join=True)
+
+
+def test_grad_bucket_roundtrip():
+    like = [torch.zeros(5, 3), torch.zeros(5, 16, 3), torch.zeros(5, 1)]
+    b = dp.GradBucket(like, stats_rows=5)
+    gs = [torch.randn(5, 3), None, torch.randn(5, 1)]
+    st = torch.randn(5, 2)
+    b.pack(gs, st)
+    v = b.views()
+    assert torch.equal(v[0], gs[0]) and torch.equal(v[2], gs[2]) and not v[1].any()
+    assert torch.equal(b.stats(), st)
+    assert b.nbytes == 4 * (15 + 240 + 5 + 10)
+    with pytest.raises(ValueError):
+        b.pack([torch.zeros(4, 3), None, None])
+
+
+def test_view_schedule_partitions_views():
+    for world in (1, 2, 4, 8):
+        got = [dp.view_schedule(64, world, r, seed=3) for r in range(world)]
+        flat = sorted(v for g in got for v in g)
+        assert flat == list(range(64))
+        assert all(len(g) == 64 // world for g in got)
+    assert dp.view_schedule(10, 2, 0, epoch=0) != dp.view_schedule(10, 2, 0, epoch=1)
+
+
+def test_rank_yaw_and_bounds():
+    assert dp.rank_yaw(0, 1) == 0.0
+    ys = [dp.rank_yaw(r, 8) for r in range(8)]
+    assert ys[0] == -20.0 and ys[-1] == 20.0 and ys == sorted(ys)
+    b = dp.allreduce_bound_ms(256 << 20, 8)
+    assert 2.5 < b["ring_1link_ms"] < 3.2 and b["all_links_ms"] < b["ring_1link_ms"]

@@ -1,0 +1,313 @@
+"""Pins the C oracle (oracle/lsr_oracle.c) against an independent float64
+torch restatement of the same algorithm, differentiated by autograd.
+
+The restatement follows SURVEY.md Appendix A (3DGS-lineage rasterizer, the
+reference's rasterizer submodule being absent from the checkout) and encodes
+the upstream backward conventions explicitly so autograd reproduces them:
+  * alpha = min(0.99, o*G) with a straight-through gradient,
+  * the +-1.3*tanfov clamp of t.x/t.y: the clamped coordinate is a constant
+    (no gradient to the mean) but J is still differentiated w.r.t. t.z,
+  * SH colour clamp at 0 zeroes the clamped channel's gradient,
+  * means2D gradient is d/d(NDC xy).
+Integer decisions (visibility, radii, tile membership, depth order) are taken
+from the oracle; everything differentiable is recomputed in float64.
+
+Tolerances (stated here): forward 2e-5 absolute on
+[0,1]-range images (fp32 oracle vs fp64); gradients 2e-5 x max|ref| + 1e-6
+(fp32 per-pair terms vs fp64 chain rule).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from harness import make_case, oracle_problem
+
+FWD_ATOL = 2e-5
+GRAD_RTOL = 2e-5
+GRAD_ATOL = 1e-6
+
+SH_C0 = 0.28209479177387814
+SH_C1 = 0.4886025119029199
+SH_C2 = [1.0925484305920792, -1.0925484305920792, 0.31539156525252005, -1.0925484305920792, 0.5462742152960396]
+SH_C3 = [-0.5900435899266435, 2.890611442640554, -0.4570457994644658, 0.3731763325901154, -0.4570457994644658,
+         1.445305721320277, -0.5900435899266435]
+
+
+def sh_eval_t(deg, sh, d):
+    """sh: (N, M, 3) ; d: (N, 3) unit directions -> (N, 3)."""
+    x, y, z = d[:, 0:1], d[:, 1:2], d[:, 2:3]
+    r = SH_C0 * sh[:, 0]
+    if deg > 0:
+        r = r - SH_C1 * y * sh[:, 1] + SH_C1 * z * sh[:, 2] - SH_C1 * x * sh[:, 3]
+    if deg > 1:
+        xx, yy, zz, xy, yz, xz = x * x, y * y, z * z, x * y, y * z, x * z
+        r = (r + SH_C2[0] * xy * sh[:, 4] + SH_C2[1] * yz * sh[:, 5] + SH_C2[2] * (2 * zz - xx - yy) * sh[:, 6]
+             + SH_C2[3] * xz * sh[:, 7] + SH_C2[4] * (xx - yy) * sh[:, 8])
+    if deg > 2:
+        r = (r + SH_C3[0] * y * (3 * xx - yy) * sh[:, 9] + SH_C3[1] * xy * z * sh[:, 10]
+             + SH_C3[2] * y * (4 * zz - xx - yy) * sh[:, 11] + SH_C3[3] * z * (2 * zz - 3 * xx - 3 * yy) * sh[:, 12]
+             + SH_C3[4] * x * (4 * zz - xx - yy) * sh[:, 13] + SH_C3[5] * z * (xx - yy) * sh[:, 14]
+             + SH_C3[6] * x * (xx - 3 * yy) * sh[:, 15])
+    return r
+
+
+def quat_R(q):
+    r, x, y, z = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+    return torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - r * z), 2 * (x * z + r * y),
+                        2 * (x * y + r * z), 1 - 2 * (x * x + z * z), 2 * (y * z - r * x),
+                        2 * (x * z - r * y), 2 * (y * z + r * x), 1 - 2 * (x * x + y * y)], 1).view(-1, 3, 3)
+
+
+def restated(case, fwd, params):
+    """float64 forward of the whole path; returns (color, lang, T_final, ndc)."""
+    cam, g = case["cam"], case["g"]
+    W, H = cam["W"], cam["H"]
+    V = cam["viewmatrix"].double()
+    P = cam["projmatrix"].double()
+    tfx, tfy = cam["tanfovx"], cam["tanfovy"]
+    fx, fy = W / (2 * tfx), H / (2 * tfy)
+    m = params["means3D"]
+    N = m.shape[0]
+    ph1 = torch.cat([m, torch.ones(N, 1, dtype=m.dtype)], 1)
+    pv = ph1 @ V[:, :3]
+    ph = ph1 @ P
+    pw = 1.0 / (ph[:, 3:4] + 1e-7)
+    ndc = ph[:, :2] * pw
+    pix = torch.stack([((ndc[:, 0] + 1) * W - 1) * 0.5, ((ndc[:, 1] + 1) * H - 1) * 0.5], 1)
+
+    if "cov3D_precomp" in params:
+        c = params["cov3D_precomp"]
+        Sig = torch.stack([c[:, 0], c[:, 1], c[:, 2], c[:, 1], c[:, 3], c[:, 4], c[:, 2], c[:, 4], c[:, 5]],
+                          1).view(-1, 3, 3)
+    else:
+        L = quat_R(params["rotations"]) @ torch.diag_embed(params["scales"] * case["scale_modifier"])
+        Sig = L @ L.transpose(1, 2)
+
+    tz = pv[:, 2]
+    outs = []
+    for k, (lim, f) in enumerate(((1.3 * tfx, fx), (1.3 * tfy, fy))):
+        t = pv[:, k]
+        ttz = t / tz
+        clamped = (ttz < -lim) | (ttz > lim)
+        t_used = torch.where(clamped, (ttz.clamp(-lim, lim) * tz).detach(), t)
+        outs.append((f / tz, -(f * t_used) / (tz * tz)))
+    (J00, J02), (J11, J12) = outs
+    Wm = V[:3, :3].T        # W[r][j] = view[j*4 + r]
+    T0 = J00[:, None] * Wm[0] + J02[:, None] * Wm[2]
+    T1 = J11[:, None] * Wm[1] + J12[:, None] * Wm[2]
+    a = torch.einsum("ni,nij,nj->n", T0, Sig, T0) + 0.3
+    b = torch.einsum("ni,nij,nj->n", T0, Sig, T1)
+    cc = torch.einsum("ni,nij,nj->n", T1, Sig, T1) + 0.3
+    det = a * cc - b * b
+    conic = torch.stack([cc / det, -b / det, a / det], 1)
+
+    if "colors_precomp" in params:
+        rgb = params["colors_precomp"]
+    else:
+        d = m - cam["campos"].double()
+        d = d / d.norm(dim=1, keepdim=True)
+        rgb = torch.clamp_min(sh_eval_t(g["sh_degree"], params["shs"], d) + 0.5, 0.0)
+    opac = params["opacities"][:, 0]
+    lang = params.get("language_feature_precomp")
+
+    # integer decisions from the oracle
+    radii = fwd["radii"]
+    gxn = (W + 15) // 16
+    Ttiles = fwd["ranges"].shape[0]
+    member = np.zeros((N, Ttiles), bool)
+    for t in range(Ttiles):
+        s, e = fwd["ranges"][t]
+        member[fwd["point_list"][s:e], t] = True
+    order = [i for i in np.lexsort((np.arange(N), fwd["depth"])) if radii[i] > 0]
+
+    ys, xs = np.mgrid[0:H, 0:W]
+    tile_of = torch.from_numpy(((ys // 16) * gxn + xs // 16).reshape(-1))
+    pfx = torch.from_numpy(xs.reshape(-1)).double()
+    pfy = torch.from_numpy(ys.reshape(-1)).double()
+    npx = H * W
+    Tt = torch.ones(npx, dtype=torch.float64)
+    done = torch.zeros(npx, dtype=torch.bool)
+    C = torch.zeros(3, npx, dtype=torch.float64)
+    D = lang.shape[1] if lang is not None else 0
+    Lg = torch.zeros(D, npx, dtype=torch.float64)
+    bg = torch.tensor(case["bg"], dtype=torch.float64)
+    for j in order:
+        inrect = torch.from_numpy(member[j])[tile_of]
+        dx = pix[j, 0] - pfx
+        dy = pix[j, 1] - pfy
+        power = -0.5 * (conic[j, 0] * dx * dx + conic[j, 2] * dy * dy) - conic[j, 1] * dx * dy
+        G = torch.exp(power)
+        araw = opac[j] * G
+        alpha = araw + (torch.clamp_max(araw, 0.99) - araw).detach()
+        with torch.no_grad():
+            valid = inrect & (power <= 0) & (alpha >= 1.0 / 255.0) & ~done
+            stop = valid & (Tt * (1 - alpha) < 1e-4)
+            contrib = valid & ~stop
+            done = done | stop
+        w = torch.where(contrib, alpha * Tt, torch.zeros_like(Tt))
+        C = C + rgb[j][:, None] * w[None]
+        if D:
+            Lg = Lg + lang[j][:, None] * w[None]
+        Tt = torch.where(contrib, Tt * (1 - alpha), Tt)
+    color = (C + Tt[None] * bg[:, None]).view(3, H, W)
+    return color, Lg.view(D, H, W), Tt.view(H, W), ndc
+
+
+ORACLE_CASES = {
+    "sh3_lang8": dict(N=70, W=64, H=48, seed=3, sh_degree=3, lang_dim=8),
+    "rgb_bg": dict(N=60, W=48, H=40, seed=5, sh_degree=None, bg=(0.2, 0.5, 0.9)),
+    "cov_precomp": dict(N=50, W=40, H=40, seed=7, sh_degree=1, cov_precomp=True, lang_dim=3),
+    "scalemod_yaw": dict(N=60, W=56, H=40, seed=9, sh_degree=2, scale_modifier=0.7, yaw=25.0),
+}
+
+
+def _grow(case, factor=6.0, seed=0):
+    """Bigger splats for dense overlap, plus a few Gaussians beyond the
+    1.3*tanfov clamp (large enough to still touch the image)."""
+    g = case["g"]
+    if "scales" in g:
+        g["scales"] = g["scales"] * factor
+    else:
+        g["cov3D_precomp"] = g["cov3D_precomp"] * factor * factor
+    cam = case["cam"]
+    gen = torch.Generator().manual_seed(seed)
+    for k in range(3):
+        z = 3.0 + k
+        sgn = 1.0 if k % 2 == 0 else -1.0
+        g["means3D"][k] = torch.tensor([sgn * 1.45 * z * cam["tanfovx"], 0.3 * k * cam["tanfovy"], z])
+        if "scales" in g:
+            g["scales"][k] = 0.6 + 0.1 * torch.rand(3, generator=gen)
+        g["opacities"][k] = 0.8
+    return case
+
+
+def _oracle_fwd_bwd(case, dC, dL):
+    from oracle import oracle as O
+    pb = oracle_problem(case)
+    fwd = O.forward(pb)
+    bwd = O.backward(pb, fwd, dC, dL)
+    return fwd, bwd
+
+
+@pytest.mark.parametrize("name", list(ORACLE_CASES))
+def test_oracle_matches_float64_autograd(oracle_lib, name):
+    kw = dict(ORACLE_CASES[name])
+    bg = kw.pop("bg", (0.0, 0.0, 0.0))
+    smod = kw.pop("scale_modifier", 1.0)
+    case = _grow(make_case(bg=bg, scale_modifier=smod, **kw), seed=kw["seed"])
+    g = case["g"]
+    W, H = case["cam"]["W"], case["cam"]["H"]
+    rng = np.random.default_rng(kw["seed"])
+    dC = rng.standard_normal((3, H, W)).astype(np.float32)
+    D = g["language_feature_precomp"].shape[1] if "language_feature_precomp" in g else 0
+    dL = rng.standard_normal((D, H, W)).astype(np.float32) if D else None
+    fwd, bwd = _oracle_fwd_bwd(case, dC, dL)
+    assert (fwd["radii"] > 0).sum() > 10
+    assert fwd["num_rendered"] > 0
+
+    params = {}
+    for k in ("means3D", "shs", "colors_precomp", "opacities", "scales", "rotations", "cov3D_precomp",
+              "language_feature_precomp"):
+        if k in g:
+            params[k] = g[k].double().clone().requires_grad_(True)
+    color, lang, Tf, ndc = restated(case, fwd, params)
+    ndc.retain_grad()
+
+    np.testing.assert_allclose(fwd["color"], color.detach().numpy(), atol=FWD_ATOL, rtol=0)
+    np.testing.assert_allclose(fwd["final_T"], Tf.detach().numpy(), atol=FWD_ATOL, rtol=0)
+    if D:
+        np.testing.assert_allclose(fwd["lang"], lang.detach().numpy(), atol=FWD_ATOL, rtol=0)
+
+    loss = (color * torch.from_numpy(dC).double()).sum()
+    if D:
+        loss = loss + (lang * torch.from_numpy(dL).double()).sum()
+    loss.backward()
+
+    def close(name, got, ref):
+        got = np.asarray(got, np.float64).reshape(-1)
+        ref = np.asarray(ref, np.float64).reshape(-1)
+        tol = GRAD_ATOL + GRAD_RTOL * max(1e-3, np.abs(ref).max(initial=0))
+        err = np.abs(got - ref).max(initial=0)
+        assert err <= tol, f"{name}: max|err| {err:.3e} > {tol:.3e}"
+
+    close("means2D", bwd["dmean2D"][:, :2], ndc.grad.numpy())
+    close("means3D", bwd["dmeans3D"], params["means3D"].grad.numpy())
+    close("opacities", bwd["dopacity"], params["opacities"].grad.numpy())
+    if "shs" in params:
+        close("shs", bwd["dsh"], params["shs"].grad.numpy())
+    if "colors_precomp" in params:
+        close("colors_precomp", bwd["dcolors"], params["colors_precomp"].grad.numpy())
+    if "scales" in params:
+        close("scales", bwd["dscales"], params["scales"].grad.numpy())
+        close("rotations", bwd["drot"], params["rotations"].grad.numpy())
+    if "cov3D_precomp" in params:
+        close("cov3D_precomp", bwd["dcov3D"], params["cov3D_precomp"].grad.numpy())
+    if D:
+        close("language_feature_precomp", bwd["dlang"], params["language_feature_precomp"].grad.numpy())
+
+
+def test_clamp_quirk_is_exercised(oracle_lib):
+    """The grown cases put visible Gaussians beyond the 1.3*tanfov clamp."""
+    kw = dict(ORACLE_CASES["sh3_lang8"])
+    case = _grow(make_case(**kw), seed=kw["seed"])
+    from oracle import oracle as O
+    fwd = O.forward(oracle_problem(case))
+    m = case["g"]["means3D"][:3].numpy()
+    assert np.all(np.abs(m[:, 0] / m[:, 2]) > 1.3 * case["cam"]["tanfovx"])
+    assert np.all(fwd["radii"][:3] > 0)
+
+
+def test_expf_accuracy(oracle_lib):
+    xs = np.concatenate([np.linspace(-30.0, 0.0, 20001), -np.logspace(-8, 1.4, 2001)]).astype(np.float32)
+    got = np.array([oracle_lib.expf(float(x)) for x in xs], np.float64)
+    ref = np.exp(xs.astype(np.float64))
+    rel = np.abs(got - ref) / ref
+    assert rel.max() < 4e-7, rel.max()   # < 4 ulp of fp32
+    assert oracle_lib.expf(0.0) == 1.0
+
+
+def test_binning_properties(oracle_lib):
+    from oracle import oracle as O
+    case = make_case(400, 96, 80, seed=11, sh_degree=0)
+    fwd = O.forward(oracle_problem(case))
+    rng = fwd["ranges"]
+    pl = fwd["point_list"]
+    tt = fwd["tiles_touched"]
+    assert fwd["num_rendered"] == int(tt.sum()) == len(pl)
+    # ranges tile the point list contiguously in tile order
+    nz = rng[rng[:, 1] > rng[:, 0]]
+    assert np.all(nz[1:, 0] == nz[:-1, 1]) and nz[0, 0] == 0 and nz[-1, 1] == len(pl)
+    # every Gaussian appears exactly tiles_touched times
+    np.testing.assert_array_equal(np.bincount(pl, minlength=len(tt)), tt)
+    # within a tile: (depth, id) ascending
+    d = fwd["depth"]
+    for s, e in rng:
+        ids = pl[s:e]
+        key = d[ids].view(np.uint32).astype(np.uint64) << np.uint64(32) | ids.astype(np.uint64)
+        assert np.all(np.diff(key.astype(np.float64)) > 0) or e - s <= 1
+
+
+def test_render_threads_do_not_change_results(oracle_lib):
+    from oracle import oracle as O
+    case = make_case(500, 80, 64, seed=13, sh_degree=3, lang_dim=4)
+    pb = oracle_problem(case)
+    a = O.forward(pb, nthreads=1)
+    b = O.forward(pb, nthreads=4)
+    for k in ("color", "lang", "final_T", "n_contrib"):
+        np.testing.assert_array_equal(a[k], b[k])
+
+
+def test_tile_subset_render_matches_full(oracle_lib):
+    from oracle import oracle as O
+    case = make_case(300, 64, 64, seed=17, sh_degree=1, lang_dim=4)
+    pb = oracle_problem(case)
+    full = O.forward(pb)
+    tiles = [0, 5, 10, 15]
+    sub = O.forward(pb, tiles=tiles)
+    for t in tiles:
+        ty, tx = divmod(t, 4)
+        sl = (slice(ty * 16, ty * 16 + 16), slice(tx * 16, tx * 16 + 16))
+        np.testing.assert_array_equal(sub["color"][(slice(None),) + sl], full["color"][(slice(None),) + sl])
+        np.testing.assert_array_equal(sub["n_contrib"][sl], full["n_contrib"][sl])
