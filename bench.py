@@ -92,7 +92,23 @@ def algorithmic_bytes(g, rs, D, S):
                    mean_n_contrib=float(nc.float().mean().item()))
 
 
-def cpu_baseline(cam, gcpu, D, budget_tiles=64):
+def pmc_traffic(stage):
+    """Measured HBM bytes per launch of `stage`'s kernel from the newest committed
+    profiles/r*_pmc_traffic.json (tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE
+    rocprofv3 passes over tools/pmc_step.py = this workload, gfx950-corrected)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        doc = json.load(f)
+    ks = [v for k, v in doc["kernels"].items() if k == "k_" + stage or k.startswith("k_" + stage + "<")]
+    if not ks:
+        return None, None
+    return int(sum(v["traffic_bytes"] for v in ks)), os.path.relpath(files[-1], ROOT)
+
+
+def cpu_baseline(cam, gcpu, D, budget_tiles=2048):
     """The oracle (C restatement, single thread) on a bounded sample of the same frame:
     full preprocess + binning + preprocess-bwd, render fwd+bwd on `budget_tiles` seeded
     tiles, the render part extrapolated by T / budget_tiles."""
@@ -229,6 +245,7 @@ def main():
         dom = max(per_stage, key=lambda k: per_stage[k]["ms_per_launch"])
         dom_ms = per_stage[dom]["ms_per_launch"]
         dom_gbps = bytes_[dom] / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+        traffic, traffic_src = pmc_traffic(dom)
         step_ms = elapsed / args.steps * 1e3
         kernel_ms = sum(v["ms_per_launch"] for v in per_stage.values())
         total_bytes = sum(bytes_.values())
@@ -261,7 +278,8 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(dom_gbps / HBM_PEAK_GBPS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": int(bytes_[dom]),
                 "ms_per_launch": round(dom_ms, 4),
             },

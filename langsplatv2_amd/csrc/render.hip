@@ -1,22 +1,30 @@
 // render.hip — per-pixel alpha blending over the per-tile depth-ordered
-// Gaussian lists (A.3) and its reverse replay (A.4).
+// Gaussian lists and its reverse replay (A.4).
 //
-// Forward: one 256-thread workgroup (4 wave64) per 16x16 tile; batches of
-// 256 instances staged into LDS (splat record 32 B + feature row); each lane
-// owns one pixel and walks the batch front to back; __syncthreads_count
-// retires the tile when all 256 pixels saturated (T < 1e-4).  A per-Gaussian
-// conservative exponent cut (splat record .z) skips pairs whose alpha is
-// certainly < 1/255 without evaluating exp.  No MFMA: the blend is a serial
-// per-pixel recurrence.
+// Work decomposition (both directions): one 64-thread workgroup = ONE wave
+// per 8x8 pixel block, four blocks per 16x16 tile, 4T workgroups.  Waves of
+// a tile never synchronise with each other (no __syncthreads anywhere), so a
+// wave whose pixels saturate retires immediately instead of idling at a block
+// barrier; the four blocks of a tile are placed consecutively inside one
+// XCD's dispatch range (WaveTile / xcd_remap) so they share that XCD's L2.
 //
-// Backward: same tiling, batches staged back to front from the tile's
-// largest n_contrib.  Per instance, each lane computes its pixel's
-// contribution to the 9 + D per-Gaussian gradient values; the wave then
-// reduces all values at once by recursive halving (gfx950 v_permlane32_swap,
-// v_permlane16_swap, then row DPP), leaving value v's wave sum in lanes 2v and
-// 2v+1, and 32 lanes issue ONE 128-byte global_atomic_add_f32 into the
-// Gaussian's gradient row.  That is 70 VALU ops + 1 atomic instruction per
-// (wave, instance) instead of (9 + D) atomics per contributing pixel.
+// Per chunk of 64 tile instances a wave loads the ids (prefetched one chunk
+// ahead), the 32-B splat records and feature rows, tests each against its
+// 8x8 block with the per-Gaussian cut ellipse (block_overlap), and compacts
+// the survivors in order with __ballot + mbcnt into its private LDS stage.
+// The conservative exponent cut (splat record B.z) skips pairs whose alpha is
+// certainly < 1/255 without evaluating exp.  No MFMA in the forward: the blend
+// is a serial per-pixel recurrence; two instances per step keep two
+// independent exp chains in flight.
+//
+// Backward: same mapping, instances replayed back to front from the wave's
+// largest n_contrib.  Per (wave, instance) the 9 geometric/colour values are
+// reduced across the wave by recursive halving (gfx950 v_permlane32_swap,
+// v_permlane16_swap, row DPP) and added with one atomic per value; for
+// D >= 16 the language-channel gradients (aT[j][p] x dL/dlang[ch][p] summed
+// over the wave's 64 pixels) are a 16x64 . 64x16 product per 16 staged
+// instances, done exactly in f32 on the matrix cores
+// (v_mfma_f32_16x16x4_f32), with the dL/dlang fragments held in registers.
 #include "lsr_internal.h"
 
 #ifndef LSR_BWD_PIPE

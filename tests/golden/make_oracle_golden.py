@@ -2,9 +2,10 @@
 oracle on seeded synthetic cases (SURVEY.md §8c fixtures cfg1_rgb,
 small_lang16, quick192; sizes reduced to keep the files small).
 
-Inputs are NOT stored: they are regenerated from seeds by
-langsplatv2_amd.scenes (a sha256 of the regenerated inputs is stored and
-checked, so generator drift is detected).  Outputs are the oracle's.
+Inputs are generated from seeds by langsplatv2_amd.scenes and STORED in the
+fixture (prefix in_ / cam_): torch's CPU transcendental kernels take
+ISA-dependent SIMD paths, so regenerating on another host's CPU can change
+last bits.  Tests rebuild the case from the stored inputs (`load_case`).
 
     python tests/golden/make_oracle_golden.py
 """
@@ -30,6 +31,19 @@ def build_case(name):
     return make_case(**CASES[name])
 
 
+def load_case(npz):
+    """The case (camera + Gaussians) exactly as stored in a fixture."""
+    import torch
+    cam = {k[4:]: (torch.from_numpy(npz[k]) if npz[k].ndim else npz[k].item()) for k in npz if k.startswith("cam_")}
+    cam["W"], cam["H"] = int(cam["W"]), int(cam["H"])
+    g = {k[3:]: torch.from_numpy(npz[k]) for k in npz if k.startswith("in_")}
+    for k in ("sh_degree", "quick_dim"):
+        if "meta_" + k in npz:
+            g[k] = int(npz["meta_" + k])
+    return dict(cam=cam, g=g, bg=tuple(float(x) for x in npz["meta_bg"]),
+                scale_modifier=float(npz["meta_scale_modifier"]), quick=bool(npz["meta_quick"]))
+
+
 def input_digest(case):
     h = hashlib.sha256()
     for k in sorted(case["g"]):
@@ -51,17 +65,26 @@ def upstream_grads(case, seed=1):
     return dC, dL
 
 
-def run(name):
+def run(name, case=None):
     from oracle import oracle as O
     from harness import oracle_problem
-    case = build_case(name)
+    case = build_case(name) if case is None else case
     pb = oracle_problem(case)
     fwd = O.forward(pb, nthreads=8)
     dC, dL = upstream_grads(case)
     bwd = O.backward(pb, fwd, dC, dL)
     out = dict(digest=np.array(input_digest(case)), num_rendered=np.array(fwd["num_rendered"]),
+               meta_bg=np.array(case["bg"], np.float32), meta_scale_modifier=np.array(case["scale_modifier"]),
+               meta_quick=np.array(case["quick"]),
                radii=fwd["radii"], color=fwd["color"], lang=fwd["lang"], final_T=fwd["final_T"],
                n_contrib=fwd["n_contrib"], point_list=fwd["point_list"], ranges=fwd["ranges"])
+    for k, v in case["g"].items():
+        if hasattr(v, "numpy"):
+            out["in_" + k] = v.numpy()
+        else:
+            out["meta_" + k] = np.array(v)
+    for k, v in case["cam"].items():
+        out["cam_" + k] = v.numpy() if hasattr(v, "numpy") else np.array(v)
     for k in ("dmean2D", "dmeans3D", "dopacity", "dcolors", "dsh", "dscales", "drot", "dlang"):
         if bwd.get(k) is not None:
             out["grad_" + k] = bwd[k]
