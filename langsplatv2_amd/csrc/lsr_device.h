@@ -252,6 +252,33 @@ __device__ __forceinline__ bool block_overlap(float x, float y, uint32_t ext, in
     return (x + hx >= (float)bx) && (x - hx <= (float)(bx + 7)) && (y + hy >= (float)by) && (y - hy <= (float)(by + 7));
 }
 
+// Exact (conservative) test: does the cut ellipse {d : Q(d) <= -2 cut},
+// Q(d) = ca dx^2 + 2 cb dx dy + cc dy^2 with d = (x, y) - pixel, meet the
+// pixel rectangle [bx, bx+7] x [by, by+7]?  Q is convex, so its minimum over
+// the rectangle is 0 when the centre is inside, else it lies on an edge; on
+// each edge Q is a 1-D quadratic minimised at a clamped stationary point.  A
+// relative + absolute margin keeps the test conservative under rounding, so
+// every pair the blend would accept survives (results stay bit-identical);
+// the bounding-box test (block_overlap) keeps far more false candidates for
+// thin, rotated splats.
+__device__ __forceinline__ bool block_overlap_exact(float x, float y, float ca, float cb, float cc, float cut,
+                                                    int bx, int by)
+{
+    if (!(ca > 0.f) || !(cc > 0.f) || !(cut > -3.0e38f)) return true;   // degenerate / no cut: keep
+    const float thr = fmaf(-2.f * cut, 1.001f, 1e-3f);
+    const float u1 = x - (float)bx, u0 = u1 - 7.f;   // dx over the block's columns
+    const float v1 = y - (float)by, v0 = v1 - 7.f;   // dy over its rows
+    if (u0 <= 0.f && u1 >= 0.f && v0 <= 0.f && v1 >= 0.f) return true;
+    const float ica = 1.f / ca, icc = 1.f / cc;
+    auto q = [&](float u, float v) { return fmaf(ca * u, u, fmaf(2.f * cb * u, v, cc * v * v)); };
+    const float va = fminf(fmaxf(-cb * u0 * icc, v0), v1);
+    const float vb = fminf(fmaxf(-cb * u1 * icc, v0), v1);
+    const float ua = fminf(fmaxf(-cb * v0 * ica, u0), u1);
+    const float ub = fminf(fmaxf(-cb * v1 * ica, u0), u1);
+    const float qmin = fminf(fminf(q(u0, va), q(u1, vb)), fminf(q(ua, v0), q(ub, v1)));
+    return !(qmin > thr);
+}
+
 // ------------------------------------------------------------- layouts --
 // Geometry workspace (per Gaussian, SoA, every section 256-B aligned).
 struct GeomLayout {

@@ -33,6 +33,12 @@
 #ifndef LSR_BF_REGS
 #define LSR_BF_REGS 1
 #endif
+#ifndef LSR_BWD_MF
+#define LSR_BWD_MF 0
+#endif
+#ifndef LSR_EXACT_CULL
+#define LSR_EXACT_CULL 1
+#endif
 
 namespace lsr {
 
@@ -228,7 +234,12 @@ __device__ __forceinline__ int stage_candidates(WaveStage<F4>& st, bool valid, u
         A = splatA[gid];
         B = splatB[gid];
     }
+#if LSR_EXACT_CULL
+    const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by) &&
+                    block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, bx, by);
+#else
     const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by);
+#endif
     const uint64_t m = __ballot(ok);
     const int cnt = __popcll(m);
     if (ok) {
@@ -767,15 +778,308 @@ __global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs b)
     }
 }
 
+
+// ------------------------------------------------ factorised backward ----
+// Every per-(pixel, instance) gradient term is a product of a per-pair
+// scalar and a per-pixel quantity, so the pixel sums of a wave are GEMMs:
+//   colour / language:  g[j][c]  = sum_p aT[j][p] * dL/dout[c][p]
+//   geometry:           with u = dL/dalpha * G, dx = X_j - lx_p (X_j, lx_p
+//                       relative to the 8x8 block centre), the six values
+//                       (mean2D x/y, conic a/b/c, opacity) are linear in the
+//                       moments  sum_p u[j][p] * {1, lx, ly, lx^2, lx*ly, ly^2}
+//   per-pair dot:       dot[j][p] = sum_c f[j][c] * dL/dout[c][p]
+// All three run on exact-f32 MFMA (v_mfma_f32_16x16x4_f32) over groups of 16
+// instances; the serial per-pixel recurrence (T recovery, rec) is the only
+// per-pair VALU work left.  The B operands (dL/dout in two layouts and the
+// pixel moments) are per-wave constants held in registers.
+template <int NL>
+struct BwdFrags {
+    static constexpr int C = 3 + NL;
+    static constexpr int KS = (C + 3) / 4;      // dot K-steps over channels
+    static constexpr int NBC = (C + 15) / 16;   // channel blocks of the gradient product
+    float dotB[KS][4];    // dL/dout[4t + (l>>4)][pb*16 + (l&15)]
+    float chB[NBC][16];   // dL/dout[nb*16 + (l&15)][4t + (l>>4)]
+    float momB[16];       // moment (l&15) of block pixel 4t + (l>>4)
+};
+
+template <int NL>
+__device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int bx, int by)
+{
+    const Cam& cm = b.f.cam;
+    const int qx = bx + (q & 7), qy = by + (q >> 3);
+    if (qx >= cm.W || qy >= cm.H || c >= 3 + b.f.D) return 0.f;
+    const size_t HW = (size_t)cm.H * cm.W;
+    const size_t pix = (size_t)qy * cm.W + qx;
+    return c < 3 ? b.dout_color[c * HW + pix] : b.dout_lang[(size_t)(c - 3) * HW + pix];
+}
+
+#define LSR_DOT_STRIDE 68   // sDot row stride: conflict-free fragment stores
+#define LSR_MOM_STRIDE 8
+#define LSR_LOG2E 1.4426950408889634f
+
+template <int NL>
+__global__ void __launch_bounds__(64) k_render_bwd_mf(RenderBwdArgs b)
+{
+    using FR = BwdFrags<NL>;
+    constexpr int C = FR::C;
+    constexpr int F4 = (C + 3) / 4;
+    constexpr int KS = FR::KS;
+    constexpr int NBC = FR::NBC;
+    __shared__ WaveStage<F4> st;
+    __shared__ float sDot[16 * LSR_DOT_STRIDE];
+    __shared__ float sU[16 * SLOT_STRIDE];
+    __shared__ float sAT[16 * SLOT_STRIDE];
+    __shared__ int sC[64];                       // compacted contributing candidates
+    __shared__ float sMom[16 * LSR_MOM_STRIDE];
+
+    const RenderArgs& a = b.f;
+    const Cam& c = a.cam;
+    const WaveTile wt;
+    const int lane = threadIdx.x;
+    const int lg = lane >> 4, li = lane & 15;
+    const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
+    const bool inside = pm.px < c.W && pm.py < c.H;
+    const float pfx = (float)pm.px, pfy = (float)pm.py;
+    const float cx = (float)pm.bx + 3.5f, cy = (float)pm.by + 3.5f;
+    const uint32_t rs = a.tile_start[wt.tile];
+    const size_t HW = (size_t)c.H * c.W;
+    const size_t pix = (size_t)pm.py * c.W + pm.px;
+    const int D = a.D;
+    const int VP = b.VP;
+    const float ddelx_dx = 0.5f * (float)c.W, ddely_dy = 0.5f * (float)c.H;
+
+    const float T_final = inside ? a.final_T[pix] : 0.f;
+    const int last = inside ? (int)a.n_contrib[pix] : 0;
+    const int wmax = wave_max_i(last);
+    if (wmax == 0) return;
+
+    FR fr;
+#pragma unroll
+    for (int t = 0; t < KS; t++)
+#pragma unroll
+        for (int pb = 0; pb < 4; pb++) fr.dotB[t][pb] = gd_at<NL>(b, 4 * t + lg, pb * 16 + li, pm.bx, pm.by);
+#pragma unroll
+    for (int nb = 0; nb < NBC; nb++)
+#pragma unroll
+        for (int t = 0; t < 16; t++) fr.chB[nb][t] = gd_at<NL>(b, nb * 16 + li, 4 * t + lg, pm.bx, pm.by);
+#pragma unroll
+    for (int t = 0; t < 16; t++) {
+        const int q = 4 * t + lg;
+        const float lx = (float)(q & 7) - 3.5f, ly = (float)(q >> 3) - 3.5f;
+        float m = 0.f;
+        m = li == 0 ? 1.f : m;
+        m = li == 1 ? lx : m;
+        m = li == 2 ? ly : m;
+        m = li == 3 ? lx * lx : m;
+        m = li == 4 ? lx * ly : m;
+        m = li == 5 ? ly * ly : m;
+        fr.momB[t] = m;
+    }
+    const float bg0 = c.bg[0], bg1 = c.bg[1], bg2 = c.bg[2];
+    const bool has_bg = (bg0 != 0.f) || (bg1 != 0.f) || (bg2 != 0.f);   // uniform
+    float bg_dot = 0.f;
+    if (has_bg && inside)
+        bg_dot = bg0 * b.dout_color[pix] + bg1 * b.dout_color[HW + pix] + bg2 * b.dout_color[2 * HW + pix];
+
+    float T = T_final;
+    float last_alpha = 0.f, last_dot = 0.f, rec = 0.f;
+    const float* Ff = reinterpret_cast<const float*>(st.F);
+
+    // positions [0, wmax) back to front, 64 per chunk
+    uint32_t next_gid = (wmax - 1 - lane >= 0) ? a.point_list[rs + wmax - 1 - lane] : 0u;
+    for (int c0 = 0; c0 < wmax; c0 += 64) {
+        const int p = wmax - 1 - (c0 + lane);
+        const bool valid = p >= 0;
+        const uint32_t gid = next_gid;
+        next_gid = (p - 64 >= 0) ? a.point_list[rs + p - 64] : 0u;
+        const int n = stage_candidates<NL, F4>(st, valid, gid, p, pm.bx, pm.by, a.splatA, a.splatB, a.rgb, a.lang, D);
+
+        // phase 0: candidates with at least one lane inside the exponent cut
+        // and before its pixel's last contributor (no exp yet)
+        uint64_t cmask = 0;
+#pragma unroll 4
+        for (int j = 0; j < n; j++) {
+            const float4 A = st.A[j];
+            const float4 B = st.B[j];
+            const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
+            const bool cj = (st.pos[j] < last) && !(power > 0.0f || power < B.z);
+            if (__any(cj)) cmask |= 1ull << j;
+        }
+        const int nc = __popcll(cmask);
+        if (nc == 0) {
+            wave_lds_fence();
+            continue;
+        }
+        if ((cmask >> lane) & 1ull) sC[__popcll(cmask & ((1ull << lane) - 1ull))] = lane;
+        wave_lds_fence();
+
+        for (int g0 = 0; g0 < nc; g0 += 16) {
+            const int kn = min(16, nc - g0);
+            // dot[k][p] of the group's candidates on MFMA: (16 x C) . (C x 64)
+            {
+                const int row = sC[g0 + (li < kn ? li : 0)];
+                f32x4 acc[4];
+#pragma unroll
+                for (int pb = 0; pb < 4; pb++) acc[pb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int t = 0; t < KS; t++) {
+                    const float av = Ff[row * (F4 * 4) + 4 * t + lg];
+#pragma unroll
+                    for (int pb = 0; pb < 4; pb++)
+                        acc[pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, fr.dotB[t][pb], acc[pb], 0, 0, 0);
+                }
+#pragma unroll
+                for (int pb = 0; pb < 4; pb++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) sDot[(4 * lg + r) * LSR_DOT_STRIDE + pb * 16 + li] = acc[pb][r];
+            }
+            // phase 1: per candidate alpha and G, independent across the group
+            float al[16], Gk[16];
+            bool any_near = false;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                al[k] = 0.f;
+                Gk[k] = 0.f;
+                if (k < kn) {
+                    const int j = sC[g0 + k];
+                    const float4 A = st.A[j];
+                    const float4 B = st.B[j];
+                    const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
+                    const bool cj = (st.pos[j] < last) && !(power > 0.0f || power < B.z);
+                    const float G = __builtin_amdgcn_exp2f(power * LSR_LOG2E);
+                    const float alpha = fminf(0.99f, B.y * G);
+                    any_near = any_near || (cj && fabsf(alpha - (1.0f / 255.0f)) < 2e-8f);
+                    const bool ok = cj && !(alpha < 1.0f / 255.0f);
+                    al[k] = ok ? alpha : 0.f;
+                    Gk[k] = ok ? G : 0.f;
+                }
+            }
+            if (__any(any_near)) {
+                // the 1/255 decision must be the forward's: lanes inside the fast
+                // exp's error band re-evaluate with the forward's exp (rare)
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    if (k < kn) {
+                        const int j = sC[g0 + k];
+                        const float4 A = st.A[j];
+                        const float4 B = st.B[j];
+                        const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
+                        const bool cj = (st.pos[j] < last) && !(power > 0.0f || power < B.z);
+                        const float Gf = __builtin_amdgcn_exp2f(power * LSR_LOG2E);
+                        const float af = fminf(0.99f, B.y * Gf);
+                        if (cj && fabsf(af - (1.0f / 255.0f)) < 2e-8f) {
+                            const float G = expf_det(power);
+                            const float alpha = fminf(0.99f, B.y * G);
+                            const bool ok = !(alpha < 1.0f / 255.0f);
+                            al[k] = ok ? alpha : 0.f;
+                            Gk[k] = ok ? G : 0.f;
+                        }
+                    }
+                }
+            }
+            wave_lds_fence();   // sDot visible
+            // phase 2: the serial back-to-front recurrence (T, rec) per pixel
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                const bool ck = al[k] != 0.f;
+                const float rcp = __builtin_amdgcn_rcpf(1.f - al[k]);
+                T = T * rcp;
+                const float aT = al[k] * T;
+                const float dot = sDot[k * LSR_DOT_STRIDE + lane];
+                const float rec_new = fmaf(last_alpha, last_dot, (1.f - last_alpha) * rec);
+                float dL_dalpha = (dot - rec_new) * T;
+                if (has_bg) dL_dalpha = fmaf(-T_final * rcp, bg_dot, dL_dalpha);
+                dL_dalpha = ck ? dL_dalpha : 0.f;
+                rec = ck ? rec_new : rec;
+                last_alpha = ck ? al[k] : last_alpha;
+                last_dot = ck ? dot : last_dot;
+                sU[k * SLOT_STRIDE + lane] = dL_dalpha * Gk[k];
+                sAT[k * SLOT_STRIDE + lane] = aT;
+            }
+            wave_lds_fence();
+            // phase 3: the group's gradients on MFMA
+            {
+                f32x4 mom = {0.f, 0.f, 0.f, 0.f};
+                f32x4 ch[NBC];
+#pragma unroll
+                for (int nb = 0; nb < NBC; nb++) ch[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int t = 0; t < 16; t++) {
+                    const float au = sU[li * SLOT_STRIDE + 4 * t + lg];
+                    const float aa = sAT[li * SLOT_STRIDE + 4 * t + lg];
+                    mom = __builtin_amdgcn_mfma_f32_16x16x4f32(au, fr.momB[t], mom, 0, 0, 0);
+#pragma unroll
+                    for (int nb = 0; nb < NBC; nb++)
+                        ch[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa, fr.chB[nb][t], ch[nb], 0, 0, 0);
+                }
+                // colour / language: lane holds slot 4*lg+r, channel nb*16+li
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int slot = 4 * lg + r;
+                    if (slot < kn) {
+                        const uint32_t gidk = st.gid[sC[g0 + slot]];
+                        float* row = b.grad_acc + (size_t)gidk * VP;
+#pragma unroll
+                        for (int nb = 0; nb < NBC; nb++) {
+                            const int chn = nb * 16 + li;
+                            const float v = ch[nb][r];
+                            if (chn < 3 + D && v != 0.f) atomicAdd(row + (chn < 3 ? 6 + chn : LSR_GROW_LANG + chn - 3), v);
+                        }
+                    }
+                }
+                if (li < 6) {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) sMom[(4 * lg + r) * LSR_MOM_STRIDE + li] = mom[r];
+                }
+                wave_lds_fence();
+                if (lane < kn) {
+                    const int j = sC[g0 + lane];
+                    const float4 A = st.A[j];
+                    const float4 B = st.B[j];
+                    const float* M = sMom + lane * LSR_MOM_STRIDE;
+                    const float S0 = M[0], S1 = M[1], S2 = M[2], S3 = M[3], S4 = M[4], S5 = M[5];
+                    const float X = A.x - cx, Y = A.y - cy;
+                    const float Sdx = fmaf(X, S0, -S1), Sdy = fmaf(Y, S0, -S2);
+                    const float Sdxx = fmaf(X, fmaf(X, S0, -2.f * S1), S3);
+                    const float Sdxy = fmaf(X, fmaf(Y, S0, -S2), fmaf(-Y, S1, S4));
+                    const float Sdyy = fmaf(Y, fmaf(Y, S0, -2.f * S2), S5);
+                    const float o = B.y;
+                    float* row = b.grad_acc + (size_t)st.gid[j] * VP;
+                    const float g0v = -o * ddelx_dx * fmaf(A.z, Sdx, A.w * Sdy);
+                    const float g1v = -o * ddely_dy * fmaf(B.x, Sdy, A.w * Sdx);
+                    const float g2v = -0.5f * o * Sdxx;
+                    const float g3v = -o * Sdxy;
+                    const float g4v = -0.5f * o * Sdyy;
+                    if (g0v != 0.f) atomicAdd(row + 0, g0v);
+                    if (g1v != 0.f) atomicAdd(row + 1, g1v);
+                    if (g2v != 0.f) atomicAdd(row + 2, g2v);
+                    if (g3v != 0.f) atomicAdd(row + 3, g3v);
+                    if (g4v != 0.f) atomicAdd(row + 4, g4v);
+                    if (S0 != 0.f) atomicAdd(row + 5, S0);
+                }
+                wave_lds_fence();
+            }
+        }
+        wave_lds_fence();
+    }
+}
+
 hipError_t launch_render_bwd(const RenderBwdArgs& b, hipStream_t st)
 {
     const int T = b.f.cam.gx * b.f.cam.gy;
     if (T == 0) return hipSuccess;
     switch (lang_set_for(b.f.D)) {
+#if LSR_BWD_MF
+        case 0: k_render_bwd_mf<0><<<4 * T, 64, 0, st>>>(b); break;
+        case 4: k_render_bwd_mf<4><<<4 * T, 64, 0, st>>>(b); break;
+        case 8: k_render_bwd_mf<8><<<4 * T, 64, 0, st>>>(b); break;
+        case 16: k_render_bwd_mf<16><<<4 * T, 64, 0, st>>>(b); break;
+#else
         case 0: k_render_bwd<0><<<4 * T, 64, 0, st>>>(b); break;
         case 4: k_render_bwd<4><<<4 * T, 64, 0, st>>>(b); break;
         case 8: k_render_bwd<8><<<4 * T, 64, 0, st>>>(b); break;
         case 16: k_render_bwd<16><<<4 * T, 64, 0, st>>>(b); break;
+#endif
         case 32: k_render_bwd<32><<<4 * T, 64, 0, st>>>(b); break;
         case 64: k_render_bwd<64><<<4 * T, 64, 0, st>>>(b); break;
         default: return hipErrorInvalidValue;

@@ -10,7 +10,7 @@ def main():
     path, sym = sys.argv[1], sys.argv[2]
     txt = open(path).read().split("\n")
     s = next(i for i, l in enumerate(txt) if l.startswith(sym + ":"))
-    e = next(i for i in range(s, len(txt)) if "s_endpgm" in txt[i])
+    e = next(i for i in range(s, len(txt)) if txt[i].startswith(".Lfunc_end"))
     lines = txt[s:e + 1]
     blocks, cur = {}, None
     for i, l in enumerate(lines):
