@@ -34,7 +34,7 @@
 #define LSR_BF_REGS 1
 #endif
 #ifndef LSR_BWD_MF
-#define LSR_BWD_MF 0
+#define LSR_BWD_MF 1
 #endif
 #ifndef LSR_EXACT_CULL
 #define LSR_EXACT_CULL 1
@@ -815,22 +815,72 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
 
 #define LSR_DOT_STRIDE 68   // sDot row stride: conflict-free fragment stores
 #define LSR_MOM_STRIDE 8
+#define LSR_GR_STRIDE 36    // staged gradient rows (32 used floats)
+#ifndef LSR_MF_WAVES
+#define LSR_MF_WAVES 3      // min waves per SIMD (caps VGPRs at 168)
+#endif
+#define LSR_GRP_STRIDE 70   // dot/u and aT tiles: conflict-free fragment stores and A-fragment reads
 #define LSR_LOG2E 1.4426950408889634f
+#ifdef LSR_MF_NO_ATOMIC   // timing experiment only: keeps the work, drops the atomics
+#define LSR_MF_ATOMIC(ptr, v) do { if ((v) == 1234.5678f) atomicAdd((ptr), (v)); } while (0)
+#else
+#define LSR_MF_ATOMIC(ptr, v) atomicAdd((ptr), (v))
+#endif
+
+// Per-wave LDS staging of one chunk's candidate geometry (no feature rows).
+// 80 entries: up to 15 candidates carried over from the previous chunk + 64.
+struct WaveStageG {
+    float4 A[80];
+    float4 B[80];
+    uint32_t gid[80];
+    int pos[80];
+};
+
+// Appends this chunk's candidates after the `carry` entries already staged.
+__device__ __forceinline__ int stage_candidates_geo(WaveStageG& st, int carry, bool valid, uint32_t gid, int pos,
+                                                    int bx, int by, const float4* __restrict__ splatA,
+                                                    const float4* __restrict__ splatB)
+{
+    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+    if (valid) {
+        A = splatA[gid];
+        B = splatB[gid];
+    }
+    const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by) &&
+                    block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, bx, by);
+    const uint64_t m = __ballot(ok);
+    if (ok) {
+        const int r = carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        st.A[r] = A;
+        st.B[r] = B;
+        st.gid[r] = gid;
+        st.pos[r] = pos;
+    }
+    wave_lds_fence();
+    return __popcll(m);
+}
+
+// Feature c of Gaussian gid (rgb, then dense language; 0 past the channels).
+template <int NL>
+__device__ __forceinline__ float feature_at(const RenderArgs& a, uint32_t gid, int c)
+{
+    if (c < 3) return a.rgb[3 * (size_t)gid + c];
+    if (c - 3 < a.D) return a.lang[(size_t)gid * a.D + (c - 3)];
+    return 0.f;
+}
 
 template <int NL>
-__global__ void __launch_bounds__(64) k_render_bwd_mf(RenderBwdArgs b)
+__global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArgs b)
 {
     using FR = BwdFrags<NL>;
-    constexpr int C = FR::C;
-    constexpr int F4 = (C + 3) / 4;
     constexpr int KS = FR::KS;
     constexpr int NBC = FR::NBC;
-    __shared__ WaveStage<F4> st;
-    __shared__ float sDot[16 * LSR_DOT_STRIDE];
-    __shared__ float sU[16 * SLOT_STRIDE];
-    __shared__ float sAT[16 * SLOT_STRIDE];
-    __shared__ int sC[64];                       // compacted contributing candidates
+    constexpr int GS = LSR_GRP_STRIDE;
+    __shared__ WaveStageG st;
+    __shared__ float sDU[16 * GS];    // dot[k][p], overwritten in place by u[k][p]
+    __shared__ float sAT[16 * GS];    // G[k][p] (phase 1), then aT[k][p] (phase 2)
     __shared__ float sMom[16 * LSR_MOM_STRIDE];
+    __shared__ float sGr[16 * LSR_GR_STRIDE];   // the group's gradient rows
 
     const RenderArgs& a = b.f;
     const Cam& c = a.cam;
@@ -853,211 +903,212 @@ __global__ void __launch_bounds__(64) k_render_bwd_mf(RenderBwdArgs b)
     const int wmax = wave_max_i(last);
     if (wmax == 0) return;
 
-    FR fr;
+    float dotB[KS][4], chB[NBC][16];
 #pragma unroll
     for (int t = 0; t < KS; t++)
 #pragma unroll
-        for (int pb = 0; pb < 4; pb++) fr.dotB[t][pb] = gd_at<NL>(b, 4 * t + lg, pb * 16 + li, pm.bx, pm.by);
+        for (int pb = 0; pb < 4; pb++) dotB[t][pb] = gd_at<NL>(b, 4 * t + lg, pb * 16 + li, pm.bx, pm.by);
 #pragma unroll
     for (int nb = 0; nb < NBC; nb++)
 #pragma unroll
-        for (int t = 0; t < 16; t++) fr.chB[nb][t] = gd_at<NL>(b, nb * 16 + li, 4 * t + lg, pm.bx, pm.by);
-#pragma unroll
-    for (int t = 0; t < 16; t++) {
-        const int q = 4 * t + lg;
-        const float lx = (float)(q & 7) - 3.5f, ly = (float)(q >> 3) - 3.5f;
-        float m = 0.f;
-        m = li == 0 ? 1.f : m;
-        m = li == 1 ? lx : m;
-        m = li == 2 ? ly : m;
-        m = li == 3 ? lx * lx : m;
-        m = li == 4 ? lx * ly : m;
-        m = li == 5 ? ly * ly : m;
-        fr.momB[t] = m;
-    }
+        for (int t = 0; t < 16; t++) chB[nb][t] = gd_at<NL>(b, nb * 16 + li, 4 * t + lg, pm.bx, pm.by);
     const float bg0 = c.bg[0], bg1 = c.bg[1], bg2 = c.bg[2];
-    const bool has_bg = (bg0 != 0.f) || (bg1 != 0.f) || (bg2 != 0.f);   // uniform
-    float bg_dot = 0.f;
-    if (has_bg && inside)
-        bg_dot = bg0 * b.dout_color[pix] + bg1 * b.dout_color[HW + pix] + bg2 * b.dout_color[2 * HW + pix];
+    const float bg_dot = inside ? bg0 * b.dout_color[pix] + bg1 * b.dout_color[HW + pix] + bg2 * b.dout_color[2 * HW + pix]
+                                : 0.f;   // 0 with a black background: the term below is then exact 0
 
     float T = T_final;
     float last_alpha = 0.f, last_dot = 0.f, rec = 0.f;
-    const float* Ff = reinterpret_cast<const float*>(st.F);
 
-    // positions [0, wmax) back to front, 64 per chunk
+    // positions [0, wmax) back to front, 64 per chunk; candidates are processed
+    // in groups of 16, a partial group carried into the next chunk
+    int carry = 0;
     uint32_t next_gid = (wmax - 1 - lane >= 0) ? a.point_list[rs + wmax - 1 - lane] : 0u;
     for (int c0 = 0; c0 < wmax; c0 += 64) {
         const int p = wmax - 1 - (c0 + lane);
         const bool valid = p >= 0;
         const uint32_t gid = next_gid;
         next_gid = (p - 64 >= 0) ? a.point_list[rs + p - 64] : 0u;
-        const int n = stage_candidates<NL, F4>(st, valid, gid, p, pm.bx, pm.by, a.splatA, a.splatB, a.rgb, a.lang, D);
+        const int n = carry + stage_candidates_geo(st, carry, valid, gid, p, pm.bx, pm.by, a.splatA, a.splatB);
+        const int nfull = (c0 + 64 >= wmax) ? n : (n & ~15);
 
-        // phase 0: candidates with at least one lane inside the exponent cut
-        // and before its pixel's last contributor (no exp yet)
-        uint64_t cmask = 0;
+        for (int g0 = 0; g0 < nfull; g0 += 16) {
+            const int kn = min(16, nfull - g0);
+            // A fragments of the dot product: feature 4t+lg of candidate g0+li,
+            // gathered now, consumed after phase 1
+            float af[KS];
+            {
+                const uint32_t gi = st.gid[g0 + (li < kn ? li : 0)];
+#pragma unroll
+                for (int t = 0; t < KS; t++) af[t] = feature_at<NL>(a, gi, 4 * t + lg);
+            }
+            // phase 1: G of the 16 candidates (0 where the pair does not
+            // contribute), independent across candidates; straight-line code
+            // (bitwise predicates, unconditional loads; rows >= kn re-read row g0)
+            uint32_t near_any = 0u;
 #pragma unroll 4
-        for (int j = 0; j < n; j++) {
-            const float4 A = st.A[j];
-            const float4 B = st.B[j];
-            const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
-            const bool cj = (st.pos[j] < last) && !(power > 0.0f || power < B.z);
-            if (__any(cj)) cmask |= 1ull << j;
-        }
-        const int nc = __popcll(cmask);
-        if (nc == 0) {
-            wave_lds_fence();
-            continue;
-        }
-        if ((cmask >> lane) & 1ull) sC[__popcll(cmask & ((1ull << lane) - 1ull))] = lane;
-        wave_lds_fence();
-
-        for (int g0 = 0; g0 < nc; g0 += 16) {
-            const int kn = min(16, nc - g0);
+            for (int k = 0; k < 16; k++) {
+                const int j = g0 + (k < kn ? k : 0);
+                const float4 A = st.A[j];
+                const float4 B = st.B[j];
+                const int pj = st.pos[j];
+                const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
+                const bool cj = (k < kn) & (pj < last) & !(power > 0.0f) & !(power < B.z);
+                const float G = __builtin_amdgcn_exp2f(power * LSR_LOG2E);
+                const float alpha = fminf(0.99f, B.y * G);
+                near_any |= (uint32_t)(cj & (fabsf(alpha - (1.0f / 255.0f)) < 2e-8f));
+                const bool ok = cj & !(alpha < 1.0f / 255.0f);
+                sAT[k * GS + lane] = ok ? G : 0.f;
+            }
+            if (__any(near_any != 0u)) {
+                // the 1/255 decision must be the forward's: lanes inside the fast
+                // exp's error band re-evaluate with the forward's exp (rare)
+                for (int k = 0; k < kn; k++) {
+                    const int j = g0 + k;
+                    const float4 A = st.A[j];
+                    const float4 B = st.B[j];
+                    const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
+                    const bool cj = (st.pos[j] < last) & !(power > 0.0f) & !(power < B.z);
+                    const float af2 = fminf(0.99f, B.y * __builtin_amdgcn_exp2f(power * LSR_LOG2E));
+                    if (cj & (fabsf(af2 - (1.0f / 255.0f)) < 2e-8f)) {
+                        const float G = expf_det(power);
+                        const float alpha = fminf(0.99f, B.y * G);
+                        sAT[k * GS + lane] = !(alpha < 1.0f / 255.0f) ? G : 0.f;
+                    }
+                }
+            }
             // dot[k][p] of the group's candidates on MFMA: (16 x C) . (C x 64)
             {
-                const int row = sC[g0 + (li < kn ? li : 0)];
                 f32x4 acc[4];
 #pragma unroll
                 for (int pb = 0; pb < 4; pb++) acc[pb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int t = 0; t < KS; t++) {
-                    const float av = Ff[row * (F4 * 4) + 4 * t + lg];
+                for (int t = 0; t < KS; t++)
 #pragma unroll
                     for (int pb = 0; pb < 4; pb++)
-                        acc[pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, fr.dotB[t][pb], acc[pb], 0, 0, 0);
-                }
+                        acc[pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[t], dotB[t][pb], acc[pb], 0, 0, 0);
 #pragma unroll
                 for (int pb = 0; pb < 4; pb++)
 #pragma unroll
-                    for (int r = 0; r < 4; r++) sDot[(4 * lg + r) * LSR_DOT_STRIDE + pb * 16 + li] = acc[pb][r];
+                    for (int r = 0; r < 4; r++) sDU[(4 * lg + r) * GS + pb * 16 + li] = acc[pb][r];
             }
-            // phase 1: per candidate alpha and G, independent across the group
-            float al[16], Gk[16];
-            bool any_near = false;
-#pragma unroll
+            wave_lds_fence();
+            // phase 2: the serial back-to-front recurrence (T, rec) per pixel.
+            // G = 0 marks a non-contributing pair: alpha = min(0.99, o*0) = 0,
+            // rcp(1) = 1, so T is unchanged; the selects keep rec/last_*.
+#pragma unroll 4
             for (int k = 0; k < 16; k++) {
-                al[k] = 0.f;
-                Gk[k] = 0.f;
-                if (k < kn) {
-                    const int j = sC[g0 + k];
-                    const float4 A = st.A[j];
-                    const float4 B = st.B[j];
-                    const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
-                    const bool cj = (st.pos[j] < last) && !(power > 0.0f || power < B.z);
-                    const float G = __builtin_amdgcn_exp2f(power * LSR_LOG2E);
-                    const float alpha = fminf(0.99f, B.y * G);
-                    any_near = any_near || (cj && fabsf(alpha - (1.0f / 255.0f)) < 2e-8f);
-                    const bool ok = cj && !(alpha < 1.0f / 255.0f);
-                    al[k] = ok ? alpha : 0.f;
-                    Gk[k] = ok ? G : 0.f;
-                }
-            }
-            if (__any(any_near)) {
-                // the 1/255 decision must be the forward's: lanes inside the fast
-                // exp's error band re-evaluate with the forward's exp (rare)
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    if (k < kn) {
-                        const int j = sC[g0 + k];
-                        const float4 A = st.A[j];
-                        const float4 B = st.B[j];
-                        const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
-                        const bool cj = (st.pos[j] < last) && !(power > 0.0f || power < B.z);
-                        const float Gf = __builtin_amdgcn_exp2f(power * LSR_LOG2E);
-                        const float af = fminf(0.99f, B.y * Gf);
-                        if (cj && fabsf(af - (1.0f / 255.0f)) < 2e-8f) {
-                            const float G = expf_det(power);
-                            const float alpha = fminf(0.99f, B.y * G);
-                            const bool ok = !(alpha < 1.0f / 255.0f);
-                            al[k] = ok ? alpha : 0.f;
-                            Gk[k] = ok ? G : 0.f;
-                        }
-                    }
-                }
-            }
-            wave_lds_fence();   // sDot visible
-            // phase 2: the serial back-to-front recurrence (T, rec) per pixel
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const bool ck = al[k] != 0.f;
-                const float rcp = __builtin_amdgcn_rcpf(1.f - al[k]);
+                const float G = sAT[k * GS + lane];
+                const float dot = sDU[k * GS + lane];
+                const float o = st.B[g0 + (k < kn ? k : 0)].y;
+                const bool ck = G != 0.f;
+                const float al = fminf(0.99f, o * G);
+                const float rcp = __builtin_amdgcn_rcpf(1.f - al);
                 T = T * rcp;
-                const float aT = al[k] * T;
-                const float dot = sDot[k * LSR_DOT_STRIDE + lane];
+                const float aT = al * T;
                 const float rec_new = fmaf(last_alpha, last_dot, (1.f - last_alpha) * rec);
-                float dL_dalpha = (dot - rec_new) * T;
-                if (has_bg) dL_dalpha = fmaf(-T_final * rcp, bg_dot, dL_dalpha);
-                dL_dalpha = ck ? dL_dalpha : 0.f;
+                const float dL_dalpha = fmaf(-T_final * rcp, bg_dot, (dot - rec_new) * T);
+                const float u = ck ? dL_dalpha * G : 0.f;
                 rec = ck ? rec_new : rec;
-                last_alpha = ck ? al[k] : last_alpha;
+                last_alpha = ck ? al : last_alpha;
                 last_dot = ck ? dot : last_dot;
-                sU[k * SLOT_STRIDE + lane] = dL_dalpha * Gk[k];
-                sAT[k * SLOT_STRIDE + lane] = aT;
+                sDU[k * GS + lane] = u;
+                sAT[k * GS + lane] = aT;
             }
             wave_lds_fence();
             // phase 3: the group's gradients on MFMA
-            {
-                f32x4 mom = {0.f, 0.f, 0.f, 0.f};
-                f32x4 ch[NBC];
+            f32x4 mom = {0.f, 0.f, 0.f, 0.f};
+            f32x4 ch[NBC];
 #pragma unroll
-                for (int nb = 0; nb < NBC; nb++) ch[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int nb = 0; nb < NBC; nb++) ch[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int t = 0; t < 16; t++) {
-                    const float au = sU[li * SLOT_STRIDE + 4 * t + lg];
-                    const float aa = sAT[li * SLOT_STRIDE + 4 * t + lg];
-                    mom = __builtin_amdgcn_mfma_f32_16x16x4f32(au, fr.momB[t], mom, 0, 0, 0);
+            for (int t = 0; t < 16; t++) {
+                const float au = sDU[li * GS + 4 * t + lg];
+                const float aa = sAT[li * GS + 4 * t + lg];
+                // moment li of block pixel q = 4t + lg (relative to the block centre)
+                const float lx = (float)(((4 * t) & 7) + lg) - 3.5f, ly = (float)(t >> 1) - 3.5f;
+                float m = li == 0 ? 1.f : 0.f;
+                m = li == 1 ? lx : m;
+                m = li == 2 ? ly : m;
+                m = li == 3 ? lx * lx : m;
+                m = li == 4 ? lx * ly : m;
+                m = li == 5 ? ly * ly : m;
+                mom = __builtin_amdgcn_mfma_f32_16x16x4f32(au, m, mom, 0, 0, 0);
 #pragma unroll
-                    for (int nb = 0; nb < NBC; nb++)
-                        ch[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa, fr.chB[nb][t], ch[nb], 0, 0, 0);
+                for (int nb = 0; nb < NBC; nb++)
+                    ch[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa, chB[nb][t], ch[nb], 0, 0, 0);
+            }
+            // Gradient rows of the group staged in LDS (row layout of lsr_device.h:
+            // [0..5] geometry, [6..8] colour, [12..) language), then added with
+            // line-coalesced atomics: each 16-lane group covers one 64-B line of
+            // one Gaussian's row.
+            // colour / language: lane holds slot 4*lg+r, channel nb*16+li
+#pragma unroll
+            for (int nb = 0; nb < NBC; nb++) {
+                const int chn = nb * 16 + li;
+                if (chn < 3 + NL) {
+                    const int col = chn < 3 ? 6 + chn : LSR_GROW_LANG + chn - 3;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) sGr[(4 * lg + r) * LSR_GR_STRIDE + col] = ch[nb][r];
                 }
-                // colour / language: lane holds slot 4*lg+r, channel nb*16+li
+            }
+            if (li < 6) {
 #pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int slot = 4 * lg + r;
-                    if (slot < kn) {
-                        const uint32_t gidk = st.gid[sC[g0 + slot]];
-                        float* row = b.grad_acc + (size_t)gidk * VP;
+                for (int r = 0; r < 4; r++) sMom[(4 * lg + r) * LSR_MOM_STRIDE + li] = mom[r];
+            }
+            wave_lds_fence();
+            if (lane < kn) {
+                const int j = g0 + lane;
+                const float4 A = st.A[j];
+                const float4 B = st.B[j];
+                const float* M = sMom + lane * LSR_MOM_STRIDE;
+                const float S0 = M[0], S1 = M[1], S2 = M[2], S3 = M[3], S4 = M[4], S5 = M[5];
+                const float X = A.x - cx, Y = A.y - cy;
+                const float Sdx = fmaf(X, S0, -S1), Sdy = fmaf(Y, S0, -S2);
+                const float Sdxx = fmaf(X, fmaf(X, S0, -2.f * S1), S3);
+                const float Sdxy = fmaf(X, fmaf(Y, S0, -S2), fmaf(-Y, S1, S4));
+                const float Sdyy = fmaf(Y, fmaf(Y, S0, -2.f * S2), S5);
+                const float o = B.y;
+                float* gr = sGr + lane * LSR_GR_STRIDE;
+                gr[0] = -o * ddelx_dx * fmaf(A.z, Sdx, A.w * Sdy);
+                gr[1] = -o * ddely_dy * fmaf(B.x, Sdy, A.w * Sdx);
+                gr[2] = -0.5f * o * Sdxx;
+                gr[3] = -o * Sdxy;
+                gr[4] = -0.5f * o * Sdyy;
+                gr[5] = S0;
+            }
+            wave_lds_fence();
 #pragma unroll
-                        for (int nb = 0; nb < NBC; nb++) {
-                            const int chn = nb * 16 + li;
-                            const float v = ch[nb][r];
-                            if (chn < 3 + D && v != 0.f) atomicAdd(row + (chn < 3 ? 6 + chn : LSR_GROW_LANG + chn - 3), v);
-                        }
-                    }
-                }
-                if (li < 6) {
+            for (int h = 0; h < (LSR_GROW_LANG + NL > 16 ? 2 : 1); h++) {
+                const int f = 16 * h + li;
+                const bool fcol = (f < 9) | ((f >= LSR_GROW_LANG) & (f < LSR_GROW_LANG + D));
 #pragma unroll
-                    for (int r = 0; r < 4; r++) sMom[(4 * lg + r) * LSR_MOM_STRIDE + li] = mom[r];
+                for (int q = 0; q < 4; q++) {
+                    const int slot = 4 * q + lg;
+                    const float v = sGr[slot * LSR_GR_STRIDE + f];
+                    if (fcol & (slot < kn) & (v != 0.f))
+                        LSR_MF_ATOMIC(b.grad_acc + (size_t)st.gid[g0 + slot] * VP + f, v);
                 }
-                wave_lds_fence();
-                if (lane < kn) {
-                    const int j = sC[g0 + lane];
-                    const float4 A = st.A[j];
-                    const float4 B = st.B[j];
-                    const float* M = sMom + lane * LSR_MOM_STRIDE;
-                    const float S0 = M[0], S1 = M[1], S2 = M[2], S3 = M[3], S4 = M[4], S5 = M[5];
-                    const float X = A.x - cx, Y = A.y - cy;
-                    const float Sdx = fmaf(X, S0, -S1), Sdy = fmaf(Y, S0, -S2);
-                    const float Sdxx = fmaf(X, fmaf(X, S0, -2.f * S1), S3);
-                    const float Sdxy = fmaf(X, fmaf(Y, S0, -S2), fmaf(-Y, S1, S4));
-                    const float Sdyy = fmaf(Y, fmaf(Y, S0, -2.f * S2), S5);
-                    const float o = B.y;
-                    float* row = b.grad_acc + (size_t)st.gid[j] * VP;
-                    const float g0v = -o * ddelx_dx * fmaf(A.z, Sdx, A.w * Sdy);
-                    const float g1v = -o * ddely_dy * fmaf(B.x, Sdy, A.w * Sdx);
-                    const float g2v = -0.5f * o * Sdxx;
-                    const float g3v = -o * Sdxy;
-                    const float g4v = -0.5f * o * Sdyy;
-                    if (g0v != 0.f) atomicAdd(row + 0, g0v);
-                    if (g1v != 0.f) atomicAdd(row + 1, g1v);
-                    if (g2v != 0.f) atomicAdd(row + 2, g2v);
-                    if (g3v != 0.f) atomicAdd(row + 3, g3v);
-                    if (g4v != 0.f) atomicAdd(row + 4, g4v);
-                    if (S0 != 0.f) atomicAdd(row + 5, S0);
-                }
-                wave_lds_fence();
+            }
+            wave_lds_fence();
+        }
+        // carry the partial group to the front of the stage
+        carry = n - nfull;
+        if (carry > 0) {
+            float4 A, B;
+            uint32_t gq;
+            int pq;
+            if (lane < carry) {
+                A = st.A[nfull + lane];
+                B = st.B[nfull + lane];
+                gq = st.gid[nfull + lane];
+                pq = st.pos[nfull + lane];
+            }
+            wave_lds_fence();
+            if (lane < carry) {
+                st.A[lane] = A;
+                st.B[lane] = B;
+                st.gid[lane] = gq;
+                st.pos[lane] = pq;
             }
         }
         wave_lds_fence();
