@@ -817,7 +817,7 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
 #define LSR_MOM_STRIDE 8
 #define LSR_GR_STRIDE 36    // staged gradient rows (32 used floats)
 #ifndef LSR_MF_WAVES
-#define LSR_MF_WAVES 3      // min waves per SIMD (caps VGPRs at 168)
+#define LSR_MF_WAVES 2      // min waves per SIMD (caps VGPRs at 256)
 #endif
 #define LSR_GRP_STRIDE 70   // dot/u and aT tiles: conflict-free fragment stores and A-fragment reads
 #define LSR_LOG2E 1.4426950408889634f
@@ -829,11 +829,12 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
 
 // Per-wave LDS staging of one chunk's candidate geometry (no feature rows).
 // 80 entries: up to 15 candidates carried over from the previous chunk + 64.
+// B.w holds the candidate's tile-list position (int bits) once staged: the
+// cut extents it carried are only needed by the staging test itself.
 struct WaveStageG {
     float4 A[80];
     float4 B[80];
     uint32_t gid[80];
-    int pos[80];
 };
 
 // Appends this chunk's candidates after the `carry` entries already staged.
@@ -852,9 +853,8 @@ __device__ __forceinline__ int stage_candidates_geo(WaveStageG& st, int carry, b
     if (ok) {
         const int r = carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         st.A[r] = A;
-        st.B[r] = B;
+        st.B[r] = make_float4(B.x, B.y, B.z, __int_as_float(pos));
         st.gid[r] = gid;
-        st.pos[r] = pos;
     }
     wave_lds_fence();
     return __popcll(m);
@@ -902,6 +902,13 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     const int last = inside ? (int)a.n_contrib[pix] : 0;
     const int wmax = wave_max_i(last);
     if (wmax == 0) return;
+    // entries past a group's end are read unconditionally (immediate-offset
+    // loads, no index clamps): keep them finite
+    for (int e = lane; e < 80; e += 64) {
+        st.A[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+        st.B[e] = make_float4(0.f, 0.f, 0.f, __int_as_float(0x7fffffff));
+        st.gid[e] = 0u;
+    }
 
     float dotB[KS][4], chB[NBC][16];
 #pragma unroll
@@ -916,8 +923,9 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     const float bg_dot = inside ? bg0 * b.dout_color[pix] + bg1 * b.dout_color[HW + pix] + bg2 * b.dout_color[2 * HW + pix]
                                 : 0.f;   // 0 with a black background: the term below is then exact 0
 
+    const bool has_bg = (bg0 != 0.f) || (bg1 != 0.f) || (bg2 != 0.f);   // uniform
     float T = T_final;
-    float last_alpha = 0.f, last_dot = 0.f, rec = 0.f;
+    float S = 0.f;
 
     // positions [0, wmax) back to front, 64 per chunk; candidates are processed
     // in groups of 16, a partial group carried into the next chunk
@@ -943,21 +951,17 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             }
             // phase 1: G of the 16 candidates (0 where the pair does not
             // contribute), independent across candidates; straight-line code
-            // (bitwise predicates, unconditional loads; rows >= kn re-read row g0)
             uint32_t near_any = 0u;
-#pragma unroll 4
+#pragma unroll
             for (int k = 0; k < 16; k++) {
-                const int j = g0 + (k < kn ? k : 0);
-                const float4 A = st.A[j];
-                const float4 B = st.B[j];
-                const int pj = st.pos[j];
+                const float4 A = st.A[g0 + k];
+                const float4 B = st.B[g0 + k];
                 const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
-                const bool cj = (k < kn) & (pj < last) & !(power > 0.0f) & !(power < B.z);
+                const bool cj = (k < kn) & (__float_as_int(B.w) < last) & !(power > 0.0f) & !(power < B.z);
                 const float G = __builtin_amdgcn_exp2f(power * LSR_LOG2E);
-                const float alpha = fminf(0.99f, B.y * G);
-                near_any |= (uint32_t)(cj & (fabsf(alpha - (1.0f / 255.0f)) < 2e-8f));
-                const bool ok = cj & !(alpha < 1.0f / 255.0f);
-                sAT[k * GS + lane] = ok ? G : 0.f;
+                const float d = fminf(0.99f, B.y * G) - (1.0f / 255.0f);
+                near_any |= (uint32_t)(cj & (fabsf(d) < 2e-8f));
+                sAT[k * GS + lane] = (cj & (d >= 0.f)) ? G : 0.f;
             }
             if (__any(near_any != 0u)) {
                 // the 1/255 decision must be the forward's: lanes inside the fast
@@ -967,7 +971,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                     const float4 A = st.A[j];
                     const float4 B = st.B[j];
                     const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
-                    const bool cj = (st.pos[j] < last) & !(power > 0.0f) & !(power < B.z);
+                    const bool cj = (__float_as_int(B.w) < last) & !(power > 0.0f) & !(power < B.z);
                     const float af2 = fminf(0.99f, B.y * __builtin_amdgcn_exp2f(power * LSR_LOG2E));
                     if (cj & (fabsf(af2 - (1.0f / 255.0f)) < 2e-8f)) {
                         const float G = expf_det(power);
@@ -992,27 +996,38 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                     for (int r = 0; r < 4; r++) sDU[(4 * lg + r) * GS + pb * 16 + li] = acc[pb][r];
             }
             wave_lds_fence();
-            // phase 2: the serial back-to-front recurrence (T, rec) per pixel.
-            // G = 0 marks a non-contributing pair: alpha = min(0.99, o*0) = 0,
-            // rcp(1) = 1, so T is unchanged; the selects keep rec/last_*.
-#pragma unroll 4
-            for (int k = 0; k < 16; k++) {
-                const float G = sAT[k * GS + lane];
-                const float dot = sDU[k * GS + lane];
-                const float o = st.B[g0 + (k < kn ? k : 0)].y;
-                const bool ck = G != 0.f;
-                const float al = fminf(0.99f, o * G);
-                const float rcp = __builtin_amdgcn_rcpf(1.f - al);
-                T = T * rcp;
-                const float aT = al * T;
-                const float rec_new = fmaf(last_alpha, last_dot, (1.f - last_alpha) * rec);
-                const float dL_dalpha = fmaf(-T_final * rcp, bg_dot, (dot - rec_new) * T);
-                const float u = ck ? dL_dalpha * G : 0.f;
-                rec = ck ? rec_new : rec;
-                last_alpha = ck ? al : last_alpha;
-                last_dot = ck ? dot : last_dot;
-                sDU[k * GS + lane] = u;
-                sAT[k * GS + lane] = aT;
+            // phase 2: the serial back-to-front recurrence per pixel.  S is the
+            // colour accumulated behind the current instance (the upstream
+            // "accum_rec" once the last contributor is folded in):
+            //   dL/dalpha_k = (dot_k - S) T_k,   S <- alpha_k dot_k + (1 - alpha_k) S
+            // G = 0 marks a non-contributing pair: alpha = 0, rcp(1) = 1 and the
+            // S update is an exact identity, so no selects are needed.
+            if (has_bg) {
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const float G = sAT[k * GS + lane];
+                    const float dot = sDU[k * GS + lane];
+                    const float al = fminf(0.99f, st.B[g0 + k].y * G);
+                    const float om = 1.f - al;
+                    const float rcp = __builtin_amdgcn_rcpf(om);
+                    T = T * rcp;
+                    const float dL_dalpha = fmaf(-T_final * rcp, bg_dot, (dot - S) * T);
+                    sDU[k * GS + lane] = dL_dalpha * G;
+                    sAT[k * GS + lane] = al * T;
+                    S = fmaf(al, dot, om * S);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const float G = sAT[k * GS + lane];
+                    const float dot = sDU[k * GS + lane];
+                    const float al = fminf(0.99f, st.B[g0 + k].y * G);
+                    const float om = 1.f - al;
+                    T = T * __builtin_amdgcn_rcpf(om);
+                    sDU[k * GS + lane] = ((dot - S) * T) * G;
+                    sAT[k * GS + lane] = al * T;
+                    S = fmaf(al, dot, om * S);
+                }
             }
             wave_lds_fence();
             // phase 3: the group's gradients on MFMA
@@ -1096,19 +1111,16 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
         if (carry > 0) {
             float4 A, B;
             uint32_t gq;
-            int pq;
             if (lane < carry) {
                 A = st.A[nfull + lane];
                 B = st.B[nfull + lane];
                 gq = st.gid[nfull + lane];
-                pq = st.pos[nfull + lane];
             }
             wave_lds_fence();
             if (lane < carry) {
                 st.A[lane] = A;
                 st.B[lane] = B;
                 st.gid[lane] = gq;
-                st.pos[lane] = pq;
             }
         }
         wave_lds_fence();
