@@ -816,6 +816,9 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
 #define LSR_DOT_STRIDE 68   // sDot row stride: conflict-free fragment stores
 #define LSR_MOM_STRIDE 8
 #define LSR_GR_STRIDE 36    // staged gradient rows (32 used floats)
+#ifndef LSR_P1_UNROLL
+#define LSR_P1_UNROLL 4
+#endif
 #ifndef LSR_MF_WAVES
 #define LSR_MF_WAVES 2      // min waves per SIMD (caps VGPRs at 256)
 #endif
@@ -952,7 +955,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             // phase 1: G of the 16 candidates (0 where the pair does not
             // contribute), independent across candidates; straight-line code
             uint32_t near_any = 0u;
-#pragma unroll
+#pragma unroll LSR_P1_UNROLL
             for (int k = 0; k < 16; k++) {
                 const float4 A = st.A[g0 + k];
                 const float4 B = st.B[g0 + k];
