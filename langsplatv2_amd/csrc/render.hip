@@ -36,6 +36,9 @@
 #ifndef LSR_BWD_MF
 #define LSR_BWD_MF 1
 #endif
+#ifndef LSR_FWD_MF
+#define LSR_FWD_MF 0
+#endif
 #ifndef LSR_EXACT_CULL
 #define LSR_EXACT_CULL 1
 #endif
@@ -465,6 +468,9 @@ int lang_set_for(int D)
     return -1;
 }
 
+template <int NL>
+__global__ void k_render_fwd_mf(RenderArgs a);
+
 hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
 {
     const int T = a.cam.gx * a.cam.gy;
@@ -475,10 +481,17 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
         return hipGetLastError();
     }
     switch (lang_set_for(a.D)) {
+#if LSR_FWD_MF
+        case 0: k_render_fwd_mf<0><<<4 * T, 64, 0, st>>>(a); break;
+        case 4: k_render_fwd_mf<4><<<4 * T, 64, 0, st>>>(a); break;
+        case 8: k_render_fwd_mf<8><<<4 * T, 64, 0, st>>>(a); break;
+        case 16: k_render_fwd_mf<16><<<4 * T, 64, 0, st>>>(a); break;
+#else
         case 0: k_render_fwd<0><<<4 * T, 64, 0, st>>>(a); break;
         case 4: k_render_fwd<4><<<4 * T, 64, 0, st>>>(a); break;
         case 8: k_render_fwd<8><<<4 * T, 64, 0, st>>>(a); break;
         case 16: k_render_fwd<16><<<4 * T, 64, 0, st>>>(a); break;
+#endif
         case 32: k_render_fwd<32><<<4 * T, 64, 0, st>>>(a); break;
         case 64: k_render_fwd<64><<<4 * T, 64, 0, st>>>(a); break;
         default: return hipErrorInvalidValue;
@@ -1111,22 +1124,194 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
         }
         // carry the partial group to the front of the stage
         carry = n - nfull;
-        if (carry > 0) {
-            float4 A, B;
-            uint32_t gq;
-            if (lane < carry) {
-                A = st.A[nfull + lane];
-                B = st.B[nfull + lane];
-                gq = st.gid[nfull + lane];
-            }
-            wave_lds_fence();
-            if (lane < carry) {
-                st.A[lane] = A;
-                st.B[lane] = B;
-                st.gid[lane] = gq;
-            }
+        if (nfull > 0 && lane < carry) {   // source >= 16 > destination: no overlap
+            st.A[lane] = st.A[nfull + lane];
+            st.B[lane] = st.B[nfull + lane];
+            st.gid[lane] = st.gid[nfull + lane];
         }
         wave_lds_fence();
+    }
+}
+
+
+// ------------------------------------------------ MFMA-accumulated forward ----
+// The blend's channel accumulation out[c][p] = sum_k f[k][c] * aT[k][p] (k in
+// front-to-back order) is a GEMM with the tile's instances as K.  On gfx950
+// v_mfma_f32_16x16x4_f32 is bitwise a fmaf chain over k = 0..3
+// (tools/micro/mfma_order.hip: 131072/131072), and non-contributing pairs carry
+// aT = 0 (fmaf(f, 0, acc) == acc), so accumulating on the matrix cores in
+// instance order is bit-identical to the sequential per-pixel blend.  Per group
+// of 16 candidates: phase 1 evaluates alpha independently per candidate (the
+// deterministic exp), phase 2 runs the serial transmittance / termination
+// recurrence and writes aT, phase 3 accumulates on MFMA.
+struct WaveStageF {
+    float4 A[80];
+    float4 B[80];         // .w = 1-based tile-list position (int bits)
+    uint32_t gid[80];
+};
+
+__device__ __forceinline__ int stage_candidates_f(WaveStageF& st, int carry, bool valid, uint32_t gid, int pos,
+                                                  int bx, int by, const float4* __restrict__ splatA,
+                                                  const float4* __restrict__ splatB)
+{
+    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+    if (valid) {
+        A = splatA[gid];
+        B = splatB[gid];
+    }
+    const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by) &&
+                    block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, bx, by);
+    const uint64_t m = __ballot(ok);
+    if (ok) {
+        const int r = carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        st.A[r] = A;
+        st.B[r] = make_float4(B.x, B.y, B.z, __int_as_float(pos));
+        st.gid[r] = gid;
+    }
+    wave_lds_fence();
+    return __popcll(m);
+}
+
+#define LSR_FWD_STRIDE 80   // aT tile row stride: conflict-free B-fragment reads
+
+template <int NL>
+__global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_fwd_mf(RenderArgs a)
+{
+    constexpr int C = 3 + NL;
+    constexpr int F4 = (C + 3) / 4;
+    constexpr int RS = F4 * 4;                 // feature row stride (floats)
+    constexpr int NBC = (C + 15) / 16;         // 16-channel output blocks
+    constexpr int FS = LSR_FWD_STRIDE;
+    __shared__ WaveStageF st;
+    __shared__ float sAT[16 * FS];
+    __shared__ float sT[64];
+
+    const Cam& c = a.cam;
+    const WaveTile wt;
+    const int lane = threadIdx.x;
+    const int lg = lane >> 4, li = lane & 15;
+    const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
+    const bool inside = pm.px < c.W && pm.py < c.H;
+    const float pfx = (float)pm.px, pfy = (float)pm.py;
+    const uint32_t rs = a.tile_start[wt.tile], re = a.tile_start[wt.tile + 1];
+    const int D = a.D;
+
+    for (int e = lane; e < 80; e += 64) {
+        st.A[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+        st.B[e] = make_float4(0.f, 0.f, 0.f, __int_as_float(0));
+        st.gid[e] = 0u;
+    }
+
+    float T = 1.0f;
+    uint32_t last = 0;
+    bool done = !inside;
+    f32x4 acc[NBC][4];
+#pragma unroll
+    for (int nb = 0; nb < NBC; nb++)
+#pragma unroll
+        for (int pb = 0; pb < 4; pb++) acc[nb][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    int carry = 0;
+    uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
+    for (uint32_t base = rs; base < re; base += 64) {
+        if (__ballot(!done) == 0) break;
+        const uint32_t idx = base + lane;
+        const bool valid = idx < re;
+        const uint32_t gid = next_gid;
+        next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;
+        const int n = carry + stage_candidates_f(st, carry, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, a.splatA,
+                                                 a.splatB);
+        const int nfull = (base + 64 >= re) ? n : (n & ~15);
+        bool all_done = false;
+        for (int g0 = 0; g0 < nfull; g0 += 16) {
+            if (__ballot(!done) == 0) {
+                all_done = true;
+                break;
+            }
+            const int kn = min(16, nfull - g0);
+            // A fragments (feature nb*16+li of candidate g0+4t+lg), gathered now,
+            // consumed in phase 3; rows >= kn carry aT = 0
+            float av[4][NBC];
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const uint32_t gk = st.gid[g0 + 4 * t + lg];
+#pragma unroll
+                for (int nb = 0; nb < NBC; nb++) av[t][nb] = feature_at<NL>(a, gk, nb * 16 + li);
+            }
+            // phase 1: alpha of the 16 candidates (0 = skipped), independent
+#pragma unroll 4
+            for (int k = 0; k < 16; k++) {
+                const float4 A = st.A[g0 + k];
+                const float4 B = st.B[g0 + k];
+                const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
+                const bool cut = (k < kn) & !(power > 0.0f) & !(power < B.z);
+                const float alpha = fminf(0.99f, B.y * expf_det(power));
+                sAT[k * FS + lane] = (cut & !(alpha < 1.0f / 255.0f)) ? alpha : 0.f;
+            }
+            // phase 2: serial transmittance and early termination per pixel
+#pragma unroll 4
+            for (int k = 0; k < 16; k++) {
+                const float al = sAT[k * FS + lane];
+                const int posk = __float_as_int(st.B[g0 + k].w);
+                bool ok = (al != 0.f) & !done;
+                const float test_T = T * (1.0f - al);
+                const bool term = ok & (test_T < 0.0001f);
+                done = done | term;
+                ok = ok & !term;
+                sAT[k * FS + lane] = ok ? al * T : 0.f;
+                T = ok ? test_T : T;
+                last = ok ? (uint32_t)posk : last;
+            }
+            wave_lds_fence();
+            // phase 3: out[c][p] += F[k][c] * aT[k][p] on MFMA, k in order
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+#pragma unroll
+                for (int pb = 0; pb < 4; pb++) {
+                    const float bv = sAT[(4 * t + lg) * FS + pb * 16 + li];
+#pragma unroll
+                    for (int nb = 0; nb < NBC; nb++)
+                        acc[nb][pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][nb], bv, acc[nb][pb], 0, 0, 0);
+                }
+            }
+            wave_lds_fence();
+        }
+        if (all_done) break;
+        // carry the partial group to the front (source >= 16 > destination:
+        // no overlap; nothing to move when nfull == 0)
+        carry = n - nfull;
+        if (nfull > 0 && lane < carry) {
+            st.A[lane] = st.A[nfull + lane];
+            st.B[lane] = st.B[nfull + lane];
+            st.gid[lane] = st.gid[nfull + lane];
+        }
+        wave_lds_fence();
+    }
+    const size_t HW = (size_t)c.H * c.W;
+    if (inside) {
+        const size_t pix = (size_t)pm.py * c.W + pm.px;
+        a.final_T[pix] = T;
+        a.n_contrib[pix] = last;
+    }
+    sT[lane] = T;
+    wave_lds_fence();
+    // lane (lg, li) holds channel nb*16 + 4*lg + r of block pixel pb*16 + li
+#pragma unroll
+    for (int pb = 0; pb < 4; pb++) {
+        const int q = pb * 16 + li;
+        const int qx = pm.bx + (q & 7), qy = pm.by + (q >> 3);
+        if (qx < c.W && qy < c.H) {
+            const size_t pix = (size_t)qy * c.W + qx;
+            const float Tq = sT[q];
+#pragma unroll
+            for (int nb = 0; nb < NBC; nb++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int ch = nb * 16 + 4 * lg + r;
+                    if (ch < 3) a.out_color[ch * HW + pix] = fmaf(Tq, c.bg[ch], acc[nb][pb][r]);
+                    else if (ch < 3 + D) a.out_lang[(size_t)(ch - 3) * HW + pix] = acc[nb][pb][r];
+                }
+        }
     }
 }
 
