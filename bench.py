@@ -102,7 +102,8 @@ def pmc_traffic(stage):
         return None, None
     with open(files[-1]) as f:
         doc = json.load(f)
-    ks = [v for k, v in doc["kernels"].items() if k == "k_" + stage or k.startswith("k_" + stage + "<")]
+    ks = [v for k, v in doc["kernels"].items()
+          if k == "k_" + stage or k.startswith("k_" + stage + "<") or k.startswith("k_" + stage + "_mf<")]
     if not ks:
         return None, None
     return int(sum(v["traffic_bytes"] for v in ks)), os.path.relpath(files[-1], ROOT)
