@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 1
+#define LSR_ABI_VERSION 2
 
 enum {
     LSR_OK = 0,
@@ -95,7 +95,7 @@ typedef struct lsr_inputs {
 } lsr_inputs;
 
 typedef void* (*lsr_alloc_fn)(void* ctx, size_t bytes, int which);
-enum { LSR_BUF_GEOM = 0, LSR_BUF_BINNING = 1, LSR_BUF_IMAGE = 2, LSR_BUF_GRAD = 3 };
+enum { LSR_BUF_GEOM = 0, LSR_BUF_BINNING = 1, LSR_BUF_IMAGE = 2, LSR_BUF_GRAD = 3, LSR_BUF_DECODE = 4 };
 
 typedef struct lsr_fwd_out {
     float* out_color;     /* (3,H,W)  caller-allocated */
@@ -144,6 +144,18 @@ int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* 
 /* _C.mark_visible: present[i] = (view-space z of means3D[i]) > 0.2. */
 int lsr_mark_visible(int P, const float* means3D, const float* viewmatrix,
                      const float* projmatrix, uint8_t* present, void* stream);
+
+/* Codebook decode of a rendered language weight map;
+ * replaces, after render(), the reference's
+ *   F = einsum('ldk,lkn->ldn', codebooks.permute(0,2,1), W.view(L, K, H*W))
+ *   F = F / (F.norm(dim=1, keepdim=True) + eps)
+ * of render_language_feature_map_quick (eval_lerf.py:210-220,
+ * backend_renderer.py:16-36); with L = 1 and normalize = 0 it is
+ * compute_final_feature_map (scene/gaussian_model.py:545-550).
+ * weight_map (L*K, H, W), codebooks (L, K, Df), out (L, Df, H, W), all fp32
+ * device pointers.  K must be 64 and Df a multiple of 16. */
+int lsr_quick_decode(const float* weight_map, const float* codebooks, int L, int K, int Df, int H, int W,
+                     int normalize, float eps, float* out, lsr_alloc_fn alloc, void* alloc_ctx, void* stream);
 
 const char* lsr_strerror(int code);
 int lsr_abi_version(void);

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSR_LIB", os.path.join(_HERE, "liblsr.so"))
 
 LSR_OK = 0
-LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_GRAD = 0, 1, 2, 3
+LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_GRAD, LSR_BUF_DECODE = 0, 1, 2, 3, 4
 LSR_INDEX_F32, LSR_INDEX_I32, LSR_INDEX_I64 = 0, 1, 2
 
 _vp = ctypes.c_void_p
@@ -103,8 +103,8 @@ class BwdOut(ctypes.Structure):
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
 
-EXPORTS = ("lsr_forward", "lsr_backward", "lsr_mark_visible", "lsr_strerror", "lsr_abi_version",
-           "lsr_max_lang_dim", "lsr_profile_enable", "lsr_profile_reset", "lsr_profile_query")
+EXPORTS = ("lsr_forward", "lsr_backward", "lsr_mark_visible", "lsr_quick_decode", "lsr_strerror",
+           "lsr_abi_version", "lsr_max_lang_dim", "lsr_profile_enable", "lsr_profile_reset", "lsr_profile_query")
 
 _lib = None
 
@@ -129,6 +129,9 @@ def load(path: str | None = None):
     lib.lsr_backward.restype = ctypes.c_int
     lib.lsr_mark_visible.argtypes = [ctypes.c_int, _vp, _vp, _vp, _vp, _vp]
     lib.lsr_mark_visible.restype = ctypes.c_int
+    lib.lsr_quick_decode.argtypes = [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_float, _vp, ALLOC_FN, _vp, _vp]
+    lib.lsr_quick_decode.restype = ctypes.c_int
     lib.lsr_strerror.argtypes = [ctypes.c_int]
     lib.lsr_strerror.restype = ctypes.c_char_p
     lib.lsr_abi_version.restype = ctypes.c_int

@@ -188,6 +188,25 @@ const char* lsr_strerror(int code)
     }
 }
 
+int lsr_quick_decode(const float* weight_map, const float* codebooks, int L, int K, int Df, int H, int W,
+                     int normalize, float eps, float* out, lsr_alloc_fn alloc, void* alloc_ctx, void* stream)
+{
+    if (L < 0 || H < 0 || W < 0 || Df <= 0 || (Df % 16) != 0) return LSR_EINVAL;
+    if (K != 64) return LSR_EUNSUPPORTED;
+    if (L == 0 || H == 0 || W == 0) return LSR_OK;
+    if (!weight_map || !codebooks || !out) return LSR_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    float* G = nullptr;
+    if (normalize) {
+        if (!alloc) return LSR_EINVAL;
+        G = (float*)alloc(alloc_ctx, sizeof(float) * (size_t)L * K * K, LSR_BUF_DECODE);
+        if (!G) return LSR_ENOMEM;
+    }
+    if (lsr::launch_quick_decode(weight_map, codebooks, L, K, Df, H, W, normalize, eps, G, out, st) != hipSuccess)
+        return LSR_EHIP;
+    return LSR_OK;
+}
+
 int lsr_abi_version(void) { return LSR_ABI_VERSION; }
 
 int lsr_max_lang_dim(void) { return 64; }

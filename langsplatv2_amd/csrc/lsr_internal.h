@@ -73,4 +73,8 @@ int grad_row_width(int D);   // VP for a dense language dim
 hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t st);
 int lang_set_for(int D);     // compiled channel set >= D, or -1
 
+// quick.hip
+hipError_t launch_quick_decode(const float* wmap, const float* cb, int L, int K, int Df, int H, int W, int normalize,
+                               float eps, float* G, float* out, hipStream_t st);
+
 }  // namespace lsr

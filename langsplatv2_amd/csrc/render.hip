@@ -36,6 +36,16 @@
 #ifndef LSR_BWD_MF
 #define LSR_BWD_MF 1
 #endif
+#ifndef LSR_MF_WAVES
+#define LSR_MF_WAVES 2      // MFMA render kernels: min waves per SIMD (caps VGPRs at 256)
+#endif
+#define LSR_QUICK_KMAX 12   // quick path: (weight, code) pairs per Gaussian staged with the record
+#ifndef LSR_QUICK_QB
+#define LSR_QUICK_QB 4      // quick path: 64-channel slabs
+#endif
+#ifndef LSR_QUICK_MF
+#define LSR_QUICK_MF 1
+#endif
 #ifndef LSR_FWD_MF
 #define LSR_FWD_MF 0
 #endif
@@ -468,14 +478,24 @@ int lang_set_for(int D)
     return -1;
 }
 
+// (declarations carry the definitions' launch bounds: without them the
+// kernels would default to 1024-thread workgroups and a 128-register cap)
 template <int NL>
-__global__ void k_render_fwd_mf(RenderArgs a);
+__global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_fwd_mf(RenderArgs a);
+template <int QB>
+__global__ void __launch_bounds__(64) k_render_fwd_quick_mf(RenderArgs a);
 
 hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
 {
     const int T = a.cam.gx * a.cam.gy;
     if (T == 0) return hipSuccess;
     if (a.qw) {
+#if LSR_QUICK_MF
+        if (a.Dq % (16 * LSR_QUICK_QB) == 0 && a.K <= LSR_QUICK_KMAX) {   // channel slabs of 16 * LSR_QUICK_QB, one wave each
+            k_render_fwd_quick_mf<LSR_QUICK_QB><<<dim3(T * 4, a.Dq / (16 * LSR_QUICK_QB)), 64, 0, st>>>(a);
+            return hipGetLastError();
+        }
+#endif
         const size_t sm = (size_t)a.Dq * 64 * 4 + 64 * 32 + 64 * 12 + (size_t)64 * a.K * 8;
         k_render_fwd_quick<<<T * 4, 64, sm, st>>>(a);
         return hipGetLastError();
@@ -831,9 +851,6 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
 #define LSR_GR_STRIDE 36    // staged gradient rows (32 used floats)
 #ifndef LSR_P1_UNROLL
 #define LSR_P1_UNROLL 4
-#endif
-#ifndef LSR_MF_WAVES
-#define LSR_MF_WAVES 2      // min waves per SIMD (caps VGPRs at 256)
 #endif
 #define LSR_GRP_STRIDE 70   // dot/u and aT tiles: conflict-free fragment stores and A-fragment reads
 #define LSR_LOG2E 1.4426950408889634f
@@ -1310,6 +1327,198 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_fwd_mf(RenderArgs a
                     const int ch = nb * 16 + 4 * lg + r;
                     if (ch < 3) a.out_color[ch * HW + pix] = fmaf(Tq, c.bg[ch], acc[nb][pb][r]);
                     else if (ch < 3 + D) a.out_lang[(size_t)(ch - 3) * HW + pix] = acc[nb][pb][r];
+                }
+        }
+    }
+}
+
+
+// ------------------------------------------------ MFMA quick (sparse) forward ----
+// Sparse language channels: each Gaussian carries K (weight, code) pairs into
+// Dq output channels.  Per group of 16 candidates the pairs are expanded into
+// a dense 16 x Dq tile in LDS and accumulated out[q][p] += W[k][q] * aT[k][p]
+// on MFMA with the candidates as K in front-to-back order: bit-identical to the
+// sequential per-pixel blend (f32 MFMA == fmaf chain; unused codes add
+// fmaf(0, aT, acc) == acc).  Codes within one Gaussian must be distinct (as
+// utils/vq_utils.py:get_weights_and_indices produces them); a repeated code
+// would be summed before the multiply.  RGB stays on the VALU (phase 2).
+struct WaveStageQ {
+    float4 A[80];
+    float4 B[80];         // .w = 1-based tile-list position (int bits)
+    float4 C[80];         // rgb
+    uint32_t gid[80];
+};
+
+template <int QB>   // one slab of 16 * QB output channels per wave (blockIdx.y = slab)
+__global__ void __launch_bounds__(64) k_render_fwd_quick_mf(RenderArgs a)
+{
+    constexpr int DQ = 16 * QB;
+    const int q0 = (int)blockIdx.y * DQ;
+    const bool slab0 = blockIdx.y == 0;
+    constexpr int FS = LSR_FWD_STRIDE;
+    __shared__ WaveStageQ st;
+    __shared__ float sAT[16 * FS];
+    __shared__ float sWd[16 * DQ];    // dense weights of the group's candidates
+    __shared__ float sT[64];
+
+    const Cam& c = a.cam;
+    const WaveTile wt;
+    const int lane = threadIdx.x;
+    const int lg = lane >> 4, li = lane & 15;
+    const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
+    const bool inside = pm.px < c.W && pm.py < c.H;
+    const float pfx = (float)pm.px, pfy = (float)pm.py;
+    const uint32_t rs = a.tile_start[wt.tile], re = a.tile_start[wt.tile + 1];
+    const int K = a.K;
+
+    for (int e = lane; e < 80; e += 64) {
+        st.A[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+        st.B[e] = make_float4(0.f, 0.f, 0.f, __int_as_float(0));
+        st.C[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+        st.gid[e] = 0u;
+    }
+
+    float T = 1.0f, cr = 0.f, cg = 0.f, cbl = 0.f;
+    uint32_t last = 0;
+    bool done = !inside;
+    f32x4 acc[QB][4];
+#pragma unroll
+    for (int qb = 0; qb < QB; qb++)
+#pragma unroll
+        for (int pb = 0; pb < 4; pb++) acc[qb][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    int carry = 0;
+    uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
+    for (uint32_t base = rs; base < re; base += 64) {
+        if (__ballot(!done) == 0) break;
+        const uint32_t idx = base + lane;
+        const bool valid = idx < re;
+        const uint32_t gid = next_gid;
+        next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;
+        int nnew;
+        {
+            float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+            if (valid) {
+                A = a.splatA[gid];
+                B = a.splatB[gid];
+            }
+            const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), pm.bx, pm.by) &&
+                            block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, pm.bx, pm.by);
+            const uint64_t m = __ballot(ok);
+            if (ok) {
+                const int r = carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                st.A[r] = A;
+                st.B[r] = make_float4(B.x, B.y, B.z, __int_as_float((int)(idx - rs) + 1));
+                st.C[r] = make_float4(a.rgb[3 * (size_t)gid], a.rgb[3 * (size_t)gid + 1], a.rgb[3 * (size_t)gid + 2], 0.f);
+                st.gid[r] = gid;
+            }
+            wave_lds_fence();
+            nnew = __popcll(m);
+        }
+        const int n = carry + nnew;
+        const int nfull = (base + 64 >= re) ? n : (n & ~15);
+        bool all_done = false;
+        for (int g0 = 0; g0 < nfull; g0 += 16) {
+            if (__ballot(!done) == 0) {
+                all_done = true;
+                break;
+            }
+            const int kn = min(16, nfull - g0);
+            // dense weight tile: zero, then scatter the group's (weight, code) pairs
+            for (int e = lane; e < 16 * DQ / 4; e += 64) reinterpret_cast<float4*>(sWd)[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+            wave_lds_fence();
+            for (int e = lane; e < 16 * K; e += 64) {
+                const int k = e / K, j = e - k * K;
+                if (k < kn) {
+                    const size_t off = (size_t)st.gid[g0 + k] * K + j;
+                    int q;
+                    if (a.qidx_dtype == LSR_INDEX_F32) q = f2i(((const float*)a.qi)[off] + 0.5f);
+                    else if (a.qidx_dtype == LSR_INDEX_I32) q = ((const int32_t*)a.qi)[off];
+                    else q = (int)((const int64_t*)a.qi)[off];
+                    if (q >= q0 && q < q0 + DQ && q < a.Dq) sWd[k * DQ + (q - q0)] = a.qw[off];
+                }
+            }
+            // phase 1: alpha of the 16 candidates (0 = skipped), independent
+#pragma unroll 4
+            for (int k = 0; k < 16; k++) {
+                const float4 A = st.A[g0 + k];
+                const float4 B = st.B[g0 + k];
+                const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
+                const bool cut = (k < kn) & !(power > 0.0f) & !(power < B.z);
+                const float alpha = fminf(0.99f, B.y * expf_det(power));
+                sAT[k * FS + lane] = (cut & !(alpha < 1.0f / 255.0f)) ? alpha : 0.f;
+            }
+            // phase 2: serial transmittance, termination, RGB per pixel
+#pragma unroll 4
+            for (int k = 0; k < 16; k++) {
+                const float al = sAT[k * FS + lane];
+                const float4 B = st.B[g0 + k];
+                const float4 Cc = st.C[g0 + k];
+                bool ok = (al != 0.f) & !done;
+                const float test_T = T * (1.0f - al);
+                const bool term = ok & (test_T < 0.0001f);
+                done = done | term;
+                ok = ok & !term;
+                const float aT = ok ? al * T : 0.f;
+                if (ok) {
+                    cr = fmaf(Cc.x, aT, cr);
+                    cg = fmaf(Cc.y, aT, cg);
+                    cbl = fmaf(Cc.z, aT, cbl);
+                }
+                sAT[k * FS + lane] = aT;
+                T = ok ? test_T : T;
+                last = ok ? (uint32_t)__float_as_int(B.w) : last;
+            }
+            wave_lds_fence();
+            // phase 3: out[q][p] += W[k][q] * aT[k][p] on MFMA, k in order
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                float bv[4];
+#pragma unroll
+                for (int pb = 0; pb < 4; pb++) bv[pb] = sAT[(4 * t + lg) * FS + pb * 16 + li];
+#pragma unroll
+                for (int qb = 0; qb < QB; qb++) {
+                    const float av = sWd[(4 * t + lg) * DQ + qb * 16 + li];
+#pragma unroll
+                    for (int pb = 0; pb < 4; pb++)
+                        acc[qb][pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[pb], acc[qb][pb], 0, 0, 0);
+                }
+            }
+            wave_lds_fence();
+        }
+        if (all_done) break;
+        carry = n - nfull;
+        if (nfull > 0 && lane < carry) {   // source >= 16 > destination: no overlap
+            st.A[lane] = st.A[nfull + lane];
+            st.B[lane] = st.B[nfull + lane];
+            st.C[lane] = st.C[nfull + lane];
+            st.gid[lane] = st.gid[nfull + lane];
+        }
+        wave_lds_fence();
+    }
+    const size_t HW = (size_t)c.H * c.W;
+    if (inside && slab0) {
+        const size_t pix = (size_t)pm.py * c.W + pm.px;
+        a.final_T[pix] = T;
+        a.n_contrib[pix] = last;
+        a.out_color[pix] = fmaf(T, c.bg[0], cr);
+        a.out_color[HW + pix] = fmaf(T, c.bg[1], cg);
+        a.out_color[2 * HW + pix] = fmaf(T, c.bg[2], cbl);
+    }
+    // lane (lg, li) holds channel qb*16 + 4*lg + r of block pixel pb*16 + li
+#pragma unroll
+    for (int pb = 0; pb < 4; pb++) {
+        const int q = pb * 16 + li;
+        const int qx = pm.bx + (q & 7), qy = pm.by + (q >> 3);
+        if (qx < c.W && qy < c.H) {
+            const size_t pix = (size_t)qy * c.W + qx;
+#pragma unroll
+            for (int qb = 0; qb < QB; qb++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int ch = q0 + qb * 16 + 4 * lg + r;
+                    if (ch < a.Dq) a.out_lang[(size_t)ch * HW + pix] = acc[qb][pb][r];
                 }
         }
     }

@@ -1,0 +1,54 @@
+"""Codebook decode of rendered language weight maps on the MI355X matrix cores.
+
+The reference decodes the rasterizer's language weight map in PyTorch after
+render() (eval_lerf.py:210-220, backend_renderer.py:16-36):
+
+    W = weight_map.view(L, K, H * W)
+    F = torch.einsum('ldk,lkn->ldn', codebooks.permute(0, 2, 1), W).view(L, Df, H, W)
+    F = F / (F.norm(dim=1, keepdim=True) + 1e-10)
+
+and, for the dense training/eval map, compute_final_feature_map
+(scene/gaussian_model.py:545-550): codebooks.view(-1, Df).T @ W.
+
+`decode_language_features` does both in one HIP kernel (csrc/quick.hip:
+exact-f32 MFMA, per-pixel norms from the codebook Gram matrix, each output
+written once).  There is no CPU path.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from .rasterizer import _Alloc, _stream
+
+
+def decode_language_features(weight_map: torch.Tensor, codebooks: torch.Tensor, normalize: bool = True,
+                             eps: float = 1e-10) -> torch.Tensor:
+    """weight_map (L*K, H, W) fp32 CUDA, codebooks (L, K, Df) fp32 CUDA ->
+    features (L, Df, H, W); L2-normalised over Df per pixel when `normalize`."""
+    if weight_map.dim() != 3 or codebooks.dim() != 3:
+        raise ValueError("decode_language_features: weight_map must be (L*K, H, W) and codebooks (L, K, Df)")
+    L, K, Df = codebooks.shape
+    D, H, W = weight_map.shape
+    if D != L * K:
+        raise ValueError(f"decode_language_features: weight_map has {D} channels, codebooks need L*K = {L * K}")
+    if not (weight_map.is_cuda and codebooks.is_cuda):
+        raise RuntimeError("decode_language_features: tensors must be on the ROCm device (there is no CPU path)")
+    if K != 64 or Df % 16 != 0:
+        raise ValueError("decode_language_features: K must be 64 and Df a multiple of 16")
+    wm = weight_map.contiguous().float()
+    cb = codebooks.contiguous().float()
+    out = torch.empty((L, Df, H, W), dtype=torch.float32, device=weight_map.device)
+    alloc = _Alloc(weight_map.device)
+    lib = _lib.load()
+    rc = lib.lsr_quick_decode(wm.data_ptr(), cb.data_ptr(), L, K, Df, H, W, int(bool(normalize)), float(eps),
+                              out.data_ptr(), alloc.fn, None, _stream(weight_map.device))
+    _lib.check(rc, "lsr_quick_decode")
+    return out
+
+
+def compute_final_feature_map(weight_map: torch.Tensor, codebooks: torch.Tensor) -> torch.Tensor:
+    """scene/gaussian_model.py:545-550: codebooks.view(-1, Df).T @ weight_map.view(D, -1) -> (Df, H, W)."""
+    Df = codebooks.shape[-1]
+    cb = codebooks.reshape(1, -1, Df)
+    return decode_language_features(weight_map, cb, normalize=False)[0]

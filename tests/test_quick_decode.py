@@ -1,0 +1,72 @@
+"""Codebook decode of the quick language map (langsplatv2_amd.quick, csrc/quick.hip)
+against a float64 restatement of the reference's post-render lines
+(eval_lerf.py:214-218: einsum('ldk,lkn->ldn') then / (norm + 1e-10); and
+scene/gaussian_model.py:545-550 for the unnormalised dense map).
+
+Tolerance (floating point, not bit-exact: f32 MFMA sums and a Gram-matrix
+norm): normalised outputs within 2e-5 absolute (values in [-1, 1]);
+unnormalised within 2e-5 x max|ref|."""
+import numpy as np
+import pytest
+import torch
+
+from langsplatv2_amd import quick
+
+DEC_ATOL = 2e-5
+
+
+def ref_decode(wmap, cb, normalize=True, eps=1e-10):
+    L, K, Df = cb.shape
+    D, H, W = wmap.shape
+    F = np.einsum("ldk,lkn->ldn", np.transpose(cb, (0, 2, 1)).astype(np.float64),
+                  wmap.reshape(L, K, H * W).astype(np.float64)).reshape(L, Df, H, W)
+    if normalize:
+        F = F / (np.linalg.norm(F, axis=1, keepdims=True) + eps)
+    return F
+
+
+def test_validation_on_cpu():
+    with pytest.raises(ValueError):
+        quick.decode_language_features(torch.zeros(100, 4, 4), torch.zeros(3, 64, 512))
+    with pytest.raises(ValueError):
+        quick.decode_language_features(torch.zeros(4, 4), torch.zeros(3, 64, 512))
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        quick.decode_language_features(torch.zeros(192, 4, 4), torch.zeros(3, 64, 512))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W", [(37, 45), (64, 128), (1, 1)])
+def test_decode_matches_float64(gpu, H, W):
+    g = np.random.default_rng(H * 1000 + W)
+    L, K, Df = 3, 64, 512
+    # quick weights: sparse non-negative mixtures (top-k soft codes blended over depth)
+    wmap = (g.random((L * K, H, W)) * (g.random((L * K, H, W)) < 0.15)).astype(np.float32)
+    cb = g.standard_normal((L, K, Df)).astype(np.float32)
+    got = quick.decode_language_features(torch.from_numpy(wmap).to(gpu), torch.from_numpy(cb).to(gpu))
+    ref = ref_decode(wmap, cb)
+    np.testing.assert_allclose(got.cpu().numpy(), ref, atol=DEC_ATOL, rtol=0)
+
+
+@pytest.mark.gpu
+def test_unnormalised_and_dense_map(gpu):
+    g = np.random.default_rng(7)
+    wmap = g.random((64, 40, 56)).astype(np.float32)
+    cb = g.standard_normal((1, 64, 512)).astype(np.float32)
+    got = quick.compute_final_feature_map(torch.from_numpy(wmap).to(gpu), torch.from_numpy(cb).to(gpu))
+    ref = ref_decode(wmap, cb, normalize=False)[0]
+    scale = np.abs(ref).max()
+    np.testing.assert_allclose(got.cpu().numpy() / scale, ref / scale, atol=DEC_ATOL, rtol=0)
+
+
+@pytest.mark.gpu
+def test_render_then_decode_end_to_end(gpu, oracle_lib):
+    """Quick render through the drop-in rasterizer (weights bit-exact vs the
+    oracle) followed by the decode, vs the oracle's weight map decoded in float64."""
+    from harness import make_case, run_gpu_forward, oracle_problem
+    case = make_case(N=3000, W=96, H=80, seed=21, sh_degree=None, quick_k=4)
+    ref_f = oracle_lib.forward(oracle_problem(case))
+    got_f = run_gpu_forward(case, gpu)
+    np.testing.assert_array_equal(got_f["lang"], ref_f["lang"])
+    cb = np.random.default_rng(3).standard_normal((3, 64, 512)).astype(np.float32)
+    feats = quick.decode_language_features(torch.from_numpy(got_f["lang"]).to(gpu), torch.from_numpy(cb).to(gpu))
+    np.testing.assert_allclose(feats.cpu().numpy(), ref_decode(ref_f["lang"], cb), atol=DEC_ATOL, rtol=0)
