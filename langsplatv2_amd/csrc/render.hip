@@ -484,6 +484,8 @@ template <int NL>
 __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_fwd_mf(RenderArgs a);
 template <int QB>
 __global__ void __launch_bounds__(64) k_render_fwd_quick_mf(RenderArgs a);
+template <int QB, int NS>
+__global__ void __launch_bounds__(64 * NS) k_render_fwd_quick_wg(RenderArgs a);
 
 hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
 {
@@ -491,9 +493,15 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
     if (T == 0) return hipSuccess;
     if (a.qw) {
 #if LSR_QUICK_MF
-        if (a.Dq % (16 * LSR_QUICK_QB) == 0 && a.K <= LSR_QUICK_KMAX) {   // channel slabs of 16 * LSR_QUICK_QB, one wave each
-            k_render_fwd_quick_mf<LSR_QUICK_QB><<<dim3(T * 4, a.Dq / (16 * LSR_QUICK_QB)), 64, 0, st>>>(a);
-            return hipGetLastError();
+        if (a.K <= LSR_QUICK_KMAX) {
+            // one workgroup of Dq/64 waves per 8x8 block (64-channel slabs)
+            if (a.Dq == 192) { k_render_fwd_quick_wg<4, 3><<<T * 4, 192, 0, st>>>(a); return hipGetLastError(); }
+            if (a.Dq == 128) { k_render_fwd_quick_wg<4, 2><<<T * 4, 128, 0, st>>>(a); return hipGetLastError(); }
+            if (a.Dq == 64) { k_render_fwd_quick_wg<4, 1><<<T * 4, 64, 0, st>>>(a); return hipGetLastError(); }
+            if (a.Dq % (16 * LSR_QUICK_QB) == 0) {   // other widths: one wave per slab, blend re-run per slab
+                k_render_fwd_quick_mf<LSR_QUICK_QB><<<dim3(T * 4, a.Dq / (16 * LSR_QUICK_QB)), 64, 0, st>>>(a);
+                return hipGetLastError();
+            }
         }
 #endif
         const size_t sm = (size_t)a.Dq * 64 * 4 + 64 * 32 + 64 * 12 + (size_t)64 * a.K * 8;
@@ -1425,20 +1433,28 @@ __global__ void __launch_bounds__(64) k_render_fwd_quick_mf(RenderArgs a)
                 break;
             }
             const int kn = min(16, nfull - g0);
-            // dense weight tile: zero, then scatter the group's (weight, code) pairs
-            for (int e = lane; e < 16 * DQ / 4; e += 64) reinterpret_cast<float4*>(sWd)[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-            wave_lds_fence();
-            for (int e = lane; e < 16 * K; e += 64) {
+            // the group's (weight, code) pairs: loads issued now, scattered into
+            // the dense tile after phases 1-2 (which hide their latency)
+            constexpr int PE = (16 * LSR_QUICK_KMAX + 63) / 64;   // pairs per lane
+            float pw[PE];
+            int pq[PE];
+#pragma unroll
+            for (int i = 0; i < PE; i++) {
+                const int e = lane + 64 * i;
                 const int k = e / K, j = e - k * K;
-                if (k < kn) {
+                pq[i] = -1;
+                pw[i] = 0.f;
+                if (e < 16 * K && k < kn) {
                     const size_t off = (size_t)st.gid[g0 + k] * K + j;
                     int q;
                     if (a.qidx_dtype == LSR_INDEX_F32) q = f2i(((const float*)a.qi)[off] + 0.5f);
                     else if (a.qidx_dtype == LSR_INDEX_I32) q = ((const int32_t*)a.qi)[off];
                     else q = (int)((const int64_t*)a.qi)[off];
-                    if (q >= q0 && q < q0 + DQ && q < a.Dq) sWd[k * DQ + (q - q0)] = a.qw[off];
+                    pw[i] = a.qw[off];
+                    pq[i] = (q >= q0 && q < q0 + DQ && q < a.Dq) ? k * DQ + (q - q0) : -1;
                 }
             }
+            for (int e = lane; e < 16 * DQ / 4; e += 64) reinterpret_cast<float4*>(sWd)[e] = make_float4(0.f, 0.f, 0.f, 0.f);
             // phase 1: alpha of the 16 candidates (0 = skipped), independent
 #pragma unroll 4
             for (int k = 0; k < 16; k++) {
@@ -1470,6 +1486,10 @@ __global__ void __launch_bounds__(64) k_render_fwd_quick_mf(RenderArgs a)
                 T = ok ? test_T : T;
                 last = ok ? (uint32_t)__float_as_int(B.w) : last;
             }
+            wave_lds_fence();   // zeroed tile before the scatter
+#pragma unroll
+            for (int i = 0; i < PE; i++)
+                if (pq[i] >= 0) sWd[pq[i]] = pw[i];
             wave_lds_fence();
             // phase 3: out[q][p] += W[k][q] * aT[k][p] on MFMA, k in order
 #pragma unroll
@@ -1507,6 +1527,202 @@ __global__ void __launch_bounds__(64) k_render_fwd_quick_mf(RenderArgs a)
         a.out_color[2 * HW + pix] = fmaf(T, c.bg[2], cbl);
     }
     // lane (lg, li) holds channel qb*16 + 4*lg + r of block pixel pb*16 + li
+#pragma unroll
+    for (int pb = 0; pb < 4; pb++) {
+        const int q = pb * 16 + li;
+        const int qx = pm.bx + (q & 7), qy = pm.by + (q >> 3);
+        if (qx < c.W && qy < c.H) {
+            const size_t pix = (size_t)qy * c.W + qx;
+#pragma unroll
+            for (int qb = 0; qb < QB; qb++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int ch = q0 + qb * 16 + 4 * lg + r;
+                    if (ch < a.Dq) a.out_lang[(size_t)ch * HW + pix] = acc[qb][pb][r];
+                }
+        }
+    }
+}
+
+
+// Quick path, one workgroup of NS waves per 8x8 block: wave 0 stages the
+// candidates and runs the blend phases (alpha, serial T, RGB) once; every wave
+// then scatters the (weight, code) pairs of its 16*QB-channel slab into a
+// dense tile and accumulates its slab on MFMA.  Same arithmetic, order and
+// bit-exactness as k_render_fwd_quick_mf, without re-running the blend per slab.
+template <int QB, int NS>
+__global__ void __launch_bounds__(64 * NS) k_render_fwd_quick_wg(RenderArgs a)
+{
+    constexpr int DQ = 16 * QB;
+    constexpr int FS = LSR_FWD_STRIDE;
+    constexpr int PE = (16 * LSR_QUICK_KMAX + 63) / 64;
+    __shared__ WaveStageQ st;
+    __shared__ float sAT[16 * FS];
+    __shared__ float sWd[NS][16 * DQ];
+    __shared__ int sN[2];
+
+    const Cam& c = a.cam;
+    const WaveTile wt;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int lg = lane >> 4, li = lane & 15;
+    const int q0 = w * DQ;
+    const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
+    const bool inside = pm.px < c.W && pm.py < c.H;
+    const float pfx = (float)pm.px, pfy = (float)pm.py;
+    const uint32_t rs = a.tile_start[wt.tile], re = a.tile_start[wt.tile + 1];
+    const int K = a.K;
+
+    if (w == 0) {
+        for (int e = lane; e < 80; e += 64) {
+            st.A[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+            st.B[e] = make_float4(0.f, 0.f, 0.f, __int_as_float(0));
+            st.C[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+            st.gid[e] = 0u;
+        }
+    }
+    float T = 1.0f, cr = 0.f, cg = 0.f, cbl = 0.f;
+    uint32_t last = 0;
+    bool done = !inside;
+    f32x4 acc[QB][4];
+#pragma unroll
+    for (int qb = 0; qb < QB; qb++)
+#pragma unroll
+        for (int pb = 0; pb < 4; pb++) acc[qb][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    int carry = 0;
+    uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
+    for (uint32_t base = rs; base < re; base += 64) {
+        if (w == 0) {
+            const bool stop = __ballot(!done) == 0;
+            int nnew = 0;
+            if (!stop) {
+                const uint32_t idx = base + lane;
+                const bool valid = idx < re;
+                const uint32_t gid = next_gid;
+                next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;
+                float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+                if (valid) {
+                    A = a.splatA[gid];
+                    B = a.splatB[gid];
+                }
+                const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), pm.bx, pm.by) &&
+                                block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, pm.bx, pm.by);
+                const uint64_t m = __ballot(ok);
+                if (ok) {
+                    const int r = carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    st.A[r] = A;
+                    st.B[r] = make_float4(B.x, B.y, B.z, __int_as_float((int)(idx - rs) + 1));
+                    st.C[r] = make_float4(a.rgb[3 * (size_t)gid], a.rgb[3 * (size_t)gid + 1],
+                                          a.rgb[3 * (size_t)gid + 2], 0.f);
+                    st.gid[r] = gid;
+                }
+                nnew = __popcll(m);
+            }
+            if (lane == 0) {
+                sN[0] = stop ? -1 : carry + nnew;
+            }
+        }
+        __syncthreads();
+        const int n = sN[0];
+        if (n < 0) break;
+        const int nfull = (base + 64 >= re) ? n : (n & ~15);
+        for (int g0 = 0; g0 < nfull; g0 += 16) {
+            const int kn = min(16, nfull - g0);
+            // this slab's (weight, code) pairs: loads issued now, scattered after the blend
+            float pw[PE];
+            int pq[PE];
+#pragma unroll
+            for (int i = 0; i < PE; i++) {
+                const int e = lane + 64 * i;
+                const int k = e / K, j = e - k * K;
+                pq[i] = -1;
+                pw[i] = 0.f;
+                if (e < 16 * K && k < kn) {
+                    const size_t off = (size_t)st.gid[g0 + k] * K + j;
+                    int q;
+                    if (a.qidx_dtype == LSR_INDEX_F32) q = f2i(((const float*)a.qi)[off] + 0.5f);
+                    else if (a.qidx_dtype == LSR_INDEX_I32) q = ((const int32_t*)a.qi)[off];
+                    else q = (int)((const int64_t*)a.qi)[off];
+                    pw[i] = a.qw[off];
+                    pq[i] = (q >= q0 && q < q0 + DQ && q < a.Dq) ? k * DQ + (q - q0) : -1;
+                }
+            }
+            for (int e = lane; e < 16 * DQ / 4; e += 64) reinterpret_cast<float4*>(sWd[w])[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (w == 0) {
+                // phase 1: alpha of the 16 candidates (0 = skipped), independent
+#pragma unroll 4
+                for (int k = 0; k < 16; k++) {
+                    const float4 A = st.A[g0 + k];
+                    const float4 B = st.B[g0 + k];
+                    const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
+                    const bool cut = (k < kn) & !(power > 0.0f) & !(power < B.z);
+                    const float alpha = fminf(0.99f, B.y * expf_det(power));
+                    sAT[k * FS + lane] = (cut & !(alpha < 1.0f / 255.0f)) ? alpha : 0.f;
+                }
+                // phase 2: serial transmittance, termination, RGB per pixel
+#pragma unroll 4
+                for (int k = 0; k < 16; k++) {
+                    const float al = sAT[k * FS + lane];
+                    const float4 B = st.B[g0 + k];
+                    const float4 Cc = st.C[g0 + k];
+                    bool ok = (al != 0.f) & !done;
+                    const float test_T = T * (1.0f - al);
+                    const bool term = ok & (test_T < 0.0001f);
+                    done = done | term;
+                    ok = ok & !term;
+                    const float aT = ok ? al * T : 0.f;
+                    if (ok) {
+                        cr = fmaf(Cc.x, aT, cr);
+                        cg = fmaf(Cc.y, aT, cg);
+                        cbl = fmaf(Cc.z, aT, cbl);
+                    }
+                    sAT[k * FS + lane] = aT;
+                    T = ok ? test_T : T;
+                    last = ok ? (uint32_t)__float_as_int(B.w) : last;
+                }
+            }
+            wave_lds_fence();   // this wave's zeroed slab tile before its scatter
+#pragma unroll
+            for (int i = 0; i < PE; i++)
+                if (pq[i] >= 0) sWd[w][pq[i]] = pw[i];
+            __syncthreads();    // aT tile (wave 0) and every slab tile complete
+            // phase 3: out[q][p] += W[k][q] * aT[k][p] on MFMA, k in order
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                float bv[4];
+#pragma unroll
+                for (int pb = 0; pb < 4; pb++) bv[pb] = sAT[(4 * t + lg) * FS + pb * 16 + li];
+#pragma unroll
+                for (int qb = 0; qb < QB; qb++) {
+                    const float av = sWd[w][(4 * t + lg) * DQ + qb * 16 + li];
+#pragma unroll
+                    for (int pb = 0; pb < 4; pb++)
+                        acc[qb][pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[pb], acc[qb][pb], 0, 0, 0);
+                }
+            }
+            __syncthreads();    // before the next group overwrites the tiles
+        }
+        if (w == 0) {
+            carry = n - nfull;
+            if (nfull > 0 && lane < carry) {   // source >= 16 > destination: no overlap
+                st.A[lane] = st.A[nfull + lane];
+                st.B[lane] = st.B[nfull + lane];
+                st.C[lane] = st.C[nfull + lane];
+                st.gid[lane] = st.gid[nfull + lane];
+            }
+        }
+        __syncthreads();
+    }
+    const size_t HW = (size_t)c.H * c.W;
+    if (inside && w == 0) {
+        const size_t pix = (size_t)pm.py * c.W + pm.px;
+        a.final_T[pix] = T;
+        a.n_contrib[pix] = last;
+        a.out_color[pix] = fmaf(T, c.bg[0], cr);
+        a.out_color[HW + pix] = fmaf(T, c.bg[1], cg);
+        a.out_color[2 * HW + pix] = fmaf(T, c.bg[2], cbl);
+    }
 #pragma unroll
     for (int pb = 0; pb < 4; pb++) {
         const int q = pb * 16 + li;
