@@ -16,6 +16,10 @@
 // duplicates emitted in Gaussian order.
 #include "lsr_internal.h"
 
+#ifndef LSR_SORT_DPP
+#define LSR_SORT_DPP 1
+#endif
+
 namespace lsr {
 
 // ---------------------------------------------------------------- scan ----
@@ -429,6 +433,90 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m)
     return ((uint64_t)hi << 32) | lo;
 }
 
+// Partner value across lanes l <-> l ^ M without the LDS crossbar where the
+// ISA has a register path: v_permlane32_swap (M = 32), v_permlane16_swap
+// (M = 16), DPP row_ror:8 (M = 8), DPP quad_perm (M = 2, 1); ds_bpermute
+// only for M = 4.
+template <int M>
+__device__ __forceinline__ uint32_t xor_lane_u32(uint32_t x)
+{
+    const int lane = threadIdx.x & 63;
+    if constexpr (M == 32) {
+        auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (lane & 32) ? r[0] : r[1];
+    } else if constexpr (M == 16) {
+        auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return (lane & 16) ? r[0] : r[1];
+    } else if constexpr (M == 8) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false);   // row_ror:8
+    } else if constexpr (M == 2) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+    } else if constexpr (M == 1) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+    } else {
+        return (uint32_t)__shfl_xor((int)x, M, 64);
+    }
+}
+
+template <int M>
+__device__ __forceinline__ uint64_t xor_lane_u64(uint64_t v)
+{
+#if LSR_SORT_DPP
+    const uint32_t lo = xor_lane_u32<M>((uint32_t)v);
+    const uint32_t hi = xor_lane_u32<M>((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+#else
+    return shfl_xor_u64(v, M);
+#endif
+}
+
+template <int KPL, int K, int J>
+__device__ __forceinline__ void wave_sort_xstep(uint64_t (&v)[KPL])
+{
+    constexpr int M = J / KPL;
+    const int lane = threadIdx.x & 63;
+    // K >= 2J >= 2 KPL: the direction bit of element lane*KPL + r is the
+    // lane's alone, so one flag serves all KPL elements
+    const bool take_min = ((lane & M) == 0) == (((lane * KPL) & K) == 0);
+#pragma unroll
+    for (int r = 0; r < KPL; r++) {
+        const uint64_t o = xor_lane_u64<M>(v[r]);
+        v[r] = ((v[r] < o) == take_min) ? v[r] : o;   // keep own value iff it is the wanted one
+    }
+}
+
+template <int KPL, int K, int J>
+__device__ __forceinline__ void wave_sort_steps(uint64_t (&v)[KPL])
+{
+    if constexpr (J >= 1) {
+        if constexpr (J < KPL) {
+            const int lane = threadIdx.x & 63;
+#pragma unroll
+            for (int r = 0; r < KPL; r++) {
+                if (r & J) continue;
+                const int e = lane * KPL + r;
+                const bool asc = (e & K) == 0;
+                const uint64_t a = v[r], b = v[r | J];
+                const bool sw = asc ? (a > b) : (a < b);
+                v[r] = sw ? b : a;
+                v[r | J] = sw ? a : b;
+            }
+        } else {
+            wave_sort_xstep<KPL, K, J>(v);
+        }
+        wave_sort_steps<KPL, K, J / 2>(v);
+    }
+}
+
+template <int KPL, int K>
+__device__ __forceinline__ void wave_sort_stages(uint64_t (&v)[KPL])
+{
+    if constexpr (K <= 64 * KPL) {
+        wave_sort_steps<KPL, K, K / 2>(v);
+        wave_sort_stages<KPL, 2 * K>(v);
+    }
+}
+
 template <int KPL>
 __device__ __forceinline__ void wave_sort_tile(uint64_t* __restrict__ g, uint32_t* __restrict__ out, int n)
 {
@@ -439,36 +527,7 @@ __device__ __forceinline__ void wave_sort_tile(uint64_t* __restrict__ g, uint32_
         const int e = lane * KPL + r;
         v[r] = e < n ? g[e] : ~0ull;
     }
-#pragma unroll
-    for (int k = 2; k <= 64 * KPL; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j >= 1; j >>= 1) {
-            if (j < KPL) {
-#pragma unroll
-                for (int r = 0; r < KPL; r++) {
-                    if (r & j) continue;
-                    const int e = lane * KPL + r;
-                    const bool asc = (e & k) == 0;
-                    const uint64_t a = v[r], b = v[r | j];
-                    const bool sw = asc ? (a > b) : (a < b);
-                    v[r] = sw ? b : a;
-                    v[r | j] = sw ? a : b;
-                }
-            } else {
-                const int m = j / KPL;
-                const bool lower = (lane & m) == 0;
-#pragma unroll
-                for (int r = 0; r < KPL; r++) {
-                    const int e = lane * KPL + r;
-                    const bool asc = (e & k) == 0;
-                    const uint64_t o = shfl_xor_u64(v[r], m);
-                    const bool take_min = (lower == asc);
-                    const uint64_t mn = v[r] < o ? v[r] : o, mx = v[r] < o ? o : v[r];
-                    v[r] = take_min ? mn : mx;
-                }
-            }
-        }
-    }
+    wave_sort_stages<KPL, 2>(v);
 #pragma unroll
     for (int r = 0; r < KPL; r++) {
         const int e = lane * KPL + r;
