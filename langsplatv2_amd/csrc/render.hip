@@ -43,6 +43,12 @@
 #ifndef LSR_QUICK_QB
 #define LSR_QUICK_QB 4      // quick path: 64-channel slabs
 #endif
+#ifndef LSR_FWD_MF_WIDE
+#define LSR_FWD_MF_WIDE 1   // D = 64: MFMA-accumulated forward
+#endif
+#ifndef LSR_BWD_MF_WIDE
+#define LSR_BWD_MF_WIDE 1   // D = 32, 64: factorised MFMA backward
+#endif
 #ifndef LSR_QUICK_MF
 #define LSR_QUICK_MF 1
 #endif
@@ -520,8 +526,14 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
         case 8: k_render_fwd<8><<<4 * T, 64, 0, st>>>(a); break;
         case 16: k_render_fwd<16><<<4 * T, 64, 0, st>>>(a); break;
 #endif
+#if LSR_FWD_MF_WIDE
+        // measured (cfg3 geometry): D = 32 legacy 0.78 vs MFMA 0.81 ms; D = 64 legacy 1.38 vs MFMA 1.13 ms
+        case 32: k_render_fwd<32><<<4 * T, 64, 0, st>>>(a); break;
+        case 64: k_render_fwd_mf<64><<<4 * T, 64, 0, st>>>(a); break;
+#else
         case 32: k_render_fwd<32><<<4 * T, 64, 0, st>>>(a); break;
         case 64: k_render_fwd<64><<<4 * T, 64, 0, st>>>(a); break;
+#endif
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -856,7 +868,6 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
 
 #define LSR_DOT_STRIDE 68   // sDot row stride: conflict-free fragment stores
 #define LSR_MOM_STRIDE 8
-#define LSR_GR_STRIDE 36    // staged gradient rows (32 used floats)
 #ifndef LSR_P1_UNROLL
 #define LSR_P1_UNROLL 4
 #endif
@@ -921,7 +932,9 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     __shared__ float sDU[16 * GS];    // dot[k][p], overwritten in place by u[k][p]
     __shared__ float sAT[16 * GS];    // G[k][p] (phase 1), then aT[k][p] (phase 2)
     __shared__ float sMom[16 * LSR_MOM_STRIDE];
-    __shared__ float sGr[16 * LSR_GR_STRIDE];   // the group's gradient rows
+    constexpr int GRL = (LSR_GROW_LANG + NL + 15) / 16;   // 16-float lines per gradient row
+    constexpr int GRS = 16 * GRL + 4;                     // staged row stride
+    __shared__ float sGr[16 * GRS];   // the group's gradient rows
 
     const RenderArgs& a = b.f;
     const Cam& c = a.cam;
@@ -1104,7 +1117,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 if (chn < 3 + NL) {
                     const int col = chn < 3 ? 6 + chn : LSR_GROW_LANG + chn - 3;
 #pragma unroll
-                    for (int r = 0; r < 4; r++) sGr[(4 * lg + r) * LSR_GR_STRIDE + col] = ch[nb][r];
+                    for (int r = 0; r < 4; r++) sGr[(4 * lg + r) * GRS + col] = ch[nb][r];
                 }
             }
             if (li < 6) {
@@ -1124,7 +1137,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 const float Sdxy = fmaf(X, fmaf(Y, S0, -S2), fmaf(-Y, S1, S4));
                 const float Sdyy = fmaf(Y, fmaf(Y, S0, -2.f * S2), S5);
                 const float o = B.y;
-                float* gr = sGr + lane * LSR_GR_STRIDE;
+                float* gr = sGr + lane * GRS;
                 gr[0] = -o * ddelx_dx * fmaf(A.z, Sdx, A.w * Sdy);
                 gr[1] = -o * ddely_dy * fmaf(B.x, Sdy, A.w * Sdx);
                 gr[2] = -0.5f * o * Sdxx;
@@ -1134,13 +1147,13 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             }
             wave_lds_fence();
 #pragma unroll
-            for (int h = 0; h < (LSR_GROW_LANG + NL > 16 ? 2 : 1); h++) {
+            for (int h = 0; h < GRL; h++) {
                 const int f = 16 * h + li;
                 const bool fcol = (f < 9) | ((f >= LSR_GROW_LANG) & (f < LSR_GROW_LANG + D));
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const int slot = 4 * q + lg;
-                    const float v = sGr[slot * LSR_GR_STRIDE + f];
+                    const float v = sGr[slot * GRS + f];
                     if (fcol & (slot < kn) & (v != 0.f))
                         LSR_MF_ATOMIC(b.grad_acc + (size_t)st.gid[g0 + slot] * VP + f, v);
                 }
@@ -1756,8 +1769,13 @@ hipError_t launch_render_bwd(const RenderBwdArgs& b, hipStream_t st)
         case 8: k_render_bwd<8><<<4 * T, 64, 0, st>>>(b); break;
         case 16: k_render_bwd<16><<<4 * T, 64, 0, st>>>(b); break;
 #endif
+#if LSR_BWD_MF_WIDE
+        case 32: k_render_bwd_mf<32><<<4 * T, 64, 0, st>>>(b); break;
+        case 64: k_render_bwd_mf<64><<<4 * T, 64, 0, st>>>(b); break;
+#else
         case 32: k_render_bwd<32><<<4 * T, 64, 0, st>>>(b); break;
         case 64: k_render_bwd<64><<<4 * T, 64, 0, st>>>(b); break;
+#endif
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
