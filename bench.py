@@ -214,8 +214,23 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    # per-stage breakdown: a separate untimed pass with every stage bracketed
+    # by events (each bracket idles the stream a few us, so the timed region
+    # below brackets only the dominant stage, for the live roofline)
+    _lib.profile_stages(None)
+    _lib.profile_reset()
+    _lib.profile_enable(True)
+    for _ in range(max(2, min(args.steps, 5))):
+        step()
+    torch.cuda.synchronize()
+    _lib.profile_enable(False)
+    stages = _lib.profile_query()
+    per_stage = {k: dict(ms_per_launch=(ms / calls if calls else 0.0), launches=calls)
+                 for k, (ms, calls) in stages.items() if calls}
+    dom = max(per_stage, key=lambda k: per_stage[k]["ms_per_launch"])
     if world > 1:
         dist.barrier()
+    _lib.profile_stages([dom])
     _lib.profile_reset()
     _lib.profile_enable(True)
     torch.cuda.synchronize()
@@ -229,7 +244,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     _lib.profile_enable(False)
-    stages = _lib.profile_query()
+    _lib.profile_stages(None)
+    dom_ms_s, dom_calls = _lib.profile_query()[dom]
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -241,10 +257,7 @@ def main():
         with torch.no_grad():
             gd = {k: v.detach() for k, v in g.items()}
             bytes_, info = algorithmic_bytes(gd, rs, D, 48)
-        per_stage = {k: dict(ms_per_launch=(ms / calls if calls else 0.0), launches=calls)
-                     for k, (ms, calls) in stages.items() if calls}
-        dom = max(per_stage, key=lambda k: per_stage[k]["ms_per_launch"])
-        dom_ms = per_stage[dom]["ms_per_launch"]
+        dom_ms = dom_ms_s / dom_calls if dom_calls else 0.0
         dom_gbps = bytes_[dom] / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
         traffic, traffic_src = pmc_traffic(dom)
         step_ms = elapsed / args.steps * 1e3
@@ -283,6 +296,7 @@ def main():
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": int(bytes_[dom]),
                 "ms_per_launch": round(dom_ms, 4),
+                "launches_timed": dom_calls,
             },
             "hbm_step": {"algorithmic_bytes": int(total_bytes),
                          "GBps_over_kernels": round(total_bytes / (kernel_ms * 1e-3) / 1e9, 1) if kernel_ms else 0,

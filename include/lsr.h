@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 2
+#define LSR_ABI_VERSION 3
 
 enum {
     LSR_OK = 0,
@@ -94,6 +94,10 @@ typedef struct lsr_inputs {
     const void* language_feature_indices;        /* (N,K) or NULL */
 } lsr_inputs;
 
+/* Workspace allocator.  lsr_forward may request LSR_BUF_BINNING twice in
+ * one call: a speculative buffer sized from the previous call's M (taken
+ * while the GPU is still counting) and, only if M outgrew it, a second one;
+ * the last pointer returned for a kind is the one the call uses. */
 typedef void* (*lsr_alloc_fn)(void* ctx, size_t bytes, int which);
 enum { LSR_BUF_GEOM = 0, LSR_BUF_BINNING = 1, LSR_BUF_IMAGE = 2, LSR_BUF_GRAD = 3, LSR_BUF_DECODE = 4 };
 
@@ -103,7 +107,7 @@ typedef struct lsr_fwd_out {
     int32_t* radii;       /* (N,) caller-allocated */
     /* filled by lsr_forward: */
     void* geom;    size_t geom_bytes;
-    void* binning; size_t binning_bytes;
+    void* binning; size_t binning_bytes;   /* capacity (>= layout for num_rendered) */
     void* image;   size_t image_bytes;
     int64_t num_rendered;
 } lsr_fwd_out;
@@ -169,6 +173,12 @@ int lsr_max_lang_dim(void);
  * lsr_profile_query fills up to max_stages (name, total ms, call count)
  * triples since the last reset and returns the number filled. */
 void lsr_profile_enable(int on);
+/* Restrict the timed stages to a comma-separated list of stage names
+ * ("render_bwd,render_fwd"); NULL or "" selects every stage.  Each timed
+ * stage adds two event records (a few us of stream idle each), so bench.py
+ * times only the roofline kernel inside its timed region.  Returns
+ * LSR_EINVAL for an unknown name (mask unchanged). */
+int lsr_profile_stages(const char* names);
 void lsr_profile_reset(void);
 int lsr_profile_query(const char** names, double* ms, int64_t* calls, int max_stages);
 

@@ -104,7 +104,8 @@ class BwdOut(ctypes.Structure):
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
 
 EXPORTS = ("lsr_forward", "lsr_backward", "lsr_mark_visible", "lsr_quick_decode", "lsr_strerror",
-           "lsr_abi_version", "lsr_max_lang_dim", "lsr_profile_enable", "lsr_profile_reset", "lsr_profile_query")
+           "lsr_abi_version", "lsr_max_lang_dim", "lsr_profile_enable", "lsr_profile_stages", "lsr_profile_reset",
+           "lsr_profile_query")
 
 _lib = None
 
@@ -138,6 +139,8 @@ def load(path: str | None = None):
     lib.lsr_max_lang_dim.restype = ctypes.c_int
     lib.lsr_profile_enable.argtypes = [ctypes.c_int]
     lib.lsr_profile_enable.restype = None
+    lib.lsr_profile_stages.argtypes = [ctypes.c_char_p]
+    lib.lsr_profile_stages.restype = ctypes.c_int
     lib.lsr_profile_reset.restype = None
     lib.lsr_profile_query.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
@@ -155,6 +158,12 @@ def check(rc: int, what: str):
 
 def profile_enable(on: bool = True):
     load().lsr_profile_enable(1 if on else 0)
+
+
+def profile_stages(names=None):
+    """Time only the named stages (None = all); see lsr_profile_stages."""
+    arg = None if not names else ",".join(names).encode()
+    check(load().lsr_profile_stages(arg), "lsr_profile_stages")
 
 
 def profile_reset():

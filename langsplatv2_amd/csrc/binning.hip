@@ -113,6 +113,29 @@ hipError_t launch_scan_u32(const uint32_t* in, uint32_t* out, uint64_t* part, si
     return hipGetLastError();
 }
 
+// Publish the scan total: writes it as the closing entry of the tile-start
+// array (tile_end, may be null) and, packed with a sequence number, into a
+// coherent pinned host word the host spins on (lsr_api.hip wait_published):
+// the host needs M to size the binning workspace, and polling one
+// PCIe-visible word avoids the staged D2H copy + stream-synchronise wake-up
+// latency in the middle of every forward.  Totals >= 2^32 - 1 saturate (the
+// host reports LSR_EOVERFLOW).
+__global__ void k_publish_total(const uint64_t* __restrict__ total, uint32_t* __restrict__ tile_end,
+                                uint64_t* host_slot, uint32_t seq)
+{
+    const uint64_t m = *total;
+    const uint32_t m32 = m >= 0xffffffffull ? 0xffffffffu : (uint32_t)m;
+    if (tile_end) *tile_end = m32;
+    __atomic_store_n(host_slot, ((uint64_t)seq << 32) | m32, __ATOMIC_RELEASE);
+}
+
+hipError_t launch_publish_total(const uint64_t* total, uint32_t* tile_end, uint64_t* host_slot, uint32_t seq,
+                                hipStream_t st)
+{
+    k_publish_total<<<1, 1, 0, st>>>(total, tile_end, host_slot, seq);
+    return hipGetLastError();
+}
+
 // ----------------------------------------------------- duplicate / scatter --
 __global__ void __launch_bounds__(256) k_duplicate(Cam c, int P, const uint8_t* __restrict__ geom,
                                                    const int32_t* __restrict__ radii, uint32_t* __restrict__ tile_cnt,

@@ -9,6 +9,7 @@
 // Backward: zero gradient rows -> render bwd (wave-reduced atomics)
 //   -> preprocess bwd (chain rule, writes every requested output).
 #include <stdio.h>
+#include <string.h>
 #include <utility>
 #include <vector>
 #include "lsr_internal.h"
@@ -55,6 +56,7 @@ const char* kStageNames[ST_N] = {"preprocess", "scan_tiles", "bin_count", "scan_
 
 struct Prof {
     bool on = false;
+    unsigned mask = ~0u;   // stages bracketed when on (lsr_profile_stages)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[ST_N];
     size_t used[ST_N] = {};
 };
@@ -64,7 +66,7 @@ struct StageScope {
     Stage s;
     hipStream_t st;
     bool on;
-    StageScope(Stage s_, hipStream_t st_) : s(s_), st(st_), on(g_prof.on)
+    StageScope(Stage s_, hipStream_t st_) : s(s_), st(st_), on(g_prof.on && ((g_prof.mask >> s_) & 1u))
     {
         if (!on) return;
         auto& v = g_prof.ev[s];
@@ -216,6 +218,25 @@ void lsr_profile_enable(int on)
     g_prof.on = on != 0;
 }
 
+int lsr_profile_stages(const char* names)
+{
+    if (!names || !*names) { g_prof.mask = ~0u; return LSR_OK; }
+    unsigned m = 0;
+    const char* p = names;
+    while (*p) {
+        const char* e = p;
+        while (*e && *e != ',') e++;
+        int hit = -1;
+        for (int k = 0; k < ST_N; k++)
+            if (strlen(kStageNames[k]) == (size_t)(e - p) && strncmp(kStageNames[k], p, (size_t)(e - p)) == 0) hit = k;
+        if (hit < 0) return LSR_EINVAL;
+        m |= 1u << hit;
+        p = *e ? e + 1 : e;
+    }
+    g_prof.mask = m;
+    return LSR_OK;
+}
+
 void lsr_profile_reset(void)
 {
     for (int k = 0; k < ST_N; k++) g_prof.used[k] = 0;
@@ -237,6 +258,65 @@ int lsr_profile_query(const char** names, double* ms, int64_t* calls, int max_st
         if (calls) calls[n] = (int64_t)g_prof.used[k];
     }
     return n;
+}
+
+// ------------------------------------------------- host-visible scan total
+// One coherent pinned word per host thread: k_publish_total stores
+// (seq << 32 | M) into it and the host spins until the sequence matches.
+struct HostSlot {
+    uint64_t* word = nullptr;   // host view
+    uint64_t* dev = nullptr;    // device view of the same word
+    uint32_t seq = 0;
+    uint64_t last_m = 0;        // previous forward's M (binning size guess)
+    ~HostSlot() { if (word) (void)hipHostFree(word); }
+};
+
+static HostSlot& host_slot()
+{
+    thread_local HostSlot hs;
+    if (!hs.word) {
+        void* p = nullptr;
+        if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocPortable | hipHostMallocMapped) != hipSuccess)
+            return hs;
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) { (void)hipHostFree(p); return hs; }
+        hs.word = (uint64_t*)p;
+        hs.dev = (uint64_t*)d;
+        *(volatile uint64_t*)hs.word = 0;
+    }
+    return hs;
+}
+
+// Spin on the published word; every 4096 polls ask the runtime whether the
+// stream has drained (which also covers a stream the runtime has not
+// submitted yet, and reports a faulted stream instead of spinning forever).
+static int wait_published(HostSlot& hs, uint32_t seq, hipStream_t st, uint64_t* M)
+{
+    volatile uint64_t* w = hs.word;
+    for (uint64_t it = 1;; it++) {
+        uint64_t v = __atomic_load_n((uint64_t*)w, __ATOMIC_ACQUIRE);
+        if ((uint32_t)(v >> 32) == seq) {
+            *M = v & 0xffffffffull;
+            return LSR_OK;
+        }
+        if ((it & 4095) == 0) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q == hipSuccess) {
+                v = __atomic_load_n((uint64_t*)w, __ATOMIC_ACQUIRE);
+                if ((uint32_t)(v >> 32) != seq) {
+                    fprintf(stderr, "[lsr] scan total was not published (stream drained)\n");
+                    return LSR_EHIP;
+                }
+                *M = v & 0xffffffffull;
+                return LSR_OK;
+            }
+            if (q != hipErrorNotReady) {
+                fprintf(stderr, "[lsr] stream failed while waiting for the scan total: %s\n", hipGetErrorString(q));
+                return LSR_EHIP;
+            }
+        }
+        __builtin_ia32_pause();
+    }
 }
 
 int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, lsr_alloc_fn alloc, void* ctx,
@@ -276,7 +356,9 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     // 1. preprocess
     { StageScope sc(ST_PRE, st); LSR_HIP(launch_preprocess(c, *in, geom, out->radii, st)); }
     LSR_DEBUG_SYNC(s, st, "preprocess");
-    uint64_t M = 0;
+    HostSlot& hs = host_slot();
+    if (!hs.word) return LSR_EHIP;
+    const uint32_t seq = ++hs.seq;
     if (priv) {
         // 2. per-block tile histograms -> column scan -> tile starts; M = total
         {
@@ -286,28 +368,44 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
         {
             StageScope sc(ST_SCAN_T, st);
             LSR_HIP(launch_scan_u32(tile_cnt, tile_start, tpart, (size_t)T, true, st));
-            LSR_HIP(hipMemcpyAsync(tile_start + T, tpart + tnb, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+            LSR_HIP(launch_publish_total(tpart + tnb, tile_start + T, hs.dev, seq, st));
         }
-        LSR_HIP(hipMemcpyAsync(&M, tpart + tnb, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     } else {
         uint64_t* gpart = (uint64_t*)(geom + GL.scan_part);
         const size_t gnb = scan_partials((size_t)P) - 1;
         StageScope sc(ST_SCAN, st);
         LSR_HIP(launch_scan_u32((const uint32_t*)(geom + GL.tiles), (uint32_t*)(geom + GL.offsets), gpart,
                                 (size_t)P, false, st));
-        LSR_HIP(hipMemcpyAsync(&M, gpart + gnb, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        LSR_HIP(launch_publish_total(gpart + gnb, nullptr, hs.dev, seq, st));
     }
-    LSR_HIP(hipStreamSynchronize(st));
+    // speculative binning workspace sized from the previous call's M, taken
+    // while the GPU is still counting, so the host usually has nothing but
+    // launches to do once M is known
+    uint8_t* bin = nullptr;
+    size_t bin_cap = 0;
+    if (hs.last_m > 0) {
+        const size_t guess = (size_t)(hs.last_m + hs.last_m / 4 + 4096);
+        bin_cap = bin_layout(guess).total;
+        bin = (uint8_t*)alloc(ctx, bin_cap, LSR_BUF_BINNING);
+        if (!bin) return LSR_ENOMEM;
+    }
+    uint64_t M = 0;
+    rc = wait_published(hs, seq, st, &M);
+    if (rc != LSR_OK) return rc;
     LSR_DEBUG_SYNC(s, st, "count");
     if (M >= 0xffffffffull) return LSR_EOVERFLOW;
     out->num_rendered = (int64_t)M;
+    hs.last_m = M;
 
     // 3. binning workspace + scatter into tile buckets
     const BinLayout BL = bin_layout((size_t)M);
-    uint8_t* bin = (uint8_t*)alloc(ctx, BL.total > 0 ? BL.total : 256, LSR_BUF_BINNING);
-    if (!bin) return LSR_ENOMEM;
+    if (!bin || BL.total > bin_cap) {
+        bin_cap = BL.total > 0 ? BL.total : 256;
+        bin = (uint8_t*)alloc(ctx, bin_cap, LSR_BUF_BINNING);
+        if (!bin) return LSR_ENOMEM;
+    }
     out->binning = bin;
-    out->binning_bytes = BL.total;
+    out->binning_bytes = bin_cap;
     if (priv) {
         StageScope sc(ST_SCATTER, st);
         LSR_HIP(launch_bin_scatter(c, P, chunk, B, geom, out->radii, table, tile_start, (uint64_t*)(bin + BL.keys),

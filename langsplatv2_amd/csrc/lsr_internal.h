@@ -29,6 +29,8 @@ hipError_t launch_mark_visible(int P, const float* means, const float* view, uin
 // to part[0] (part must hold scan_partials(n) uint64 entries).
 size_t scan_partials(size_t n);
 hipError_t launch_scan_u32(const uint32_t* in, uint32_t* out, uint64_t* part, size_t n, bool exclusive, hipStream_t st);
+hipError_t launch_publish_total(const uint64_t* total, uint32_t* tile_end, uint64_t* host_slot, uint32_t seq,
+                                hipStream_t st);
 hipError_t launch_duplicate(const Cam& c, int P, const uint8_t* geom, const int32_t* radii, uint32_t* tile_cnt,
                             uint32_t* rank, hipStream_t st);
 hipError_t launch_scatter(const Cam& c, int P, const uint8_t* geom, const int32_t* radii, const uint32_t* tile_start,
