@@ -161,6 +161,26 @@ int lsr_mark_visible(int P, const float* means3D, const float* viewmatrix,
 int lsr_quick_decode(const float* weight_map, const float* codebooks, int L, int K, int Df, int H, int W,
                      int normalize, float eps, float* out, lsr_alloc_fn alloc, void* alloc_ctx, void* stream);
 
+/* Fused top-k soft codes (replaces softmax_to_topk_soft_code,
+ * utils/vq_utils.py:9-24; get_weights_and_indices, :26-40; the per-level
+ * loop of GaussianModel.get_render_weights, scene/gaussian_model.py:510-518;
+ * and the level-offset concatenation of eval_lerf.py:340-348).
+ * logits (N, L*K) fp32: L levels of K-way codes; K in {64,128,192,256},
+ * 1 <= k <= K.  Outputs (any may be NULL, at least one not):
+ *   dense      (N, L*K) fp32: y*mask / (sum(y*mask) + 1e-10) per level;
+ *   sparse_w   (N, L*k) fp32: the k non-zeros of each level in ascending
+ *              channel order;
+ *   sparse_idx (N, L*k) of LSR_INDEX_* idx_dtype: their channel indices,
+ *              + l*K for level l when level_offset != 0.
+ * Top-k ties go to the lower channel (torch.topk's tie order is
+ * implementation-defined). */
+int lsr_topk_code_forward(const float* logits, int64_t N, int L, int K, int k, float* dense, float* sparse_w,
+                          void* sparse_idx, int idx_dtype, int level_offset, void* stream);
+/* dL/dlogits (N, L*K) from dL/ddense (N, L*K): the autograd chain of
+ * softmax_to_topk_soft_code (mask recomputed from the logits). */
+int lsr_topk_code_backward(const float* logits, const float* grad_dense, int64_t N, int L, int K, int k,
+                           float* grad_logits, void* stream);
+
 const char* lsr_strerror(int code);
 int lsr_abi_version(void);
 

@@ -103,7 +103,8 @@ class BwdOut(ctypes.Structure):
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
 
-EXPORTS = ("lsr_forward", "lsr_backward", "lsr_mark_visible", "lsr_quick_decode", "lsr_strerror",
+EXPORTS = ("lsr_forward", "lsr_backward", "lsr_mark_visible", "lsr_quick_decode", "lsr_topk_code_forward",
+           "lsr_topk_code_backward", "lsr_strerror",
            "lsr_abi_version", "lsr_max_lang_dim", "lsr_profile_enable", "lsr_profile_stages", "lsr_profile_reset",
            "lsr_profile_query")
 
@@ -133,6 +134,12 @@ def load(path: str | None = None):
     lib.lsr_quick_decode.argtypes = [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_float, _vp, ALLOC_FN, _vp, _vp]
     lib.lsr_quick_decode.restype = ctypes.c_int
+    lib.lsr_topk_code_forward.argtypes = [_vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp,
+                                          _vp, ctypes.c_int, ctypes.c_int, _vp]
+    lib.lsr_topk_code_forward.restype = ctypes.c_int
+    lib.lsr_topk_code_backward.argtypes = [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp,
+                                           _vp]
+    lib.lsr_topk_code_backward.restype = ctypes.c_int
     lib.lsr_strerror.argtypes = [ctypes.c_int]
     lib.lsr_strerror.restype = ctypes.c_char_p
     lib.lsr_abi_version.restype = ctypes.c_int

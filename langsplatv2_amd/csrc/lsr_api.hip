@@ -209,6 +209,36 @@ int lsr_quick_decode(const float* weight_map, const float* codebooks, int L, int
     return LSR_OK;
 }
 
+static bool topk_code_args_ok(int64_t N, int L, int K, int k)
+{
+    return N >= 0 && L >= 1 && K >= 64 && K <= 256 && (K % 64) == 0 && k >= 1 && k <= K &&
+           N <= (int64_t)0x7fffffff / ((int64_t)L * K);
+}
+
+int lsr_topk_code_forward(const float* logits, int64_t N, int L, int K, int k, float* dense, float* sparse_w,
+                          void* sparse_idx, int idx_dtype, int level_offset, void* stream)
+{
+    if (!topk_code_args_ok(N, L, K, k)) return (K % 64 || K > 256) && K > 0 ? LSR_EUNSUPPORTED : LSR_EINVAL;
+    if (idx_dtype < LSR_INDEX_F32 || idx_dtype > LSR_INDEX_I64) return LSR_EINVAL;
+    if (N == 0) return LSR_OK;
+    if (!logits || (!dense && !sparse_w && !sparse_idx)) return LSR_EINVAL;
+    if (lsr::launch_topk_code_fwd(logits, N, L, K, k, dense, sparse_w, sparse_idx, idx_dtype, level_offset,
+                                  (hipStream_t)stream) != hipSuccess)
+        return LSR_EHIP;
+    return LSR_OK;
+}
+
+int lsr_topk_code_backward(const float* logits, const float* grad_dense, int64_t N, int L, int K, int k,
+                           float* grad_logits, void* stream)
+{
+    if (!topk_code_args_ok(N, L, K, k)) return (K % 64 || K > 256) && K > 0 ? LSR_EUNSUPPORTED : LSR_EINVAL;
+    if (N == 0) return LSR_OK;
+    if (!logits || !grad_dense || !grad_logits) return LSR_EINVAL;
+    if (lsr::launch_topk_code_bwd(logits, grad_dense, N, L, K, k, grad_logits, (hipStream_t)stream) != hipSuccess)
+        return LSR_EHIP;
+    return LSR_OK;
+}
+
 int lsr_abi_version(void) { return LSR_ABI_VERSION; }
 
 int lsr_max_lang_dim(void) { return 64; }

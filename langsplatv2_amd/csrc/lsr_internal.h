@@ -76,6 +76,10 @@ hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t st);
 int lang_set_for(int D);     // compiled channel set >= D, or -1
 
 // quick.hip
+hipError_t launch_topk_code_fwd(const float* logits, int64_t N, int L, int K, int k, float* dense, float* sw,
+                                void* sidx, int idx_dtype, int level_offset, hipStream_t st);
+hipError_t launch_topk_code_bwd(const float* logits, const float* g, int64_t N, int L, int K, int k, float* dlogits,
+                                hipStream_t st);
 hipError_t launch_quick_decode(const float* wmap, const float* cb, int L, int K, int Df, int H, int W, int normalize,
                                float eps, float* G, float* out, hipStream_t st);
 

@@ -1,36 +1,95 @@
-"""Language-coefficient producers on the rasterizer's input edge.
+"""Top-k soft codes on the rasterizer's language input edge, fused on the GPU.
 
-Restatements (torch, device-agnostic) of utils/vq_utils.py:
-  softmax_to_topk_soft_code  :9-24  -> dense (N, K) with k non-zeros per row
-  get_weights_and_indices    :26-40 -> packed (N, k) weights, (N, k) fp32 indices
-                                       in ascending channel order (mask order)
-and of GaussianModel.get_render_weights (scene/gaussian_model.py:510-518).
-Golden vectors from the reference's own functions pin them
-(tests/golden/ref_utils.npz, tests/test_ref_golden.py).
+One HIP kernel (csrc/lang_codes.hip, C ABI lsr_topk_code_forward/backward)
+replaces the reference's chains of PyTorch ops:
+  softmax_to_topk_soft_code  utils/vq_utils.py:9-24   -> dense (N, K), k non-zeros per row
+  get_weights_and_indices    utils/vq_utils.py:26-40  -> packed (N, k) weights + fp32
+                                                         indices in ascending channel order
+  get_render_weights         scene/gaussian_model.py:510-518 (per-level concatenation)
+  quick_inputs               eval_lerf.py:340-348, backend_renderer.py:121-128
+                             (levels' packed codes, indices offset by 64*level)
+The dense codes are differentiable w.r.t. the logits (the backward is the
+same autograd chain torch applies, computed by a second fused kernel).
+There is no CPU path; ties in the top-k go to the lower channel.
 """
 from __future__ import annotations
 
 import torch
 
+from . import _lib
+from .rasterizer import _stream
+
+
+def _check_logits(logits: torch.Tensor, levels: int, what: str) -> tuple[torch.Tensor, int, int]:
+    if logits.dim() != 2:
+        raise ValueError(f"{what}: logits must be (N, levels*K), got {tuple(logits.shape)}")
+    if not logits.is_cuda:
+        raise RuntimeError(f"{what}: logits must be a ROCm device tensor (there is no CPU path)")
+    N, LK = logits.shape
+    if levels < 1 or LK % levels:
+        raise ValueError(f"{what}: {LK} channels do not split into {levels} levels")
+    return logits.contiguous().float(), N, LK // levels
+
+
+class _TopkSoftCode(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, k, levels):
+        x, N, K = _check_logits(logits, levels, "softmax_to_topk_soft_code")
+        out = torch.empty_like(x)
+        lib = _lib.load()
+        _lib.check(lib.lsr_topk_code_forward(x.data_ptr(), N, levels, K, int(k), out.data_ptr(), None, None,
+                                             _lib.LSR_INDEX_F32, 0, _stream(x.device)), "lsr_topk_code_forward")
+        ctx.save_for_backward(x)
+        ctx.k, ctx.levels = int(k), levels
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        (x,) = ctx.saved_tensors
+        N, LK = x.shape
+        g = grad.contiguous().float()
+        dx = torch.empty_like(x)
+        lib = _lib.load()
+        _lib.check(lib.lsr_topk_code_backward(x.data_ptr(), g.data_ptr(), N, ctx.levels, LK // ctx.levels, ctx.k,
+                                              dx.data_ptr(), _stream(x.device)), "lsr_topk_code_backward")
+        return dx, None, None
+
 
 def softmax_to_topk_soft_code(logits: torch.Tensor, k: int) -> torch.Tensor:
-    y = logits.softmax(dim=1)
-    _, idx = torch.topk(y, k, dim=1)
-    mask = torch.zeros_like(y, dtype=torch.bool).scatter_(1, idx, True)
-    y = torch.where(mask, y, torch.zeros_like(y))
-    return y / (y.sum(dim=1, keepdim=True) + 1e-10)
-
-
-def get_weights_and_indices(logits: torch.Tensor, k: int):
-    code = softmax_to_topk_soft_code(logits, k)
-    nz = code != 0
-    w = code[nz].view(code.shape[0], k)
-    i = torch.arange(code.shape[1], device=code.device).expand_as(code)[nz].view(code.shape[0], k)
-    return w.float(), i.float()
+    """utils/vq_utils.py:9-24 -> (N, K) fp32, differentiable w.r.t. logits."""
+    return _TopkSoftCode.apply(logits, k, 1)
 
 
 def get_render_weights(logits: torch.Tensor, layer_num: int, codebook_size: int, k: int) -> torch.Tensor:
-    """Per-level top-k soft codes concatenated -> (N, layer_num*codebook_size)."""
-    parts = [softmax_to_topk_soft_code(logits[:, i * codebook_size:(i + 1) * codebook_size], k)
-             for i in range(layer_num)]
-    return torch.cat(parts, dim=-1).float()
+    """scene/gaussian_model.py:510-518: per-level top-k soft codes of
+    logits (N, layer_num*codebook_size), concatenated -> (N, layer_num*codebook_size)."""
+    if logits.shape[-1] != layer_num * codebook_size:
+        raise ValueError(f"get_render_weights: logits have {logits.shape[-1]} channels, "
+                         f"expected {layer_num}*{codebook_size}")
+    return _TopkSoftCode.apply(logits, k, layer_num)
+
+
+def quick_inputs(logits: torch.Tensor, k: int, levels: int = 1, level_offset: bool = True,
+                 index_dtype: torch.dtype = torch.float32):
+    """Packed sparse codes of every level: (weights (N, levels*k) fp32, indices
+    (N, levels*k) of index_dtype), indices + K*level when level_offset —
+    the language_feature_weights_quick / language_feature_indices pair of
+    eval_lerf.py:340-348.  Not differentiable (every quick caller is no_grad)."""
+    x, N, K = _check_logits(logits, levels, "quick_inputs")
+    codes = {torch.float32: _lib.LSR_INDEX_F32, torch.int32: _lib.LSR_INDEX_I32, torch.int64: _lib.LSR_INDEX_I64}
+    if index_dtype not in codes:
+        raise ValueError(f"quick_inputs: index dtype {index_dtype} unsupported (float32/int32/int64)")
+    w = torch.empty((N, levels * k), dtype=torch.float32, device=x.device)
+    idx = torch.empty((N, levels * k), dtype=index_dtype, device=x.device)
+    lib = _lib.load()
+    _lib.check(lib.lsr_topk_code_forward(x.data_ptr(), N, levels, K, int(k), None, w.data_ptr(), idx.data_ptr(),
+                                         codes[index_dtype], int(bool(level_offset)), _stream(x.device)),
+               "lsr_topk_code_forward")
+    return w, idx
+
+
+def get_weights_and_indices(logits: torch.Tensor, k: int):
+    """utils/vq_utils.py:26-40: (weights (N, k) fp32, indices (N, k) fp32) in
+    ascending channel order."""
+    with torch.no_grad():
+        return quick_inputs(logits, k, 1, level_offset=False)

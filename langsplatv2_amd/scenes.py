@@ -7,7 +7,8 @@ Camera conventions restate the reference:
   getProjectionMatrix   utils/graphics_utils.py:51-71
   world_view_transform / full_proj_transform / camera_center
                         scene/cameras.py:55-58 (znear 0.01, zfar 100 :49-50)
-Language inputs restate utils/vq_utils.py:9-40 (see lang_codes.py).
+Language inputs restate utils/vq_utils.py:9-40 on the CPU (input synthesis
+only; the product producer is the fused HIP kernel behind lang_codes.py).
 """
 from __future__ import annotations
 
@@ -16,7 +17,24 @@ import math
 import numpy as np
 import torch
 
-from .lang_codes import get_weights_and_indices, softmax_to_topk_soft_code
+
+
+def softmax_to_topk_soft_code(logits: torch.Tensor, k: int) -> torch.Tensor:
+    """CPU torch restatement of utils/vq_utils.py:9-24 (input synthesis)."""
+    y = logits.softmax(dim=1)
+    _, idx = torch.topk(y, k, dim=1)
+    mask = torch.zeros_like(y, dtype=torch.bool).scatter_(1, idx, True)
+    y = torch.where(mask, y, torch.zeros_like(y))
+    return y / (y.sum(dim=1, keepdim=True) + 1e-10)
+
+
+def get_weights_and_indices(logits: torch.Tensor, k: int):
+    """CPU torch restatement of utils/vq_utils.py:26-40 (input synthesis)."""
+    code = softmax_to_topk_soft_code(logits, k)
+    nz = code != 0
+    w = code[nz].view(code.shape[0], k)
+    i = torch.arange(code.shape[1], device=code.device).expand_as(code)[nz].view(code.shape[0], k)
+    return w.float(), i.float()
 
 
 def get_world2view2(R: np.ndarray, t: np.ndarray, translate=np.zeros(3), scale=1.0) -> np.ndarray:

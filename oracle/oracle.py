@@ -232,3 +232,79 @@ def cov3D(s: np.ndarray, q: np.ndarray, mod: float = 1.0) -> np.ndarray:
     out = np.zeros((s.shape[0], 6), np.float32)
     load().lso_cov3D(s.shape[0], _p(s), ctypes.c_float(mod), _p(q), _p(out))
     return out
+
+
+# --------------------------------------------------------------- language codes
+# numpy float64 restatement of the top-k soft codes (utils/vq_utils.py:9-40)
+# and of their autograd chain; checks the fused HIP producer
+# (csrc/lang_codes.hip).  Pinned by tests/golden/ref_utils.npz (the
+# reference's own functions, forward and torch-autograd gradients).
+
+def _topk_mask(y: np.ndarray, k: int) -> np.ndarray:
+    """utils/vq_utils.py:16-18: top-k of each row; ties -> lower channel
+    (stable sort of -y)."""
+    order = np.argsort(-y, axis=1, kind="stable")[:, :k]
+    mask = np.zeros(y.shape, dtype=bool)
+    np.put_along_axis(mask, order, True, axis=1)
+    return mask
+
+
+def _softmax(x: np.ndarray) -> np.ndarray:
+    """utils/vq_utils.py:14 (row softmax, max-shifted)."""
+    e = np.exp(x - x.max(axis=1, keepdims=True))
+    return e / e.sum(axis=1, keepdims=True)
+
+
+def topk_soft_code(logits: np.ndarray, k: int, levels: int = 1) -> np.ndarray:
+    """softmax_to_topk_soft_code (utils/vq_utils.py:9-24); with levels > 1 the
+    per-level concatenation of GaussianModel.get_render_weights
+    (scene/gaussian_model.py:510-518).  float64."""
+    x = np.asarray(logits, np.float64)
+    N, LK = x.shape
+    K = LK // levels
+    out = np.zeros_like(x)
+    for l in range(levels):
+        y = _softmax(x[:, l * K:(l + 1) * K])
+        z = np.where(_topk_mask(y, k), y, 0.0)
+        out[:, l * K:(l + 1) * K] = z / (z.sum(axis=1, keepdims=True) + 1e-10)
+    return out
+
+
+def weights_and_indices(logits: np.ndarray, k: int, levels: int = 1, level_offset: bool = True):
+    """get_weights_and_indices (utils/vq_utils.py:26-40) per level, indices
+    offset by l*K and concatenated as the quick-path callers do
+    (eval_lerf.py:340-348).  Returns (w (N, L*k) float64, idx (N, L*k) int64)."""
+    x = np.asarray(logits, np.float64)
+    N, LK = x.shape
+    K = LK // levels
+    ws, ids = [], []
+    for l in range(levels):
+        y = _softmax(x[:, l * K:(l + 1) * K])
+        m = _topk_mask(y, k)
+        z = np.where(m, y, 0.0)
+        z = z / (z.sum(axis=1, keepdims=True) + 1e-10)
+        idx = np.nonzero(m)[1].reshape(N, k)          # ascending channel order per row
+        ws.append(np.take_along_axis(z, idx, axis=1))
+        ids.append(idx + (l * K if level_offset else 0))
+    return np.concatenate(ws, axis=1), np.concatenate(ids, axis=1)
+
+
+def topk_soft_code_backward(logits: np.ndarray, grad: np.ndarray, k: int, levels: int = 1) -> np.ndarray:
+    """dL/dlogits of topk_soft_code for upstream dL/dcode: the chain torch's
+    autograd applies to utils/vq_utils.py:14-21 (division by sum + 1e-10, the
+    where-mask, softmax).  float64."""
+    x = np.asarray(logits, np.float64)
+    g = np.asarray(grad, np.float64)
+    N, LK = x.shape
+    K = LK // levels
+    out = np.zeros_like(x)
+    for l in range(levels):
+        sl = slice(l * K, (l + 1) * K)
+        y = _softmax(x[:, sl])
+        m = _topk_mask(y, k)
+        z = np.where(m, y, 0.0)
+        d = z.sum(axis=1, keepdims=True) + 1e-10
+        gz = g[:, sl] / d - (g[:, sl] * z).sum(axis=1, keepdims=True) / (d * d)
+        dy = np.where(m, gz, 0.0)
+        out[:, sl] = y * (dy - (dy * y).sum(axis=1, keepdims=True))
+    return out

@@ -87,6 +87,28 @@ def main():
     w, idx = vq_utils.get_weights_and_indices(logits, 4)
     out["lang_quick_w"] = w.numpy()
     out["lang_quick_idx"] = idx.numpy()
+    # k = 1 and 8 codes; torch-autograd gradient of the reference function
+    for kk in (1, 8):
+        out[f"lang_topk{kk}"] = vq_utils.softmax_to_topk_soft_code(logits, kk).numpy()
+    gup = torch.randn(300, 64, generator=g)
+    x = logits.clone().requires_grad_(True)
+    vq_utils.softmax_to_topk_soft_code(x, 4).backward(gup)
+    out["lang_grad_up"] = gup.numpy()
+    out["lang_topk4_dlogits"] = x.grad.numpy()
+    # 3 levels x 64: get_render_weights' per-level loop (scene/gaussian_model.py:510-518,
+    # restated here because scene/ does not import offline) and the quick-path
+    # level-offset concatenation (eval_lerf.py:340-348)
+    logits3 = torch.randn(200, 192, generator=g) * 1.5
+    out["lang3_logits"] = logits3.numpy()
+    out["lang3_render_weights"] = torch.cat(
+        [vq_utils.softmax_to_topk_soft_code(logits3[:, i * 64:(i + 1) * 64], 4) for i in range(3)], dim=-1).numpy()
+    ws, ids = [], []
+    for i in range(3):
+        w3, i3 = vq_utils.get_weights_and_indices(logits3[:, i * 64:(i + 1) * 64], 4)
+        ws.append(w3)
+        ids.append(i3 + int(i * 64))
+    out["lang3_quick_w"] = torch.cat(ws, dim=1).numpy()
+    out["lang3_quick_idx"] = torch.cat(ids, dim=1).numpy()
     np.savez_compressed(OUT, **out)
     print("wrote", OUT, {k: v.shape for k, v in out.items()})
 

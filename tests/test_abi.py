@@ -51,6 +51,12 @@ def test_host_only_entry_points(lib):
     assert lib.lsr_strerror(0).decode().lower() in ("ok", "success", "no error")
     for code in range(1, 8):
         assert isinstance(lib.lsr_strerror(code), bytes)
+    # argument validation happens before any device call
+    assert lib.lsr_topk_code_forward(None, 10, 1, 48, 4, None, None, None, 0, 0, None) == 2  # K % 64 -> unsupported
+    assert lib.lsr_topk_code_forward(None, 10, 1, 64, 0, None, None, None, 0, 0, None) == 1  # k < 1
+    assert lib.lsr_topk_code_forward(1, 10, 1, 64, 4, None, None, None, 0, 0, None) == 1     # no output
+    assert lib.lsr_topk_code_forward(None, 0, 1, 64, 4, 1, None, None, 0, 0, None) == 0      # N = 0: no-op
+    assert lib.lsr_topk_code_backward(None, None, 10, 1, 64, 65, None, None) == 1           # k > K
 
 
 def _c_layout(structs):

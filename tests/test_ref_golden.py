@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 import torch
 
-from langsplatv2_amd import lang_codes, scenes
+from langsplatv2_amd import scenes
 
 G = np.load(os.path.join(os.path.dirname(__file__), "golden", "ref_utils.npz"))
 
@@ -47,11 +47,34 @@ def test_camera_matrices_match_reference(i):
 
 
 def test_language_codes_match_reference():
+    """Input synthesis (scenes.py) and the oracle against utils/vq_utils.py:9-40."""
     logits = torch.from_numpy(G["lang_logits"])
-    np.testing.assert_allclose(lang_codes.softmax_to_topk_soft_code(logits, 4).numpy(), G["lang_topk4"],
+    np.testing.assert_allclose(scenes.softmax_to_topk_soft_code(logits, 4).numpy(), G["lang_topk4"],
                                rtol=1e-6, atol=1e-7)
-    w, idx = lang_codes.get_weights_and_indices(logits, 4)
+    w, idx = scenes.get_weights_and_indices(logits, 4)
     np.testing.assert_allclose(w.numpy(), G["lang_quick_w"], rtol=1e-6, atol=1e-7)
     np.testing.assert_array_equal(idx.numpy(), G["lang_quick_idx"])
     # indices are fp32-encoded integers in ascending channel order (utils/vq_utils.py:38)
     assert np.all(np.diff(G["lang_quick_idx"], axis=1) > 0)
+
+
+@pytest.mark.parametrize("k", [1, 4, 8])
+def test_oracle_topk_codes_match_reference(k):
+    from oracle import oracle as O
+    np.testing.assert_allclose(O.topk_soft_code(G["lang_logits"], k), G[f"lang_topk{k}"], rtol=1e-6, atol=1e-7)
+
+
+def test_oracle_topk_code_grad_matches_reference_autograd():
+    from oracle import oracle as O
+    d = O.topk_soft_code_backward(G["lang_logits"], G["lang_grad_up"], 4)
+    ref = G["lang_topk4_dlogits"]
+    np.testing.assert_allclose(d, ref, rtol=0, atol=2e-6 * max(1.0, np.abs(ref).max()))
+
+
+def test_oracle_multilevel_codes_match_reference():
+    from oracle import oracle as O
+    x = G["lang3_logits"]
+    np.testing.assert_allclose(O.topk_soft_code(x, 4, levels=3), G["lang3_render_weights"], rtol=1e-6, atol=1e-7)
+    w, idx = O.weights_and_indices(x, 4, levels=3)
+    np.testing.assert_allclose(w, G["lang3_quick_w"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_array_equal(idx, G["lang3_quick_idx"].astype(np.int64))
