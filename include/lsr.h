@@ -99,7 +99,8 @@ typedef struct lsr_inputs {
  * while the GPU is still counting) and, only if M outgrew it, a second one;
  * the last pointer returned for a kind is the one the call uses. */
 typedef void* (*lsr_alloc_fn)(void* ctx, size_t bytes, int which);
-enum { LSR_BUF_GEOM = 0, LSR_BUF_BINNING = 1, LSR_BUF_IMAGE = 2, LSR_BUF_GRAD = 3, LSR_BUF_DECODE = 4 };
+enum { LSR_BUF_GEOM = 0, LSR_BUF_BINNING = 1, LSR_BUF_IMAGE = 2, LSR_BUF_GRAD = 3, LSR_BUF_DECODE = 4,
+       LSR_BUF_KNN = 5 };
 
 typedef struct lsr_fwd_out {
     float* out_color;     /* (3,H,W)  caller-allocated */
@@ -180,6 +181,12 @@ int lsr_topk_code_forward(const float* logits, int64_t N, int L, int K, int k, f
  * softmax_to_topk_soft_code (mask recomputed from the logits). */
 int lsr_topk_code_backward(const float* logits, const float* grad_dense, int64_t N, int L, int K, int k,
                            float* grad_logits, void* stream);
+
+/* simple_knn._C.distCUDA2 (scene/gaussian_model.py:20,194): for points
+ * (N, 3) fp32, out[i] = mean of the three smallest squared distances
+ * dx*dx + dy*dy + dz*dz to points j != i (exact; FLT_MAX for missing
+ * neighbours when N < 4).  Workspace (~40 B/point) via alloc. */
+int lsr_knn_dist2(const float* points, int64_t N, float* out, lsr_alloc_fn alloc, void* alloc_ctx, void* stream);
 
 const char* lsr_strerror(int code);
 int lsr_abi_version(void);

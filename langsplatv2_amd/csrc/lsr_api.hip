@@ -239,6 +239,19 @@ int lsr_topk_code_backward(const float* logits, const float* grad_dense, int64_t
     return LSR_OK;
 }
 
+int lsr_knn_dist2(const float* points, int64_t N, float* out, lsr_alloc_fn alloc, void* alloc_ctx, void* stream)
+{
+    if (N < 0 || N > 0x7fffffffLL) return LSR_EINVAL;
+    if (N == 0) return LSR_OK;
+    if (!points || !out || !alloc) return LSR_EINVAL;
+    size_t sort_temp = 0;
+    if (lsr::knn_sort_temp_bytes(N, &sort_temp) != hipSuccess) return LSR_EHIP;
+    uint8_t* ws = (uint8_t*)alloc(alloc_ctx, lsr::knn_workspace_bytes(N, sort_temp), LSR_BUF_KNN);
+    if (!ws) return LSR_ENOMEM;
+    if (lsr::launch_knn_dist2(points, N, out, ws, sort_temp, (hipStream_t)stream) != hipSuccess) return LSR_EHIP;
+    return LSR_OK;
+}
+
 int lsr_abi_version(void) { return LSR_ABI_VERSION; }
 
 int lsr_max_lang_dim(void) { return 64; }

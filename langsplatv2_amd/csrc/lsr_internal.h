@@ -80,6 +80,9 @@ hipError_t launch_topk_code_fwd(const float* logits, int64_t N, int L, int K, in
                                 void* sidx, int idx_dtype, int level_offset, hipStream_t st);
 hipError_t launch_topk_code_bwd(const float* logits, const float* g, int64_t N, int L, int K, int k, float* dlogits,
                                 hipStream_t st);
+size_t knn_workspace_bytes(int64_t N, size_t sort_temp);
+hipError_t knn_sort_temp_bytes(int64_t N, size_t* bytes);
+hipError_t launch_knn_dist2(const float* points, int64_t N, float* out, uint8_t* ws, size_t sort_temp, hipStream_t st);
 hipError_t launch_quick_decode(const float* wmap, const float* cb, int L, int K, int Df, int H, int W, int normalize,
                                float eps, float* G, float* out, hipStream_t st);
 

@@ -13,6 +13,7 @@
  *   outputs              gaussian_renderer/__init__.py:108-129
  */
 #include "lsr_oracle.h"
+#include <float.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -754,5 +755,26 @@ void lso_preprocess_bwd(const lso_settings* s, const lso_inputs* in, const lso_g
             pg->drot[4 * i + 2] = gy;
             pg->drot[4 * i + 3] = gz;
         }
+    }
+}
+
+void lso_knn_dist2(int N, const float* pts, float* out)
+{
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int i = 0; i < N; i++) {
+        float b[3] = {FLT_MAX, FLT_MAX, FLT_MAX};
+        const float qx = pts[3 * i], qy = pts[3 * i + 1], qz = pts[3 * i + 2];
+        for (int j = 0; j < N; j++) {
+            if (j == i) continue;
+            const float dx = pts[3 * j] - qx, dy = pts[3 * j + 1] - qy, dz = pts[3 * j + 2] - qz;
+            float d = dx * dx + dy * dy + dz * dz;
+            for (int k = 0; k < 3; k++)
+                if (b[k] > d) {
+                    const float t = b[k];
+                    b[k] = d;
+                    d = t;
+                }
+        }
+        out[i] = (b[0] + b[1] + b[2]) / 3.0f;
     }
 }

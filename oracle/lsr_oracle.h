@@ -144,6 +144,13 @@ void lso_sh_eval(int deg, int N, int M, const float* sh, const float* dirs, floa
 void lso_quat_to_R(int N, const float* q, float* R);
 void lso_cov3D(int N, const float* s, float mod, const float* q, float* cov);
 
+/* simple_knn distCUDA2 (scene/gaussian_model.py:20,194), by brute force:
+ * out[i] = (b0 + b1 + b2) / 3 of the three smallest squared distances
+ * dx*dx + dy*dy + dz*dz (left to right, no contraction) to points j != i,
+ * b ascending by insertion (strict >), FLT_MAX where fewer than 3 exist.
+ * O(N^2); OpenMP over i. */
+void lso_knn_dist2(int N, const float* pts, float* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -234,6 +234,14 @@ def cov3D(s: np.ndarray, q: np.ndarray, mod: float = 1.0) -> np.ndarray:
     return out
 
 
+def knn_dist2(pts: np.ndarray) -> np.ndarray:
+    """simple_knn distCUDA2 by brute force (lso_knn_dist2); O(N^2), N <= ~30k."""
+    p = np.ascontiguousarray(pts, np.float32).reshape(-1, 3)
+    out = np.zeros(p.shape[0], np.float32)
+    load().lso_knn_dist2(p.shape[0], _p(p), _p(out))
+    return out
+
+
 # --------------------------------------------------------------- language codes
 # numpy float64 restatement of the top-k soft codes (utils/vq_utils.py:9-40)
 # and of their autograd chain; checks the fused HIP producer
