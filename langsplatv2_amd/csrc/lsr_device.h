@@ -18,26 +18,27 @@
 namespace lsr {
 
 // ------------------------------------------------------------------ math --
-// Deterministic exp for x <= 0: Cody-Waite reduction + degree-7 Taylor
-// (|rel err| < 2 ulp).  Replaces the CUDA reference's expf so results are
-// reproducible on the CPU bit for bit.
+// Deterministic exp for x <= 0, shared bit for bit with the oracle
+// (lso_expf): n = round(x log2 e) by the 1.5*2^23 magic-number fma, Cody-Waite
+// reduction, a degree-6 near-minimax polynomial on |r| <= ln2/2 (<= 0.96 ulp
+// measured), and 2^n inserted by a shift of the magic sum's bits.  11 VALU
+// instructions after the range guard.  Replaces the CUDA reference's expf so
+// results are reproducible on the CPU.
 __device__ __forceinline__ float expf_det(float x)
 {
     if (x < -87.0f) return 0.0f;
-    float n = rintf(x * 1.44269504088896341f);
+    const float t = fmaf(x, 1.44269504088896341f, 12582912.0f);
+    const float n = t - 12582912.0f;
     float r = fmaf(n, -0.693145751953125f, x);
     r = fmaf(n, -1.428606765330187e-06f, r);
-    float p = 1.98412698412698413e-04f;
-    p = fmaf(p, r, 1.38888888888888889e-03f);
-    p = fmaf(p, r, 8.33333333333333333e-03f);
-    p = fmaf(p, r, 4.16666666666666667e-02f);
-    p = fmaf(p, r, 1.66666666666666667e-01f);
-    p = fmaf(p, r, 0.5f);
+    float p = 0x1.6aea1ap-10f;
+    p = fmaf(p, r, 0x1.1267d2p-7f);
+    p = fmaf(p, r, 0x1.555820p-5f);
+    p = fmaf(p, r, 0x1.555418p-3f);
+    p = fmaf(p, r, 0x1.fffffcp-2f);
     p = fmaf(p, r, 1.0f);
     p = fmaf(p, r, 1.0f);
-    int ni = (int)n;
-    float sc = __int_as_float((ni + 127) << 23);
-    return p * sc;
+    return p * __uint_as_float((__float_as_uint(t) << 23) + 0x3f800000u);
 }
 
 // float -> int truncating + saturating; NaN -> 0 (matches oracle f2i).

@@ -36,6 +36,9 @@
 #ifndef LSR_BWD_MF
 #define LSR_BWD_MF 1
 #endif
+#ifndef LSR_FWD_PK
+#define LSR_FWD_PK 1        // fwd: pair-interleaved candidate geometry, packed (v_pk_*) exponent of 2 candidates
+#endif
 #ifndef LSR_MF_WAVES
 #define LSR_MF_WAVES 2      // MFMA render kernels: min waves per SIMD (caps VGPRs at 256)
 #endif
@@ -66,6 +69,22 @@ template <int CTRL>
 __device__ __forceinline__ float dpp(float v)
 {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Value of lane l ^ M (M = 16 or 32) via the gfx950 permlane swaps.
+template <int M>
+__device__ __forceinline__ float xor_f32(float v)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t x = __float_as_uint(v);
+    if constexpr (M == 32) {
+        auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return __uint_as_float((lane & 32) ? r[0] : r[1]);
+    } else {
+        static_assert(M == 16, "xor_f32: M must be 16 or 32");
+        auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return __uint_as_float((lane & 16) ? r[0] : r[1]);
+    }
 }
 
 // Reduce 32 per-lane values across the wave.  On return, lane l holds the
@@ -273,12 +292,62 @@ __device__ __forceinline__ int stage_candidates(WaveStage<F4>& st, bool valid, u
     return cnt;
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Forward staging with the candidates' geometry pair-interleaved: entry
+// j >> 1, component j & 1, so the blend loop reads candidates (2i, 2i+1) of
+// each field with one ds_read_b64 and evaluates both exponents with packed
+// f32 instructions (bitwise identical to the scalar ones).
+template <int F4>
+struct WaveStageP {
+    f32x2 X[32], Y[32], CA[32], CB[32], CC[32], OP[32], CUT[32];
+    float4 F[64 * F4];
+    int pos[64];
+};
+
+template <int NL, int F4>
+__device__ __forceinline__ int stage_candidates_p(WaveStageP<F4>& st, bool valid, uint32_t gid, int pos, int bx,
+                                                  int by, const float4* __restrict__ splatA,
+                                                  const float4* __restrict__ splatB, const float* __restrict__ rgb,
+                                                  const float* __restrict__ lang, int D)
+{
+    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+    if (valid) {
+        A = splatA[gid];
+        B = splatB[gid];
+    }
+    const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by) &&
+                    block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, bx, by);
+    const uint64_t m = __ballot(ok);
+    const int cnt = __popcll(m);
+    if (ok) {
+        const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        float* base = reinterpret_cast<float*>(&st) + (r & 1);
+        const int e = (r >> 1) * 2;
+        base[0 * 64 + e] = A.x;
+        base[1 * 64 + e] = A.y;
+        base[2 * 64 + e] = A.z;
+        base[3 * 64 + e] = A.w;
+        base[4 * 64 + e] = B.x;
+        base[5 * 64 + e] = B.y;
+        base[6 * 64 + e] = B.z;
+        st.pos[r] = pos;
+        stage_features<NL, F4>(&st.F[r * F4], rgb, lang, D, gid);
+    }
+    wave_lds_fence();
+    return cnt;
+}
+
 template <int NL>
 __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
 {
     constexpr int C = 3 + NL;
     constexpr int F4 = (C + 3) / 4;  // float4 per feature row
+#if LSR_FWD_PK
+    __shared__ WaveStageP<F4> st;
+#else
     __shared__ WaveStage<F4> st;
+#endif
 
     const Cam& c = a.cam;
     const WaveTile wt;
@@ -303,8 +372,13 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
         const bool valid = idx < re;
         const uint32_t gid = next_gid;
         next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;   // prefetch the next chunk's ids
+#if LSR_FWD_PK
+        const int n = stage_candidates_p<NL, F4>(st, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, a.splatA,
+                                                 a.splatB, a.rgb, a.lang, D);
+#else
         const int n = stage_candidates<NL, F4>(st, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, a.splatA, a.splatB,
                                                a.rgb, a.lang, D);
+#endif
         // Two instances per iteration, branch-free per lane: a lane that
         // skips an instance (exponent cut, alpha < 1/255, saturated or done)
         // blends it with weight 0 and keeps T.  The two exp chains are
@@ -314,6 +388,22 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
             if (__ballot(!done) == 0) break;
             const bool two = j0 + 1 < n;
             const int j1 = two ? j0 + 1 : j0;
+#if LSR_FWD_PK
+            // both candidates' exponents at once (splat_power, lane-wise);
+            // a missing second candidate reads a stale slot: ok1 masks it
+            const int e = j0 >> 1;
+            const f32x2 dx = st.X[e] - f32x2{pfx, pfx}, dy = st.Y[e] - f32x2{pfy, pfy};
+            const f32x2 P = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f},
+                                                      __builtin_elementwise_fma(st.CA[e] * dx, dx, (st.CC[e] * dy) * dy),
+                                                      -((st.CB[e] * dx) * dy));
+            const f32x2 CUT = st.CUT[e], OP = st.OP[e];
+            const float p0 = P.x, p1 = P.y;
+            bool ok0 = !done && !(p0 > 0.0f || p0 < CUT.x);
+            bool ok1 = two && !done && !(p1 > 0.0f || p1 < CUT.y);
+            if (!__any(ok0 || ok1)) continue;
+            const float al0 = fminf(0.99f, OP.x * expf_det(p0));
+            const float al1 = fminf(0.99f, OP.y * expf_det(p1));
+#else
             const float4 A0 = st.A[j0], B0 = st.B[j0];
             const float4 A1 = st.A[j1], B1 = st.B[j1];
             const float p0 = splat_power(A0.z, A0.w, B0.x, A0.x - pfx, A0.y - pfy);
@@ -323,6 +413,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
             if (!__any(ok0 || ok1)) continue;
             const float al0 = fminf(0.99f, B0.y * expf_det(p0));
             const float al1 = fminf(0.99f, B1.y * expf_det(p1));
+#endif
             ok0 = ok0 && !(al0 < 1.0f / 255.0f);
             ok1 = ok1 && !(al1 < 1.0f / 255.0f);
             {
@@ -871,7 +962,15 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
 #ifndef LSR_P1_UNROLL
 #define LSR_P1_UNROLL 4
 #endif
-#define LSR_GRP_STRIDE 70   // dot/u and aT tiles: conflict-free fragment stores and A-fragment reads
+#ifndef LSR_BWD_VMOM
+#define LSR_BWD_VMOM 1      // bwd: geometry moments and RGB sums on the VALU, MFMA only for dot + language
+#endif
+#ifndef LSR_BWD_ALIAS
+#define LSR_BWD_ALIAS 1
+#endif
+#ifndef LSR_GRP_STRIDE
+#define LSR_GRP_STRIDE 66   // dot/u and aT tiles: conflict-free A-fragment reads (li*66 mod 32 = 2 li)
+#endif
 #define LSR_LOG2E 1.4426950408889634f
 #ifdef LSR_MF_NO_ATOMIC   // timing experiment only: keeps the work, drops the atomics
 #define LSR_MF_ATOMIC(ptr, v) do { if ((v) == 1234.5678f) atomicAdd((ptr), (v)); } while (0)
@@ -921,20 +1020,46 @@ __device__ __forceinline__ float feature_at(const RenderArgs& a, uint32_t gid, i
     return 0.f;
 }
 
+#ifdef LSR_EXP_NOMF   // timing experiment only (wrong results): no matrix-core work
+#define BWD_MFMA(a, b_, c) (c)
+#else
+#define BWD_MFMA(a, b_, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b_), (c), 0, 0, 0)
+#endif
 template <int NL>
 __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArgs b)
 {
     using FR = BwdFrags<NL>;
     constexpr int KS = FR::KS;
+#if LSR_BWD_VMOM
+    // MFMA channel blocks cover the language channels only; RGB (3) and the
+    // six geometry moments are summed on the VALU (see phase 3)
+    constexpr int NBC = (NL + 15) / 16;
+    constexpr int NBA = NBC > 0 ? NBC : 1;
+    __shared__ float4 sDrgb[64];      // dL/dout RGB of the block's pixels
+#else
     constexpr int NBC = FR::NBC;
+    constexpr int NBA = NBC;
+#endif
     constexpr int GS = LSR_GRP_STRIDE;
     __shared__ WaveStageG st;
+    constexpr int GRL = (LSR_GROW_LANG + NL + 15) / 16;   // 16-float lines per gradient row
+    constexpr int GRS = 16 * GRL + 4;                     // staged row stride
+#if LSR_BWD_ALIAS
+    // The gradient-row tile and the moments are written only after phase 3
+    // has read dot/u and aT into registers (a wave's LDS operations complete
+    // in order), so they share those buffers: 2.3-5.4 KB less LDS per wave,
+    // 12 instead of 10 resident waves per CU at D = 16.
+    constexpr int DUG = (16 * GS > 16 * GRS) ? 16 * GS : 16 * GRS;
+    __shared__ float sDU[DUG];        // dot[k][p] -> u[k][p] -> the group's gradient rows
+    __shared__ float sAT[16 * GS];    // G[k][p] (phase 1) -> aT[k][p] (phase 2) -> moments
+    float* const sGr = sDU;
+    float* const sMom = sAT;
+#else
     __shared__ float sDU[16 * GS];    // dot[k][p], overwritten in place by u[k][p]
     __shared__ float sAT[16 * GS];    // G[k][p] (phase 1), then aT[k][p] (phase 2)
     __shared__ float sMom[16 * LSR_MOM_STRIDE];
-    constexpr int GRL = (LSR_GROW_LANG + NL + 15) / 16;   // 16-float lines per gradient row
-    constexpr int GRS = 16 * GRL + 4;                     // staged row stride
     __shared__ float sGr[16 * GRS];   // the group's gradient rows
+#endif
 
     const RenderArgs& a = b.f;
     const Cam& c = a.cam;
@@ -964,15 +1089,28 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
         st.gid[e] = 0u;
     }
 
-    float dotB[KS][4], chB[NBC][16];
+    float dotB[KS][4], chB[NBA][16];
 #pragma unroll
     for (int t = 0; t < KS; t++)
 #pragma unroll
         for (int pb = 0; pb < 4; pb++) dotB[t][pb] = gd_at<NL>(b, 4 * t + lg, pb * 16 + li, pm.bx, pm.by);
+#if LSR_BWD_VMOM
+#pragma unroll
+    for (int nb = 0; nb < NBC; nb++)
+#pragma unroll
+        for (int t = 0; t < 16; t++) chB[nb][t] = gd_at<NL>(b, 3 + nb * 16 + li, 4 * t + lg, pm.bx, pm.by);
+    sDrgb[lane] = make_float4(gd_at<NL>(b, 0, lane, pm.bx, pm.by), gd_at<NL>(b, 1, lane, pm.bx, pm.by),
+                              gd_at<NL>(b, 2, lane, pm.bx, pm.by), 0.f);
+    // block-centred x of the pixels this lane's fragments cover: columns lg
+    // (even K-steps) and 4 + lg (odd K-steps)
+    const float lxe = (float)lg - 3.5f, lxo = (float)lg + 0.5f;
+    const float lxe2 = lxe * lxe, lxo2 = lxo * lxo;
+#else
 #pragma unroll
     for (int nb = 0; nb < NBC; nb++)
 #pragma unroll
         for (int t = 0; t < 16; t++) chB[nb][t] = gd_at<NL>(b, nb * 16 + li, 4 * t + lg, pm.bx, pm.by);
+#endif
     const float bg0 = c.bg[0], bg1 = c.bg[1], bg2 = c.bg[2];
     const float bg_dot = inside ? bg0 * b.dout_color[pix] + bg1 * b.dout_color[HW + pix] + bg2 * b.dout_color[2 * HW + pix]
                                 : 0.f;   // 0 with a black background: the term below is then exact 0
@@ -1043,7 +1181,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 for (int t = 0; t < KS; t++)
 #pragma unroll
                     for (int pb = 0; pb < 4; pb++)
-                        acc[pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[t], dotB[t][pb], acc[pb], 0, 0, 0);
+                        acc[pb] = BWD_MFMA(af[t], dotB[t][pb], acc[pb]);
 #pragma unroll
                 for (int pb = 0; pb < 4; pb++)
 #pragma unroll
@@ -1084,6 +1222,87 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 }
             }
             wave_lds_fence();
+#if LSR_BWD_VMOM
+            // phase 3: language gradients on MFMA; RGB gradients and the six
+            // pixel moments sum_p u {1, lx, ly, lx^2, lx ly, ly^2} on the VALU.
+            // Lane (li, lg) reads candidate li's aT and u at pixel q = 4t + lg
+            // (the MFMA A fragments) and keeps partial sums over its 16 pixels;
+            // the four lane groups are then added.  Rows pair K-steps 2r
+            // (columns lg) and 2r + 1 (columns 4 + lg) at ly = r - 3.5.
+            f32x4 ch[NBA];
+#pragma unroll
+            for (int nb = 0; nb < NBA; nb++) ch[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+            float M0 = 0.f, M1 = 0.f, M2 = 0.f, M3 = 0.f, M4 = 0.f, M5 = 0.f;
+            float C0 = 0.f, C1 = 0.f, C2 = 0.f;
+            float ue = 0.f;
+#pragma unroll
+            for (int t = 0; t < 16; t++) {
+                const float au = sDU[li * GS + 4 * t + lg];
+                const float aa = sAT[li * GS + 4 * t + lg];
+#pragma unroll
+                for (int nb = 0; nb < NBC; nb++) ch[nb] = BWD_MFMA(aa, chB[nb][t], ch[nb]);
+                const float4 d = sDrgb[4 * t + lg];
+                C0 = fmaf(aa, d.x, C0);
+                C1 = fmaf(aa, d.y, C1);
+                C2 = fmaf(aa, d.z, C2);
+                if ((t & 1) == 0) {
+                    ue = au;
+                } else {
+                    const float ly = (float)(t >> 1) - 3.5f;
+                    const float R0 = ue + au;
+                    const float R1 = fmaf(ue, lxe, au * lxo);
+                    const float R2 = fmaf(ue, lxe2, au * lxo2);
+                    M0 += R0;
+                    M1 += R1;
+                    M2 = fmaf(ly, R0, M2);
+                    M3 += R2;
+                    M4 = fmaf(ly, R1, M4);
+                    M5 = fmaf(ly * ly, R0, M5);
+                }
+            }
+            M0 += xor_f32<16>(M0); M1 += xor_f32<16>(M1); M2 += xor_f32<16>(M2);
+            M3 += xor_f32<16>(M3); M4 += xor_f32<16>(M4); M5 += xor_f32<16>(M5);
+            C0 += xor_f32<16>(C0); C1 += xor_f32<16>(C1); C2 += xor_f32<16>(C2);
+            M0 += xor_f32<32>(M0); M1 += xor_f32<32>(M1); M2 += xor_f32<32>(M2);
+            M3 += xor_f32<32>(M3); M4 += xor_f32<32>(M4); M5 += xor_f32<32>(M5);
+            C0 += xor_f32<32>(C0); C1 += xor_f32<32>(C1); C2 += xor_f32<32>(C2);
+            // Gradient rows of the group staged in LDS (row layout of lsr_device.h:
+            // [0..5] geometry, [6..8] colour, [12..) language), then added with
+            // line-coalesced atomics: each 16-lane group covers one 64-B line of
+            // one Gaussian's row.  Language: lane holds slot 4*lg+r, channel nb*16+li.
+#pragma unroll
+            for (int nb = 0; nb < NBC; nb++) {
+                const int chn = nb * 16 + li;
+                if (chn < NL) {
+#pragma unroll
+                    for (int r = 0; r < 4; r++) sGr[(4 * lg + r) * GRS + LSR_GROW_LANG + chn] = ch[nb][r];
+                }
+            }
+            if (lane < kn) {   // lane = candidate li (lg = 0)
+                const int j = g0 + lane;
+                const float4 A = st.A[j];
+                const float4 B = st.B[j];
+                const float S0 = M0, S1 = M1, S2 = M2, S3 = M3, S4 = M4, S5 = M5;
+                const float X = A.x - cx, Y = A.y - cy;
+                const float Sdx = fmaf(X, S0, -S1), Sdy = fmaf(Y, S0, -S2);
+                const float Sdxx = fmaf(X, fmaf(X, S0, -2.f * S1), S3);
+                const float Sdxy = fmaf(X, fmaf(Y, S0, -S2), fmaf(-Y, S1, S4));
+                const float Sdyy = fmaf(Y, fmaf(Y, S0, -2.f * S2), S5);
+                const float o = B.y;
+                float* gr = sGr + lane * GRS;
+                gr[0] = -o * ddelx_dx * fmaf(A.z, Sdx, A.w * Sdy);
+                gr[1] = -o * ddely_dy * fmaf(B.x, Sdy, A.w * Sdx);
+                gr[2] = -0.5f * o * Sdxx;
+                gr[3] = -o * Sdxy;
+                gr[4] = -0.5f * o * Sdyy;
+                gr[5] = S0;
+#if LSR_BWD_VMOM
+                gr[6] = C0;
+                gr[7] = C1;
+                gr[8] = C2;
+#endif
+            }
+#else
             // phase 3: the group's gradients on MFMA
             f32x4 mom = {0.f, 0.f, 0.f, 0.f};
             f32x4 ch[NBC];
@@ -1101,10 +1320,10 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 m = li == 3 ? lx * lx : m;
                 m = li == 4 ? lx * ly : m;
                 m = li == 5 ? ly * ly : m;
-                mom = __builtin_amdgcn_mfma_f32_16x16x4f32(au, m, mom, 0, 0, 0);
+                mom = BWD_MFMA(au, m, mom);
 #pragma unroll
                 for (int nb = 0; nb < NBC; nb++)
-                    ch[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa, chB[nb][t], ch[nb], 0, 0, 0);
+                    ch[nb] = BWD_MFMA(aa, chB[nb][t], ch[nb]);
             }
             // Gradient rows of the group staged in LDS (row layout of lsr_device.h:
             // [0..5] geometry, [6..8] colour, [12..) language), then added with
@@ -1145,6 +1364,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 gr[4] = -0.5f * o * Sdyy;
                 gr[5] = S0;
             }
+#endif
             wave_lds_fence();
 #pragma unroll
             for (int h = 0; h < GRL; h++) {
@@ -1782,3 +2002,4 @@ hipError_t launch_render_bwd(const RenderBwdArgs& b, hipStream_t st)
 }
 
 }  // namespace lsr
+

@@ -36,19 +36,20 @@ static const float SH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570
 float lso_expf(float x)
 {
     if (x < -87.0f) return 0.0f;
-    float n = rintf(x * 1.44269504088896341f);
+    const float t = fmaf(x, 1.44269504088896341f, 12582912.0f);
+    const float n = t - 12582912.0f;
     float r = fmaf(n, -0.693145751953125f, x);
     r = fmaf(n, -1.428606765330187e-06f, r);
-    float p = 1.98412698412698413e-04f;
-    p = fmaf(p, r, 1.38888888888888889e-03f);
-    p = fmaf(p, r, 8.33333333333333333e-03f);
-    p = fmaf(p, r, 4.16666666666666667e-02f);
-    p = fmaf(p, r, 1.66666666666666667e-01f);
-    p = fmaf(p, r, 0.5f);
+    float p = 0x1.6aea1ap-10f;
+    p = fmaf(p, r, 0x1.1267d2p-7f);
+    p = fmaf(p, r, 0x1.555820p-5f);
+    p = fmaf(p, r, 0x1.555418p-3f);
+    p = fmaf(p, r, 0x1.fffffcp-2f);
     p = fmaf(p, r, 1.0f);
     p = fmaf(p, r, 1.0f);
-    int ni = (int)n;
-    uint32_t bits = (uint32_t)(ni + 127) << 23;
+    uint32_t tb;
+    memcpy(&tb, &t, 4);
+    const uint32_t bits = (tb << 23) + 0x3f800000u;
     float sc;
     memcpy(&sc, &bits, 4);
     return p * sc;

@@ -135,7 +135,8 @@ void lso_preprocess_bwd(const lso_settings* s, const lso_inputs* in, const lso_g
                         const lso_render_grads* rg, lso_param_grads* pg);
 
 /* The deterministic exponential shared (as a specification) with the HIP
- * kernels: Cody-Waite reduction + degree-7 Taylor in fmaf. */
+ * kernels: magic-number rounding, Cody-Waite reduction, degree-6 near-minimax
+ * polynomial in fmaf (<= 0.96 ulp). */
 float lso_expf(float x);
 
 /* Primitives: SH evaluation (sh: N*M*3, no +0.5), quaternion -> row-major R,

@@ -92,8 +92,12 @@ def run(name, case=None):
 
 
 if __name__ == "__main__":
+    # an existing fixture's stored inputs are reused (regenerating the inputs
+    # on another host could change their last bits); --fresh rebuilds them
+    fresh = "--fresh" in sys.argv
     for name in CASES:
-        out = run(name)
         path = os.path.join(HERE, f"oracle_{name}.npz")
+        case = None if fresh or not os.path.exists(path) else load_case(np.load(path))
+        out = run(name, case)
         np.savez_compressed(path, **out)
         print(name, os.path.getsize(path), "bytes", {k: v.shape for k, v in out.items()})

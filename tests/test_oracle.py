@@ -264,7 +264,7 @@ def test_expf_accuracy(oracle_lib):
     got = np.array([oracle_lib.expf(float(x)) for x in xs], np.float64)
     ref = np.exp(xs.astype(np.float64))
     rel = np.abs(got - ref) / ref
-    assert rel.max() < 4e-7, rel.max()   # < 4 ulp of fp32
+    assert rel.max() < 1.2e-7, rel.max()   # <= 1 ulp of fp32
     assert oracle_lib.expf(0.0) == 1.0
 
 
