@@ -41,6 +41,12 @@ __device__ __forceinline__ float expf_det(float x)
     return p * __uint_as_float((__float_as_uint(t) << 23) + 0x3f800000u);
 }
 
+// Wave votes on a bool.  HIP's __ballot/__any take an int, which makes the
+// compiler round-trip an SGPR lane mask through a VGPR (v_cndmask + v_cmp,
+// 2 VALU per vote); the builtin on i1 stays on the scalar unit.
+__device__ __forceinline__ uint64_t wave_ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+__device__ __forceinline__ bool wave_any(bool b) { return __builtin_amdgcn_ballot_w64(b) != 0; }
+
 // float -> int truncating + saturating; NaN -> 0 (matches oracle f2i).
 __device__ __forceinline__ int f2i(float v)
 {

@@ -39,6 +39,9 @@
 #ifndef LSR_FWD_PK
 #define LSR_FWD_PK 1        // fwd: pair-interleaved candidate geometry, packed (v_pk_*) exponent of 2 candidates
 #endif
+#ifndef LSR_FWD_SKIPVOTE
+#define LSR_FWD_SKIPVOTE 0  // fwd: skip a pair / its second candidate when no lane needs it (votes cost more than they save)
+#endif
 #ifndef LSR_MF_WAVES
 #define LSR_MF_WAVES 2      // MFMA render kernels: min waves per SIMD (caps VGPRs at 256)
 #endif
@@ -230,7 +233,7 @@ __device__ __forceinline__ uint64_t sub_mask(const float4* sA, const float4* sB,
         const float4 B = sB[j];
         ok = block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by);
     }
-    return __ballot(ok);
+    return wave_ballot(ok);
 }
 
 // Work-item mapping for the wave-independent render kernels: one 64-thread
@@ -278,7 +281,7 @@ __device__ __forceinline__ int stage_candidates(WaveStage<F4>& st, bool valid, u
 #else
     const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by);
 #endif
-    const uint64_t m = __ballot(ok);
+    const uint64_t m = wave_ballot(ok);
     const int cnt = __popcll(m);
     if (ok) {
         const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -318,7 +321,7 @@ __device__ __forceinline__ int stage_candidates_p(WaveStageP<F4>& st, bool valid
     }
     const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by) &&
                     block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, bx, by);
-    const uint64_t m = __ballot(ok);
+    const uint64_t m = wave_ballot(ok);
     const int cnt = __popcll(m);
     if (ok) {
         const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -367,7 +370,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
 
     uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
     for (uint32_t base = rs; base < re; base += 64) {
-        if (__ballot(!done) == 0) break;
+        if (wave_ballot(!done) == 0) break;
         const uint32_t idx = base + lane;
         const bool valid = idx < re;
         const uint32_t gid = next_gid;
@@ -385,7 +388,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
         // independent (ILP); T carries from the first to the second exactly
         // as in the sequential per-pixel order.
         for (int j0 = 0; j0 < n; j0 += 2) {
-            if (__ballot(!done) == 0) break;
+            if (wave_ballot(!done) == 0) break;
             const bool two = j0 + 1 < n;
             const int j1 = two ? j0 + 1 : j0;
 #if LSR_FWD_PK
@@ -400,7 +403,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
             const float p0 = P.x, p1 = P.y;
             bool ok0 = !done && !(p0 > 0.0f || p0 < CUT.x);
             bool ok1 = two && !done && !(p1 > 0.0f || p1 < CUT.y);
-            if (!__any(ok0 || ok1)) continue;
+            if (LSR_FWD_SKIPVOTE && !wave_any(ok0 || ok1)) continue;
             const float al0 = fminf(0.99f, OP.x * expf_det(p0));
             const float al1 = fminf(0.99f, OP.y * expf_det(p1));
 #else
@@ -410,7 +413,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
             const float p1 = splat_power(A1.z, A1.w, B1.x, A1.x - pfx, A1.y - pfy);
             bool ok0 = !done && !(p0 > 0.0f || p0 < B0.z);
             bool ok1 = two && !done && !(p1 > 0.0f || p1 < B1.z);
-            if (!__any(ok0 || ok1)) continue;
+            if (!wave_any(ok0 || ok1)) continue;
             const float al0 = fminf(0.99f, B0.y * expf_det(p0));
             const float al1 = fminf(0.99f, B1.y * expf_det(p1));
 #endif
@@ -434,7 +437,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 T = ok0 ? test_T : T;
                 last = ok0 ? (uint32_t)st.pos[j0] : last;
             }
-            if (__any(ok1)) {
+            if (!LSR_FWD_SKIPVOTE || wave_any(ok1)) {
                 const float test_T = T * (1.0f - al1);
                 const bool term = ok1 && (test_T < 0.0001f);
                 done = done || term;
@@ -521,9 +524,9 @@ __global__ void __launch_bounds__(64) k_render_fwd_quick(RenderArgs a)
         const uint32_t pos0 = base - rs + 1;
         bool ok = false;
         if (t < n) ok = block_overlap(sA[t].x, sA[t].y, __float_as_uint(sB[t].w), pm.bx, pm.by);
-        uint64_t bits = __ballot(ok);
+        uint64_t bits = wave_ballot(ok);
         while (bits) {
-            if (__ballot(!done) == 0) break;
+            if (wave_ballot(!done) == 0) break;
             const int j = __builtin_ctzll(bits);
             bits &= bits - 1;
             if (done) continue;
@@ -852,7 +855,7 @@ __global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs b)
                 alpha = fminf(0.99f, B.y * G);
                 contrib = alpha >= 1.0f / 255.0f;
             }
-            if (!__any(contrib)) continue;
+            if (!wave_any(contrib)) continue;
             // Branch-free from here: a non-contributing lane carries
             // alpha = G = 0, so every value it contributes is 0 and its
             // running state is left unchanged.
@@ -1000,7 +1003,7 @@ __device__ __forceinline__ int stage_candidates_geo(WaveStageG& st, int carry, b
     }
     const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by) &&
                     block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, bx, by);
-    const uint64_t m = __ballot(ok);
+    const uint64_t m = wave_ballot(ok);
     if (ok) {
         const int r = carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         st.A[r] = A;
@@ -1155,7 +1158,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 near_any |= (uint32_t)(cj & (fabsf(d) < 2e-8f));
                 sAT[k * GS + lane] = (cj & (d >= 0.f)) ? G : 0.f;
             }
-            if (__any(near_any != 0u)) {
+            if (wave_any(near_any != 0u)) {
                 // the 1/255 decision must be the forward's: lanes inside the fast
                 // exp's error band re-evaluate with the forward's exp (rare)
                 for (int k = 0; k < kn; k++) {
@@ -1419,7 +1422,7 @@ __device__ __forceinline__ int stage_candidates_f(WaveStageF& st, int carry, boo
     }
     const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by) &&
                     block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, bx, by);
-    const uint64_t m = __ballot(ok);
+    const uint64_t m = wave_ballot(ok);
     if (ok) {
         const int r = carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
         st.A[r] = A;
@@ -1472,7 +1475,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_fwd_mf(RenderArgs a
     int carry = 0;
     uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
     for (uint32_t base = rs; base < re; base += 64) {
-        if (__ballot(!done) == 0) break;
+        if (wave_ballot(!done) == 0) break;
         const uint32_t idx = base + lane;
         const bool valid = idx < re;
         const uint32_t gid = next_gid;
@@ -1482,7 +1485,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_fwd_mf(RenderArgs a
         const int nfull = (base + 64 >= re) ? n : (n & ~15);
         bool all_done = false;
         for (int g0 = 0; g0 < nfull; g0 += 16) {
-            if (__ballot(!done) == 0) {
+            if (wave_ballot(!done) == 0) {
                 all_done = true;
                 break;
             }
@@ -1631,7 +1634,7 @@ __global__ void __launch_bounds__(64) k_render_fwd_quick_mf(RenderArgs a)
     int carry = 0;
     uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
     for (uint32_t base = rs; base < re; base += 64) {
-        if (__ballot(!done) == 0) break;
+        if (wave_ballot(!done) == 0) break;
         const uint32_t idx = base + lane;
         const bool valid = idx < re;
         const uint32_t gid = next_gid;
@@ -1645,7 +1648,7 @@ __global__ void __launch_bounds__(64) k_render_fwd_quick_mf(RenderArgs a)
             }
             const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), pm.bx, pm.by) &&
                             block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, pm.bx, pm.by);
-            const uint64_t m = __ballot(ok);
+            const uint64_t m = wave_ballot(ok);
             if (ok) {
                 const int r = carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -1661,7 +1664,7 @@ __global__ void __launch_bounds__(64) k_render_fwd_quick_mf(RenderArgs a)
         const int nfull = (base + 64 >= re) ? n : (n & ~15);
         bool all_done = false;
         for (int g0 = 0; g0 < nfull; g0 += 16) {
-            if (__ballot(!done) == 0) {
+            if (wave_ballot(!done) == 0) {
                 all_done = true;
                 break;
             }
@@ -1826,7 +1829,7 @@ __global__ void __launch_bounds__(64 * NS) k_render_fwd_quick_wg(RenderArgs a)
     uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
     for (uint32_t base = rs; base < re; base += 64) {
         if (w == 0) {
-            const bool stop = __ballot(!done) == 0;
+            const bool stop = wave_ballot(!done) == 0;
             int nnew = 0;
             if (!stop) {
                 const uint32_t idx = base + lane;
@@ -1840,7 +1843,7 @@ __global__ void __launch_bounds__(64 * NS) k_render_fwd_quick_wg(RenderArgs a)
                 }
                 const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), pm.bx, pm.by) &&
                                 block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, pm.bx, pm.by);
-                const uint64_t m = __ballot(ok);
+                const uint64_t m = wave_ballot(ok);
                 if (ok) {
                     const int r = carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
