@@ -42,6 +42,12 @@
 #ifndef LSR_FWD_SKIPVOTE
 #define LSR_FWD_SKIPVOTE 0  // fwd: skip a pair / its second candidate when no lane needs it (votes cost more than they save)
 #endif
+#ifndef LSR_BWD_SPLAT_PF
+#define LSR_BWD_SPLAT_PF 1  // bwd: chunk records loaded one chunk ahead (ids two ahead), D <= 32
+#endif
+#ifndef LSR_BWD_AF_PF
+#define LSR_BWD_AF_PF 0     // bwd: next group's feature fragments loaded after the current dot product (slower: +4 %)
+#endif
 #ifndef LSR_MF_WAVES
 #define LSR_MF_WAVES 2      // MFMA render kernels: min waves per SIMD (caps VGPRs at 256)
 #endif
@@ -1014,6 +1020,23 @@ __device__ __forceinline__ int stage_candidates_geo(WaveStageG& st, int carry, b
     return __popcll(m);
 }
 
+// As stage_candidates_geo, with the chunk's records already loaded.
+__device__ __forceinline__ int stage_candidates_geo_rec(WaveStageG& st, int carry, bool valid, uint32_t gid, int pos,
+                                                        int bx, int by, float4 A, float4 B)
+{
+    const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by) &&
+                    block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, bx, by);
+    const uint64_t m = wave_ballot(ok);
+    if (ok) {
+        const int r = carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        st.A[r] = A;
+        st.B[r] = make_float4(B.x, B.y, B.z, __int_as_float(pos));
+        st.gid[r] = gid;
+    }
+    wave_lds_fence();
+    return __popcll(m);
+}
+
 // Feature c of Gaussian gid (rgb, then dense language; 0 past the channels).
 template <int NL>
 __device__ __forceinline__ float feature_at(const RenderArgs& a, uint32_t gid, int c)
@@ -1125,24 +1148,59 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     // positions [0, wmax) back to front, 64 per chunk; candidates are processed
     // in groups of 16, a partial group carried into the next chunk
     int carry = 0;
-    uint32_t next_gid = (wmax - 1 - lane >= 0) ? a.point_list[rs + wmax - 1 - lane] : 0u;
+    float af[KS];
+#if LSR_BWD_AF_PF
+    bool af_ready = false;
+#endif
+    // SPF: chunk c's ids are loaded two chunks ahead and its records one chunk
+    // ahead, so staging never waits on a dependent gather (9 more VGPRs: off
+    // for the widest language set, where they would spill)
+    constexpr bool SPF = LSR_BWD_SPLAT_PF && NL <= 32;
+    uint32_t gid1 = (wmax - 1 - lane >= 0) ? a.point_list[rs + wmax - 1 - lane] : 0u;
+    uint32_t gid2 = 0u;
+    float4 A1 = make_float4(0.f, 0.f, 0.f, 0.f), B1 = A1;
+    if constexpr (SPF) {
+        gid2 = (wmax - 65 - lane >= 0) ? a.point_list[rs + wmax - 65 - lane] : 0u;
+        if (wmax - 1 - lane >= 0) {
+            A1 = a.splatA[gid1];
+            B1 = a.splatB[gid1];
+        }
+    }
     for (int c0 = 0; c0 < wmax; c0 += 64) {
         const int p = wmax - 1 - (c0 + lane);
         const bool valid = p >= 0;
-        const uint32_t gid = next_gid;
-        next_gid = (p - 64 >= 0) ? a.point_list[rs + p - 64] : 0u;
-        const int n = carry + stage_candidates_geo(st, carry, valid, gid, p, pm.bx, pm.by, a.splatA, a.splatB);
+        int n;
+        if constexpr (SPF) {
+            const uint32_t gid = gid1;
+            const float4 Ac = A1, Bc = B1;
+            gid1 = gid2;
+            A1 = make_float4(0.f, 0.f, 0.f, 0.f);
+            B1 = A1;
+            if (p - 64 >= 0) {
+                A1 = a.splatA[gid1];
+                B1 = a.splatB[gid1];
+            }
+            gid2 = (p - 128 >= 0) ? a.point_list[rs + p - 128] : 0u;
+            n = carry + stage_candidates_geo_rec(st, carry, valid, gid, p, pm.bx, pm.by, Ac, Bc);
+        } else {
+            const uint32_t gid = gid1;
+            gid1 = (p - 64 >= 0) ? a.point_list[rs + p - 64] : 0u;
+            n = carry + stage_candidates_geo(st, carry, valid, gid, p, pm.bx, pm.by, a.splatA, a.splatB);
+        }
         const int nfull = (c0 + 64 >= wmax) ? n : (n & ~15);
 
         for (int g0 = 0; g0 < nfull; g0 += 16) {
             const int kn = min(16, nfull - g0);
             // A fragments of the dot product: feature 4t+lg of candidate g0+li,
             // gathered now, consumed after phase 1
-            float af[KS];
+#if LSR_BWD_AF_PF
+            if (!af_ready)
+#endif
             {
                 const uint32_t gi = st.gid[g0 + (li < kn ? li : 0)];
 #pragma unroll
-                for (int t = 0; t < KS; t++) af[t] = feature_at<NL>(a, gi, 4 * t + lg);
+                for (int t = 0; t < KS; t++)
+                    af[t] = feature_at<NL>(a, gi, 4 * t + lg);
             }
             // phase 1: G of the 16 candidates (0 where the pair does not
             // contribute), independent across candidates; straight-line code
@@ -1190,6 +1248,16 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #pragma unroll
                     for (int r = 0; r < 4; r++) sDU[(4 * lg + r) * GS + pb * 16 + li] = acc[pb][r];
             }
+#if LSR_BWD_AF_PF
+            // the next group's feature fragments, when it is staged already
+            af_ready = g0 + 16 < nfull;
+            if (af_ready) {
+                const int kn2 = min(16, nfull - g0 - 16);
+                const uint32_t gi = st.gid[g0 + 16 + (li < kn2 ? li : 0)];
+#pragma unroll
+                for (int t = 0; t < KS; t++) af[t] = feature_at<NL>(a, gi, 4 * t + lg);
+            }
+#endif
             wave_lds_fence();
             // phase 2: the serial back-to-front recurrence per pixel.  S is the
             // colour accumulated behind the current instance (the upstream

@@ -193,6 +193,9 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.save_for_backward(*saved, radii, bufs[_lib.LSR_BUF_GEOM], bufs[_lib.LSR_BUF_BINNING],
                               bufs[_lib.LSR_BUF_IMAGE])
         ctx.mark_non_differentiable(radii)
+        # backward handles None upstream gradients itself; without this autograd
+        # zero-fills a gradient for the int radii output every step
+        ctx.set_materialize_grads(False)
         return color, lang_out, radii
 
     @staticmethod
