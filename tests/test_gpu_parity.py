@@ -106,6 +106,16 @@ def test_big_tile_global_sort(gpu, oracle_lib):
     assert counts.max() > 4096, counts.max()
 
 
+@pytest.mark.parametrize("N,W,H,lo,hi", [(4000, 48, 32, 512, 1024), (12000, 64, 48, 1024, 2048)])
+def test_tile_sort_size_classes(gpu, oracle_lib, N, W, H, lo, hi):
+    """Tiles of 513-1024 instances (one wave, 16 keys per lane) and of
+    1025-2048 (one wave, 32 keys per lane): bit-exact lists."""
+    case = make_case(N=N, W=W, H=H, sh_degree=None, seed=12)
+    ref, got = _fwd_compare(case, gpu, oracle_lib)
+    counts = ref["ranges"][:, 1] - ref["ranges"][:, 0]
+    assert counts.min() > lo and counts.max() <= hi, (counts.min(), counts.max())
+
+
 def test_forward_deterministic(gpu):
     case = make_case(**CASES["sh3_lang16_ragged"])
     a = run_gpu_forward(case, gpu)
