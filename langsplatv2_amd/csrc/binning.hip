@@ -16,6 +16,8 @@
 // duplicates emitted in Gaussian order.
 #include "lsr_internal.h"
 
+#include <algorithm>
+
 #ifndef LSR_SORT_DPP
 #define LSR_SORT_DPP 1
 #endif
@@ -121,19 +123,70 @@ hipError_t launch_scan_u32(const uint32_t* in, uint32_t* out, uint64_t* part, si
 // latency in the middle of every forward.  Totals >= 2^32 - 1 saturate (the
 // host reports LSR_EOVERFLOW).
 __global__ void k_publish_total(const uint64_t* __restrict__ total, uint32_t* __restrict__ tile_end,
-                                uint64_t* host_slot, uint32_t seq)
+                                uint64_t* host_slot, uint32_t seq, const uint32_t* __restrict__ cls_cnt)
 {
     const uint64_t m = *total;
     const uint32_t m32 = m >= 0xffffffffull ? 0xffffffffu : (uint32_t)m;
     if (tile_end) *tile_end = m32;
+    if (cls_cnt) {
+        // per-class tile counts ride along in the same pinned line: the host
+        // launches exactly the sort classes that have work
+        uint32_t* h = (uint32_t*)(host_slot + 1);
+#pragma unroll
+        for (int k = 0; k < SORT_NCLS; k++) h[k] = cls_cnt[k];
+    }
     __atomic_store_n(host_slot, ((uint64_t)seq << 32) | m32, __ATOMIC_RELEASE);
 }
 
 hipError_t launch_publish_total(const uint64_t* total, uint32_t* tile_end, uint64_t* host_slot, uint32_t seq,
-                                hipStream_t st)
+                                const uint32_t* cls_cnt, hipStream_t st)
 {
-    k_publish_total<<<1, 1, 0, st>>>(total, tile_end, host_slot, seq);
+    k_publish_total<<<1, 1, 0, st>>>(total, tile_end, host_slot, seq, cls_cnt);
     return hipGetLastError();
+}
+
+// Sort size classes: 0 wave sort (n <= 512), 1..4 block merge sorts with
+// KPL = 4, 8, 16, 32 (n <= 256*KPL), 5 chunked LDS/global (n > 8192).  Empty
+// tiles are in no class.
+__device__ __forceinline__ int tile_class(int n)
+{
+    if (n <= 0) return -1;
+    if (n <= 512) return 0;
+    if (n <= 1024) return 1;
+    if (n <= 2048) return 2;
+    if (n <= 4096) return 3;
+    if (n <= 8192) return 4;
+    return 5;
+}
+
+// Wave-aggregated append of tile t (lanes with active) to its class list.
+// Every lane of the wave must call it.
+__device__ __forceinline__ void tile_class_append(bool active, int t, int n, int T, uint32_t* __restrict__ cls_cnt,
+                                                  uint32_t* __restrict__ cls_list)
+{
+    const int c = active ? tile_class(n) : -1;
+    const int lane = threadIdx.x & 63;
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+#pragma unroll
+    for (int k = 0; k < SORT_NCLS; k++) {
+        const uint64_t m = __ballot(c == k);
+        if (m == 0) continue;
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&cls_cnt[k], (uint32_t)__popcll(m));
+        base = __shfl(base, leader, 64);
+        if (c == k) cls_list[(size_t)k * T + base + __popcll(m & below)] = (uint32_t)t;
+    }
+}
+
+// Classification pass for the global-atomic binning path (the privatised path
+// classifies inside k_bin_table).  cls_cnt must be zero.
+__global__ void __launch_bounds__(256) k_tile_classify(int T, const uint32_t* __restrict__ tile_start,
+                                                       uint32_t* __restrict__ cls_cnt, uint32_t* __restrict__ cls_list)
+{
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    const int n = t < T ? (int)(tile_start[t + 1] - tile_start[t]) : 0;
+    tile_class_append(t < T, t, n, T, cls_cnt, cls_list);
 }
 
 // ----------------------------------------------------- duplicate / scatter --
@@ -211,12 +264,35 @@ __device__ __forceinline__ void bin_rect(const Cam& c, const uint8_t* geom, int 
     get_rect(A.x, A.y, r, c.gx, c.gy, x0, y0, x1, y1);
 }
 
-__global__ void __launch_bounds__(BIN_BLOCK) k_bin_count(Cam c, int P, int chunk, const uint8_t* __restrict__ geom,
-                                                         const int32_t* __restrict__ radii, uint32_t* __restrict__ table)
+// Screen bands: blockIdx.y = band of `rows` tile rows, so a block's LDS
+// histogram covers rows * gx tiles (<= LSR_BAND_LDS bytes) and several blocks
+// stay resident per CU at any resolution; a Gaussian's rect is clipped to the
+// band (each band re-reads the chunk's 20-B records, cheap next to the
+// instance work).
+#ifndef LSR_BAND_LDS
+#define LSR_BAND_LDS 32768
+#endif
+struct Band {
+    int ty0, ty1, t0, nt;
+    __device__ Band(const Cam& c, int rows)
+    {
+        ty0 = blockIdx.y * rows;
+        ty1 = min(c.gy, ty0 + rows);
+        t0 = ty0 * c.gx;
+        nt = (ty1 - ty0) * c.gx;
+    }
+};
+
+__global__ void __launch_bounds__(BIN_BLOCK) k_bin_count(Cam c, int P, int chunk, int rows,
+                                                         const uint8_t* __restrict__ geom,
+                                                         const int32_t* __restrict__ radii, uint32_t* __restrict__ table,
+                                                         uint32_t* __restrict__ cls_cnt)
 {
     extern __shared__ uint32_t hist[];
     const int T = c.gx * c.gy;
-    for (int k = threadIdx.x; k < T; k += BIN_BLOCK) hist[k] = 0;
+    const Band bd(c, rows);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < SORT_NCLS) cls_cnt[threadIdx.x] = 0;   // k_bin_table appends after us
+    for (int k = threadIdx.x; k < bd.nt; k += BIN_BLOCK) hist[k] = 0;
     __syncthreads();
     const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
     for (int i = g0 + threadIdx.x; i < g1; i += BIN_BLOCK) {
@@ -224,12 +300,14 @@ __global__ void __launch_bounds__(BIN_BLOCK) k_bin_count(Cam c, int P, int chunk
         if (r <= 0) continue;
         int x0, y0, x1, y1;
         bin_rect(c, geom, P, i, r, x0, y0, x1, y1);
+        y0 = max(y0, bd.ty0);
+        y1 = min(y1, bd.ty1);
         for (int y = y0; y < y1; y++)
-            for (int x = x0; x < x1; x++) atomicAdd(&hist[y * c.gx + x], 1u);
+            for (int x = x0; x < x1; x++) atomicAdd(&hist[(y - bd.ty0) * c.gx + x], 1u);
     }
     __syncthreads();
-    uint32_t* row = table + (size_t)blockIdx.x * T;
-    for (int k = threadIdx.x; k < T; k += BIN_BLOCK) row[k] = hist[k];
+    uint32_t* row = table + (size_t)blockIdx.x * T + bd.t0;
+    for (int k = threadIdx.x; k < bd.nt; k += BIN_BLOCK) row[k] = hist[k];
 }
 
 // Column scan: table[b][t] <- sum_{b' < b} table[b'][t]; tile_cnt[t] <- total.
@@ -239,7 +317,8 @@ __global__ void __launch_bounds__(BIN_BLOCK) k_bin_count(Cam c, int P, int chunk
 #define TBL_COLS 32
 #define TBL_SEGS 8
 __global__ void __launch_bounds__(256) k_bin_table(int T, int B, uint32_t* __restrict__ table,
-                                                   uint32_t* __restrict__ tile_cnt)
+                                                   uint32_t* __restrict__ tile_cnt, uint32_t* __restrict__ cls_cnt,
+                                                   uint32_t* __restrict__ cls_list)
 {
     __shared__ uint32_t seg_sum[TBL_SEGS][TBL_COLS];
     const int col = threadIdx.x % TBL_COLS, seg = threadIdx.x / TBL_COLS;
@@ -266,6 +345,7 @@ __global__ void __launch_bounds__(256) k_bin_table(int T, int B, uint32_t* __res
         run += (k < seg) ? x : 0u;
         tot += x;
     }
+    if (threadIdx.x < 64) tile_class_append(seg == 0 && t < T, t, (int)tot, T, cls_cnt, cls_list);
     if (t >= T) return;
     if (seg == 0) tile_cnt[t] = tot;
     for (int b = b0; b < b1; b++) {
@@ -275,7 +355,8 @@ __global__ void __launch_bounds__(256) k_bin_table(int T, int B, uint32_t* __res
     }
 }
 
-__global__ void __launch_bounds__(BIN_BLOCK) k_bin_scatter(Cam c, int P, int chunk, const uint8_t* __restrict__ geom,
+__global__ void __launch_bounds__(BIN_BLOCK) k_bin_scatter(Cam c, int P, int chunk, int rows,
+                                                           const uint8_t* __restrict__ geom,
                                                            const int32_t* __restrict__ radii,
                                                            const uint32_t* __restrict__ table,
                                                            const uint32_t* __restrict__ tile_start,
@@ -283,8 +364,9 @@ __global__ void __launch_bounds__(BIN_BLOCK) k_bin_scatter(Cam c, int P, int chu
 {
     extern __shared__ uint32_t base[];
     const int T = c.gx * c.gy;
-    const uint32_t* row = table + (size_t)blockIdx.x * T;
-    for (int k = threadIdx.x; k < T; k += BIN_BLOCK) base[k] = tile_start[k] + row[k];
+    const Band bd(c, rows);
+    const uint32_t* row = table + (size_t)blockIdx.x * T + bd.t0;
+    for (int k = threadIdx.x; k < bd.nt; k += BIN_BLOCK) base[k] = tile_start[bd.t0 + k] + row[k];
     __syncthreads();
     const GeomLayout L = geom_layout(P);
     const float* depth = (const float*)(geom + L.depth);
@@ -294,35 +376,55 @@ __global__ void __launch_bounds__(BIN_BLOCK) k_bin_scatter(Cam c, int P, int chu
         if (r <= 0) continue;
         int x0, y0, x1, y1;
         bin_rect(c, geom, P, i, r, x0, y0, x1, y1);
+        y0 = max(y0, bd.ty0);
+        y1 = min(y1, bd.ty1);
+        if (y0 >= y1) continue;
         const uint64_t key = ((uint64_t)__float_as_uint(depth[i]) << 32) | (uint32_t)i;
         for (int y = y0; y < y1; y++)
-            for (int x = x0; x < x1; x++) keys[atomicAdd(&base[y * c.gx + x], 1u)] = key;
+            for (int x = x0; x < x1; x++) keys[atomicAdd(&base[(y - bd.ty0) * c.gx + x], 1u)] = key;
     }
 }
 
-int bin_blocks(int P, int T, int& chunk)
+// Tile rows per band: the largest band whose histogram fits LSR_BAND_LDS.
+static int bin_band_rows(const Cam& c)
 {
-    // ~512 blocks (2 per CU) of >= 1024 Gaussians; the B x T table stays small
-    chunk = max(1024, (P + 511) / 512);
+    return std::max(1, std::min(c.gy, LSR_BAND_LDS / (4 * c.gx)));
+}
+
+int bin_blocks(int P, const Cam& c, int& chunk)
+{
+    // ~512 (chunk x band) blocks, 2 per CU, of >= 1024 Gaussians; fewer
+    // chunks when there are several bands keeps the B x T table small
+    const int rows = bin_band_rows(c);
+    const int S = (c.gy + rows - 1) / rows;
+    const int target = std::max(64, 512 / S);
+    chunk = max(1024, (P + target - 1) / target);
     chunk = (chunk + BIN_BLOCK - 1) / BIN_BLOCK * BIN_BLOCK;
     return (P + chunk - 1) / chunk;
 }
 
-bool bin_privatised_ok(int T) { return (size_t)T * 4 <= 150 * 1024; }
+// The privatised path needs one band row of tiles to fit LDS and a B x T
+// table of moderate size.
+bool bin_privatised_ok(const Cam& c) { return (size_t)c.gx * 4 <= LSR_BAND_LDS && (size_t)c.gx * c.gy <= (1u << 20); }
 
 hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t* geom, const int32_t* radii,
-                            uint32_t* table, uint32_t* tile_cnt, hipStream_t st)
+                            uint32_t* table, uint32_t* tile_cnt, uint32_t* cls_cnt, uint32_t* cls_list,
+                            hipStream_t st)
 {
     const int T = c.gx * c.gy;
-    if ((size_t)T * 4 > 65536) {
-        (void)hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize, T * 4);
-        (void)hipFuncSetAttribute((const void*)k_bin_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, T * 4);
+    const int rows = bin_band_rows(c);
+    const dim3 grid(B, (c.gy + rows - 1) / rows);
+    const size_t lds = (size_t)rows * c.gx * 4;
+    if (lds > 65536) {
+        (void)hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)k_bin_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
     if (B > 0) {
-        k_bin_count<<<B, BIN_BLOCK, (size_t)T * 4, st>>>(c, P, chunk, geom, radii, table);
-        k_bin_table<<<(T + TBL_COLS - 1) / TBL_COLS, 256, 0, st>>>(T, B, table, tile_cnt);
+        k_bin_count<<<grid, BIN_BLOCK, lds, st>>>(c, P, chunk, rows, geom, radii, table, cls_cnt);
+        k_bin_table<<<(T + TBL_COLS - 1) / TBL_COLS, 256, 0, st>>>(T, B, table, tile_cnt, cls_cnt, cls_list);
     } else {
         (void)hipMemsetAsync(tile_cnt, 0, (size_t)T * 4, st);
+        (void)hipMemsetAsync(cls_cnt, 0, SORT_NCLS * 4, st);
     }
     return hipGetLastError();
 }
@@ -330,8 +432,11 @@ hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t
 hipError_t launch_bin_scatter(const Cam& c, int P, int chunk, int B, const uint8_t* geom, const int32_t* radii,
                               const uint32_t* table, const uint32_t* tile_start, uint64_t* keys, hipStream_t st)
 {
-    const int T = c.gx * c.gy;
-    if (B > 0) k_bin_scatter<<<B, BIN_BLOCK, (size_t)T * 4, st>>>(c, P, chunk, geom, radii, table, tile_start, keys);
+    const int rows = bin_band_rows(c);
+    const dim3 grid(B, (c.gy + rows - 1) / rows);
+    if (B > 0)
+        k_bin_scatter<<<grid, BIN_BLOCK, (size_t)rows * c.gx * 4, st>>>(c, P, chunk, rows, geom, radii, table,
+                                                                       tile_start, keys);
     return hipGetLastError();
 }
 
@@ -388,22 +493,21 @@ __device__ __forceinline__ int next_pow2(int n)
     return p;
 }
 
-__global__ void __launch_bounds__(SORT_BLOCK) k_tile_sort(int T, const uint32_t* __restrict__ tile_start,
-                                                          uint64_t* __restrict__ keys, uint32_t* __restrict__ point_list,
-                                                          int min_n)
+// Tiles of class 5 (n > 8192): one workgroup per tile (grid-stride over the
+// class list), chunk-local bitonic stages in LDS, cross-chunk stages in
+// global memory.
+__device__ void tile_sort_big(int t, const uint32_t* __restrict__ tile_start, uint64_t* __restrict__ keys,
+                              uint32_t* __restrict__ point_list, uint64_t* buf)
 {
-    __shared__ uint64_t buf[SORT_CHUNK];
-    const int t = xcd_remap(blockIdx.x, gridDim.x);
-    if (t >= T) return;
     const uint32_t s0 = tile_start[t], s1 = tile_start[t + 1];
     const int n = (int)(s1 - s0);
-    if (n == 0 || n < min_n) return;
     uint64_t* g = keys + s0;
     if (n <= SORT_CHUNK) {
         for (int k = threadIdx.x; k < n; k += SORT_BLOCK) buf[k] = g[k];
         __syncthreads();
         bitonic_lds(buf, n, next_pow2(n));
         for (int k = threadIdx.x; k < n; k += SORT_BLOCK) point_list[s0 + k] = (uint32_t)buf[k];
+        __syncthreads();
         return;
     }
     // Large tile: chunk-local stages in LDS, cross-chunk stages in global
@@ -443,6 +547,19 @@ __global__ void __launch_bounds__(SORT_BLOCK) k_tile_sort(int T, const uint32_t*
         }
     }
     for (int k = threadIdx.x; k < n; k += SORT_BLOCK) point_list[s0 + k] = (uint32_t)g[k];
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(SORT_BLOCK) k_tile_sort_big(int T, const uint32_t* __restrict__ tile_start,
+                                                              uint64_t* __restrict__ keys,
+                                                              uint32_t* __restrict__ point_list,
+                                                              const uint32_t* __restrict__ cls_cnt,
+                                                              const uint32_t* __restrict__ cls_list)
+{
+    __shared__ uint64_t buf[SORT_CHUNK];
+    const uint32_t cnt = cls_cnt[5];
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x)
+        tile_sort_big((int)cls_list[(size_t)5 * T + i], tile_start, keys, point_list, buf);
 }
 
 // Wave-level register bitonic sort for tiles of n <= 64*KPL keys: lane l
@@ -541,7 +658,7 @@ __device__ __forceinline__ void wave_sort_stages(uint64_t (&v)[KPL])
 }
 
 template <int KPL>
-__device__ __forceinline__ void wave_sort_tile(uint64_t* __restrict__ g, uint32_t* __restrict__ out, int n)
+__device__ __forceinline__ void wave_sort_tile(const uint64_t* __restrict__ g, uint32_t* __restrict__ out, int n)
 {
     const int lane = threadIdx.x & 63;
     uint64_t v[KPL];
@@ -558,35 +675,163 @@ __device__ __forceinline__ void wave_sort_tile(uint64_t* __restrict__ g, uint32_
     }
 }
 
-// One wave per tile (4 tiles per 256-thread block).  Tiles above 2048 keys are
-// left to k_tile_sort_big.
-__global__ void __launch_bounds__(256) k_tile_sort_wave(int T, const uint32_t* __restrict__ tile_start,
-                                                        uint64_t* __restrict__ keys, uint32_t* __restrict__ point_list)
+// LDS slot of logical element e of a block sort: one u64 of padding every 16
+// keys, so the lane-major run reads (lane stride KPL*8 bytes) spread over
+// the banks instead of piling onto a few.
+__device__ __forceinline__ int lpad(int e) { return e + (e >> 4); }
+
+// Merge-path co-rank: how many of the first d outputs of merge(A, B) come
+// from A, A = lds[a0, a0+na), B = lds[b0, b0+nb) (logical indices; keys are
+// unique, so ties never occur).
+__device__ __forceinline__ int merge_corank(const uint64_t* lds, int a0, int na, int b0, int nb, int d)
 {
-    const int w = threadIdx.x >> 6;
-    const int t = xcd_remap(blockIdx.x, gridDim.x) * 4 + w;
-    if (t >= T) return;
-    const uint32_t s0 = tile_start[t];
-    const int n = (int)(tile_start[t + 1] - s0);
-    if (n <= 1) {
-        if (n == 1 && (threadIdx.x & 63) == 0) point_list[s0] = (uint32_t)keys[s0];
-        return;
+    int lo = max(0, d - nb), hi = min(d, na);
+    while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (lds[lpad(a0 + m)] < lds[lpad(b0 + d - 1 - m)]) lo = m + 1;
+        else hi = m;
     }
-    uint64_t* g = keys + s0;
-    uint32_t* o = point_list + s0;
-    if (n <= 64) wave_sort_tile<1>(g, o, n);
-    else if (n <= 128) wave_sort_tile<2>(g, o, n);
-    else if (n <= 256) wave_sort_tile<4>(g, o, n);
-    else if (n <= 512) wave_sort_tile<8>(g, o, n);
-    else if (n <= 1024) wave_sort_tile<16>(g, o, n);
-    else if (n <= 2048) wave_sort_tile<32>(g, o, n);
+    return lo;
 }
 
-hipError_t launch_tile_sort(int T, const uint32_t* tile_start, uint64_t* keys, uint32_t* point_list, hipStream_t st)
+// KPL consecutive outputs of merge(A, B) starting at output d, into v.
+template <int KPL>
+__device__ __forceinline__ void merge_run(const uint64_t* lds, int a0, int na, int b0, int nb, int d,
+                                          uint64_t (&v)[KPL])
+{
+    int i = merge_corank(lds, a0, na, b0, nb, d), j = d - i;
+    uint64_t a = i < na ? lds[lpad(a0 + i)] : ~0ull, b = j < nb ? lds[lpad(b0 + j)] : ~0ull;
+#pragma unroll
+    for (int k = 0; k < KPL; k++) {
+        const bool ta = a < b;
+        v[k] = ta ? a : b;
+        i += ta ? 1 : 0;
+        j += ta ? 0 : 1;
+        const bool ok = ta ? (i < na) : (j < nb);
+        const uint64_t nx = ok ? lds[lpad(ta ? a0 + i : b0 + j)] : ~0ull;
+        a = ta ? nx : a;
+        b = ta ? b : nx;
+    }
+}
+
+// One 4-wave workgroup per tile of 128*KPL < n <= 256*KPL keys.  The bucket
+// is staged into LDS with coalesced loads (+inf padding), each wave sorts a
+// 64*KPL run in registers (the wave bitonic network above), two merge-path
+// rounds (every thread producing KPL consecutive outputs after a binary
+// co-rank search) finish the order, and the ids leave through LDS with
+// coalesced stores.
+template <int KPL>
+__device__ __forceinline__ void block_sort_tile(const uint64_t* __restrict__ g, uint32_t* __restrict__ out, int n,
+                                                uint64_t* lds)
+{
+    constexpr int R = 64 * KPL;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // batches of 8 loads in flight per thread (a full unroll would hold all
+    // 4*KPL keys in VGPRs and collapse occupancy)
+#pragma unroll 1
+    for (int k0 = 0; k0 < 4 * KPL; k0 += 8) {
+        uint64_t x[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int e = (k0 + k) * 256 + tid;
+            x[k] = e < n ? g[e] : ~0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) lds[lpad((k0 + k) * 256 + tid)] = x[k];
+    }
+    __syncthreads();
+    uint64_t v[KPL];
+#pragma unroll
+    for (int r = 0; r < KPL; r++) v[r] = lds[lpad(w * R + lane * KPL + r)];
+    wave_sort_stages<KPL, 2>(v);
+#pragma unroll
+    for (int r = 0; r < KPL; r++) lds[lpad(w * R + lane * KPL + r)] = v[r];
+    __syncthreads();
+    {
+        const int p0 = (tid >> 7) * 2 * R, d = (tid & 127) * KPL;
+        merge_run<KPL>(lds, p0, R, p0 + R, R, d, v);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < KPL; k++) lds[lpad(p0 + d + k)] = v[k];
+    }
+    __syncthreads();
+    const int d = tid * KPL;
+    merge_run<KPL>(lds, 0, 2 * R, 2 * R, 2 * R, d, v);
+    __syncthreads();
+    uint32_t* l32 = (uint32_t*)lds;
+#pragma unroll
+    for (int k = 0; k < KPL; k++) l32[d + k + ((d + k) >> 5)] = (uint32_t)v[k];
+    __syncthreads();
+#pragma unroll 8
+    for (int e = tid; e < n; e += 256) out[e] = l32[e + (e >> 5)];
+    __syncthreads();
+}
+
+// Class c = 1..4 (KPL = 4 << (c - 1)): one workgroup per listed tile.
+template <int KPL>
+__global__ void __launch_bounds__(256) k_tile_sort_blk(int T, const uint32_t* __restrict__ tile_start,
+                                                       const uint64_t* __restrict__ keys,
+                                                       uint32_t* __restrict__ point_list,
+                                                       const uint32_t* __restrict__ cls_cnt,
+                                                       const uint32_t* __restrict__ cls_list, int cls)
+{
+    __shared__ uint64_t lds[(4 * 64 * KPL) * 17 / 16];
+    const uint32_t cnt = cls_cnt[cls];
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+        const int t = (int)cls_list[(size_t)cls * T + i];
+        const uint32_t s0 = tile_start[t];
+        block_sort_tile<KPL>(keys + s0, point_list + s0, (int)(tile_start[t + 1] - s0), lds);
+    }
+}
+
+// Class 0 (n <= 512): one wave per listed tile, four per workgroup.
+__global__ void __launch_bounds__(256) k_tile_sort_wave(int T, const uint32_t* __restrict__ tile_start,
+                                                        const uint64_t* __restrict__ keys,
+                                                        uint32_t* __restrict__ point_list,
+                                                        const uint32_t* __restrict__ cls_cnt,
+                                                        const uint32_t* __restrict__ cls_list)
+{
+    const uint32_t cnt = cls_cnt[0];
+    for (uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6); i < cnt; i += gridDim.x * 4) {
+        const int t = (int)cls_list[i];
+        const uint32_t s0 = tile_start[t];
+        const int n = (int)(tile_start[t + 1] - s0);
+        const uint64_t* g = keys + s0;
+        uint32_t* o = point_list + s0;
+        if (n == 1) {
+            if ((threadIdx.x & 63) == 0) o[0] = (uint32_t)g[0];
+        } else if (n <= 64) wave_sort_tile<1>(g, o, n);
+        else if (n <= 128) wave_sort_tile<2>(g, o, n);
+        else if (n <= 256) wave_sort_tile<4>(g, o, n);
+        else wave_sort_tile<8>(g, o, n);
+    }
+}
+
+// host_cnt: the per-class tile counts when the host already has them (the
+// privatised binning path publishes them with M); null = unknown, the lists
+// are built here and every class runs a persistent grid.
+hipError_t launch_tile_sort(int T, const uint32_t* tile_start, uint64_t* keys, uint32_t* point_list,
+                            uint32_t* cls_cnt, uint32_t* cls_list, const uint32_t* host_cnt, hipStream_t st)
 {
     if (T == 0) return hipSuccess;
-    k_tile_sort_wave<<<(T + 3) / 4, 256, 0, st>>>(T, tile_start, keys, point_list);
-    k_tile_sort<<<T, SORT_BLOCK, 0, st>>>(T, tile_start, keys, point_list, 2049);
+    uint32_t cnt[SORT_NCLS];
+    if (host_cnt) {
+        for (int k = 0; k < SORT_NCLS; k++) cnt[k] = host_cnt[k];
+    } else {
+        (void)hipMemsetAsync(cls_cnt, 0, SORT_NCLS * 4, st);
+        k_tile_classify<<<(T + 255) / 256, 256, 0, st>>>(T, tile_start, cls_cnt, cls_list);
+        // persistent grids: enough workgroups to fill the chip, or the tiles
+        const uint32_t fill[SORT_NCLS] = {256 * 8, 256 * 8, 256 * 8, 256 * 4, 256 * 2, 256 * 2};
+        for (int k = 0; k < SORT_NCLS; k++) cnt[k] = std::min<uint32_t>((uint32_t)T, fill[k] * (k == 0 ? 4 : 1));
+    }
+    const uint32_t* cc = cls_cnt;
+    const uint32_t* cl = cls_list;
+    if (cnt[0]) k_tile_sort_wave<<<(cnt[0] + 3) / 4, 256, 0, st>>>(T, tile_start, keys, point_list, cc, cl);
+    if (cnt[1]) k_tile_sort_blk<4><<<cnt[1], 256, 0, st>>>(T, tile_start, keys, point_list, cc, cl, 1);
+    if (cnt[2]) k_tile_sort_blk<8><<<cnt[2], 256, 0, st>>>(T, tile_start, keys, point_list, cc, cl, 2);
+    if (cnt[3]) k_tile_sort_blk<16><<<cnt[3], 256, 0, st>>>(T, tile_start, keys, point_list, cc, cl, 3);
+    if (cnt[4]) k_tile_sort_blk<32><<<cnt[4], 256, 0, st>>>(T, tile_start, keys, point_list, cc, cl, 4);
+    if (cnt[5]) k_tile_sort_big<<<cnt[5], SORT_BLOCK, 0, st>>>(T, tile_start, keys, point_list, cc, cl);
     return hipGetLastError();
 }
 

@@ -379,9 +379,9 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     const GeomLayout GL = geom_layout((size_t)P);
     const ImageLayout IL = image_layout(NPIX, (size_t)T);
     // privatised binning needs a B x T table (tail of the image workspace)
-    const bool priv = P > 0 && bin_privatised_ok(T);
+    const bool priv = P > 0 && bin_privatised_ok(c);
     int chunk = 0;
-    const int B = priv ? bin_blocks(P, T, chunk) : 0;
+    const int B = priv ? bin_blocks(P, c, chunk) : 0;
     const size_t table_bytes = priv ? align256((size_t)B * T * 4) : 0;
     uint8_t* geom = (uint8_t*)alloc(ctx, GL.total, LSR_BUF_GEOM);
     uint8_t* img = (uint8_t*)alloc(ctx, IL.total + table_bytes, LSR_BUF_IMAGE);
@@ -395,6 +395,8 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     uint32_t* tile_start = (uint32_t*)(img + IL.tile_start);
     uint64_t* tpart = (uint64_t*)(img + IL.tile_part);
     const size_t tnb = scan_partials((size_t)T) - 1;
+    uint32_t* cls_cnt = (uint32_t*)(img + IL.cls_cnt);
+    uint32_t* cls_list = (uint32_t*)(img + IL.cls_list);
 
     // 1. preprocess
     { StageScope sc(ST_PRE, st); LSR_HIP(launch_preprocess(c, *in, geom, out->radii, st)); }
@@ -406,12 +408,12 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
         // 2. per-block tile histograms -> column scan -> tile starts; M = total
         {
             StageScope sc(ST_DUP, st);
-            LSR_HIP(launch_bin_count(c, P, chunk, B, geom, out->radii, table, tile_cnt, st));
+            LSR_HIP(launch_bin_count(c, P, chunk, B, geom, out->radii, table, tile_cnt, cls_cnt, cls_list, st));
         }
         {
             StageScope sc(ST_SCAN_T, st);
             LSR_HIP(launch_scan_u32(tile_cnt, tile_start, tpart, (size_t)T, true, st));
-            LSR_HIP(launch_publish_total(tpart + tnb, tile_start + T, hs.dev, seq, st));
+            LSR_HIP(launch_publish_total(tpart + tnb, tile_start + T, hs.dev, seq, cls_cnt, st));
         }
     } else {
         uint64_t* gpart = (uint64_t*)(geom + GL.scan_part);
@@ -419,7 +421,7 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
         StageScope sc(ST_SCAN, st);
         LSR_HIP(launch_scan_u32((const uint32_t*)(geom + GL.tiles), (uint32_t*)(geom + GL.offsets), gpart,
                                 (size_t)P, false, st));
-        LSR_HIP(launch_publish_total(gpart + gnb, nullptr, hs.dev, seq, st));
+        LSR_HIP(launch_publish_total(gpart + gnb, nullptr, hs.dev, seq, nullptr, st));
     }
     // speculative binning workspace sized from the previous call's M, taken
     // while the GPU is still counting, so the host usually has nothing but
@@ -439,6 +441,10 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     if (M >= 0xffffffffull) return LSR_EOVERFLOW;
     out->num_rendered = (int64_t)M;
     hs.last_m = M;
+    // the privatised path published the tile-sort class counts with M
+    uint32_t host_cls[SORT_NCLS];
+    if (priv)
+        for (int k = 0; k < SORT_NCLS; k++) host_cls[k] = ((volatile uint32_t*)(hs.word + 1))[k];
 
     // 3. binning workspace + scatter into tile buckets
     const BinLayout BL = bin_layout((size_t)M);
@@ -471,7 +477,8 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     LSR_DEBUG_SYNC(s, st, "scatter");
     {
         StageScope sc(ST_SORT, st);
-        LSR_HIP(launch_tile_sort(T, tile_start, (uint64_t*)(bin + BL.keys), (uint32_t*)(bin + BL.point_list), st));
+        LSR_HIP(launch_tile_sort(T, tile_start, (uint64_t*)(bin + BL.keys), (uint32_t*)(bin + BL.point_list), cls_cnt,
+                                 cls_list, priv ? host_cls : nullptr, st));
     }
     LSR_DEBUG_SYNC(s, st, "tile_sort");
 

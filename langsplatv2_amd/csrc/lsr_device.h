@@ -313,7 +313,7 @@ __host__ __device__ inline GeomLayout geom_layout(size_t N)
 
 // Image workspace (per pixel + per tile).
 struct ImageLayout {
-    size_t final_T, n_contrib, tile_cnt, tile_start, tile_part, total;
+    size_t final_T, n_contrib, tile_cnt, tile_start, tile_part, cls_cnt, cls_list, total;
 };
 
 __host__ __device__ inline ImageLayout image_layout(size_t P, size_t T)
@@ -325,6 +325,8 @@ __host__ __device__ inline ImageLayout image_layout(size_t P, size_t T)
     L.tile_cnt = o;   o += align256(T * 4);
     L.tile_start = o; o += align256((T + 1) * 4);   // exclusive scan, [T] = num_rendered
     L.tile_part = o;  o += align256(((T + 4095) / 4096 + 1) * 8);
+    L.cls_cnt = o;    o += 256;                        // per-class tile counts (tile-sort classes)
+    L.cls_list = o;   o += align256(T * 6 * 4);        // per-class tile lists, T slots each
     L.total = o;
     return L;
 }

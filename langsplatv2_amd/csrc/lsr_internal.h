@@ -29,19 +29,24 @@ hipError_t launch_mark_visible(int P, const float* means, const float* view, uin
 // to part[0] (part must hold scan_partials(n) uint64 entries).
 size_t scan_partials(size_t n);
 hipError_t launch_scan_u32(const uint32_t* in, uint32_t* out, uint64_t* part, size_t n, bool exclusive, hipStream_t st);
+// Tile-sort size classes (binning.hip tile_class); their per-class tile counts
+// and lists live in the image workspace (cls_cnt, cls_list).
+#define SORT_NCLS 6
 hipError_t launch_publish_total(const uint64_t* total, uint32_t* tile_end, uint64_t* host_slot, uint32_t seq,
-                                hipStream_t st);
+                                const uint32_t* cls_cnt, hipStream_t st);
 hipError_t launch_duplicate(const Cam& c, int P, const uint8_t* geom, const int32_t* radii, uint32_t* tile_cnt,
                             uint32_t* rank, hipStream_t st);
 hipError_t launch_scatter(const Cam& c, int P, const uint8_t* geom, const int32_t* radii, const uint32_t* tile_start,
                           const uint32_t* rank, uint64_t* keys, hipStream_t st);
-int bin_blocks(int P, int T, int& chunk);
-bool bin_privatised_ok(int T);
+int bin_blocks(int P, const Cam& c, int& chunk);
+bool bin_privatised_ok(const Cam& c);
 hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t* geom, const int32_t* radii,
-                            uint32_t* table, uint32_t* tile_cnt, hipStream_t st);
+                            uint32_t* table, uint32_t* tile_cnt, uint32_t* cls_cnt, uint32_t* cls_list,
+                            hipStream_t st);
 hipError_t launch_bin_scatter(const Cam& c, int P, int chunk, int B, const uint8_t* geom, const int32_t* radii,
                               const uint32_t* table, const uint32_t* tile_start, uint64_t* keys, hipStream_t st);
-hipError_t launch_tile_sort(int T, const uint32_t* tile_start, uint64_t* keys, uint32_t* point_list, hipStream_t st);
+hipError_t launch_tile_sort(int T, const uint32_t* tile_start, uint64_t* keys, uint32_t* point_list,
+                            uint32_t* cls_cnt, uint32_t* cls_list, const uint32_t* host_cnt, hipStream_t st);
 
 // render.hip
 struct RenderArgs {
