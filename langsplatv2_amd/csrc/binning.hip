@@ -18,6 +18,9 @@
 
 #include <algorithm>
 
+#ifndef LSR_SCATTER_PROBE
+#define LSR_SCATTER_PROBE 0
+#endif
 #ifndef LSR_SORT_DPP
 #define LSR_SORT_DPP 1
 #endif
@@ -283,27 +286,141 @@ struct Band {
     }
 };
 
+// Load-balanced rect expansion.  Lane l of a wave owns Gaussian i0 + l with
+// n_l instances (its tile rect clipped to the band); the wave's instances are
+// numbered by an exclusive scan of n_l and handed out 64 at a time, each lane
+// finding its owner by binary search over the scan in LDS.  Every lane does
+// one instance per step however unequal the rects are (a per-lane rect loop
+// runs as long as the wave's largest rect: ~10x the mean here).
+struct WaveRects {
+    int pre[65];   // exclusive scan; pre[64] = total
+    int x0[64], y0[64], w[64];
+    uint64_t key[64];
+};
+
+// Wave-uniform: stage the lanes' rects, return the wave's instance total.
+__device__ __forceinline__ int wave_rects_stage(WaveRects& wr, int n, int x0, int y0, int w)
+{
+    const int lane = threadIdx.x & 63;
+    int s = n;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(s, d, 64);
+        if (lane >= d) s += t;
+    }
+    wr.pre[lane] = s - n;
+    if (lane == 63) wr.pre[64] = s;
+    wr.x0[lane] = x0;
+    wr.y0[lane] = y0;
+    wr.w[lane] = w;
+    wave_lds_fence();
+    return __shfl(s, 63, 64);
+}
+
+// Instance k of the staged wave -> (owner lane, tile x, tile y).
+__device__ __forceinline__ int wave_rects_item(const WaveRects& wr, int k, int& x, int& y)
+{
+    int o = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1)
+        if (wr.pre[o + step] <= k) o += step;
+    const int local = k - wr.pre[o], w = wr.w[o];
+    // exact: (local + 0.5) / w is >= 0.5/w away from an integer, far more
+    // than the approximate reciprocal's error for w, local < 2^16
+    const int dy = (int)__fdividef((float)local + 0.5f, (float)w);
+    y = wr.y0[o] + dy;
+    x = wr.x0[o] + (local - dy * w);
+    return o;
+}
+
+// Contiguous split of the staged instances: lane l takes [l*q, l*q + q),
+// q = ceil(total / 64); one owner search, then a walk along the rects (LDS
+// reads only when the walk crosses into the next owner).
+#ifndef LSR_BIN_WALK
+#define LSR_BIN_WALK 1
+#endif
+struct RectWalk {
+    int o, x, y, xs, xe, left;
+    __device__ __forceinline__ RectWalk(const WaveRects& wr, int k)
+    {
+        o = wave_rects_item(wr, k, x, y);
+        xs = wr.x0[o];
+        xe = xs + wr.w[o];
+        left = wr.pre[o + 1] - k;
+    }
+    // advance to the next instance (the caller guarantees there is one)
+    __device__ __forceinline__ void next(const WaveRects& wr)
+    {
+        if (--left > 0) {
+            if (++x == xe) {
+                x = xs;
+                ++y;
+            }
+            return;
+        }
+        do { ++o; } while (wr.pre[o + 1] == wr.pre[o]);
+        xs = x = wr.x0[o];
+        xe = xs + wr.w[o];
+        y = wr.y0[o];
+        left = wr.pre[o + 1] - wr.pre[o];
+    }
+};
+
+// Lane's Gaussian -> its rect clipped to the band (n = 0 if none).
+__device__ __forceinline__ int band_rect(const Cam& c, const Band& bd, const uint8_t* geom, int P, int g1,
+                                         const int32_t* __restrict__ radii, int i, int& x0, int& y0, int& w)
+{
+    x0 = y0 = w = 0;
+    if (i >= g1) return 0;
+    const int r = radii[i];
+    if (r <= 0) return 0;
+    int x1, y1;
+    bin_rect(c, geom, P, i, r, x0, y0, x1, y1);
+    y0 = max(y0, bd.ty0);
+    y1 = min(y1, bd.ty1);
+    w = x1 - x0;
+    return (y1 > y0 && w > 0) ? w * (y1 - y0) : 0;
+}
+
 __global__ void __launch_bounds__(BIN_BLOCK) k_bin_count(Cam c, int P, int chunk, int rows,
                                                          const uint8_t* __restrict__ geom,
                                                          const int32_t* __restrict__ radii, uint32_t* __restrict__ table,
                                                          uint32_t* __restrict__ cls_cnt)
 {
     extern __shared__ uint32_t hist[];
+    __shared__ WaveRects wrs[BIN_BLOCK / 64];
     const int T = c.gx * c.gy;
     const Band bd(c, rows);
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < SORT_NCLS) cls_cnt[threadIdx.x] = 0;   // k_bin_table appends after us
     for (int k = threadIdx.x; k < bd.nt; k += BIN_BLOCK) hist[k] = 0;
     __syncthreads();
+    WaveRects& wr = wrs[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63;
     const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
-    for (int i = g0 + threadIdx.x; i < g1; i += BIN_BLOCK) {
-        const int r = radii[i];
-        if (r <= 0) continue;
-        int x0, y0, x1, y1;
-        bin_rect(c, geom, P, i, r, x0, y0, x1, y1);
-        y0 = max(y0, bd.ty0);
-        y1 = min(y1, bd.ty1);
-        for (int y = y0; y < y1; y++)
-            for (int x = x0; x < x1; x++) atomicAdd(&hist[(y - bd.ty0) * c.gx + x], 1u);
+    for (int i0 = g0 + (threadIdx.x & ~63); i0 < g1; i0 += BIN_BLOCK) {
+        int x0, y0, w;
+        const int n = band_rect(c, bd, geom, P, g1, radii, i0 + lane, x0, y0, w);
+        const int tot = wave_rects_stage(wr, n, x0, y0 - bd.ty0, w);
+#if LSR_BIN_WALK
+        const int q = (tot + 63) >> 6;
+        int k = lane * q;
+        const int kend = min(tot, k + q);
+        if (k < kend) {
+            RectWalk rw(wr, k);
+            for (;;) {
+                atomicAdd(&hist[rw.y * c.gx + rw.x], 1u);
+                if (++k >= kend) break;
+                rw.next(wr);
+            }
+        }
+#else
+        for (int k = lane; k < tot; k += 64) {
+            int x, y;
+            wave_rects_item(wr, k, x, y);
+            atomicAdd(&hist[y * c.gx + x], 1u);
+        }
+#endif
+        wave_lds_fence();
     }
     __syncthreads();
     uint32_t* row = table + (size_t)blockIdx.x * T + bd.t0;
@@ -363,6 +480,7 @@ __global__ void __launch_bounds__(BIN_BLOCK) k_bin_scatter(Cam c, int P, int chu
                                                            uint64_t* __restrict__ keys)
 {
     extern __shared__ uint32_t base[];
+    __shared__ WaveRects wrs[BIN_BLOCK / 64];
     const int T = c.gx * c.gy;
     const Band bd(c, rows);
     const uint32_t* row = table + (size_t)blockIdx.x * T + bd.t0;
@@ -370,18 +488,64 @@ __global__ void __launch_bounds__(BIN_BLOCK) k_bin_scatter(Cam c, int P, int chu
     __syncthreads();
     const GeomLayout L = geom_layout(P);
     const float* depth = (const float*)(geom + L.depth);
+    WaveRects& wr = wrs[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63;
     const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
-    for (int i = g0 + threadIdx.x; i < g1; i += BIN_BLOCK) {
-        const int r = radii[i];
-        if (r <= 0) continue;
-        int x0, y0, x1, y1;
-        bin_rect(c, geom, P, i, r, x0, y0, x1, y1);
-        y0 = max(y0, bd.ty0);
-        y1 = min(y1, bd.ty1);
-        if (y0 >= y1) continue;
-        const uint64_t key = ((uint64_t)__float_as_uint(depth[i]) << 32) | (uint32_t)i;
-        for (int y = y0; y < y1; y++)
-            for (int x = x0; x < x1; x++) keys[atomicAdd(&base[(y - bd.ty0) * c.gx + x], 1u)] = key;
+    for (int i0 = g0 + (threadIdx.x & ~63); i0 < g1; i0 += BIN_BLOCK) {
+        const int i = i0 + lane;
+        int x0, y0, w;
+        const int n = band_rect(c, bd, geom, P, g1, radii, i, x0, y0, w);
+        if (n > 0) wr.key[lane] = ((uint64_t)__float_as_uint(depth[i]) << 32) | (uint32_t)i;
+        const int tot = wave_rects_stage(wr, n, x0, y0 - bd.ty0, w);
+#if LSR_BIN_WALK
+        const int q = (tot + 63) >> 6;
+        int k = lane * q;
+        const int kend = min(tot, k + q);
+        if (k < kend) {
+            RectWalk rw(wr, k);
+            // two instances per step: both LDS-atomic returns in flight
+            for (;;) {
+                const uint32_t sa = atomicAdd(&base[rw.y * c.gx + rw.x], 1u);
+                const uint64_t ka = wr.key[rw.o];
+                const bool two = k + 1 < kend;
+                uint32_t sb = 0;
+                uint64_t kb = 0;
+                if (two) {
+                    rw.next(wr);
+                    sb = atomicAdd(&base[rw.y * c.gx + rw.x], 1u);
+                    kb = wr.key[rw.o];
+                }
+#if LSR_SCATTER_PROBE
+                if (sa == 0xffffffffu) keys[0] = ka;
+                if (two && sb == 0xffffffffu) keys[0] = kb;
+#else
+                keys[sa] = ka;
+                if (two) keys[sb] = kb;
+#endif
+                k += 2;
+                if (k >= kend) break;
+                rw.next(wr);
+            }
+        }
+#else
+        // two instances per lane per step: both LDS-atomic returns in flight
+        for (int k = lane; k < tot; k += 128) {
+            const bool two = k + 64 < tot;
+            int xa, ya, xb = 0, yb = 0;
+            const int oa = wave_rects_item(wr, k, xa, ya);
+            const int ob = two ? wave_rects_item(wr, k + 64, xb, yb) : 0;
+            const uint32_t sa = atomicAdd(&base[ya * c.gx + xa], 1u);
+            const uint32_t sb = two ? atomicAdd(&base[yb * c.gx + xb], 1u) : 0u;
+#if LSR_SCATTER_PROBE   // measurement only: atomics without the scattered stores
+            if (sa == 0xffffffffu) keys[0] = wr.key[oa];
+            if (two && sb == 0xffffffffu) keys[0] = wr.key[ob];
+#else
+            keys[sa] = wr.key[oa];
+            if (two) keys[sb] = wr.key[ob];
+#endif
+        }
+#endif
+        wave_lds_fence();
     }
 }
 

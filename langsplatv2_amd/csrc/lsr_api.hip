@@ -455,6 +455,11 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     }
     out->binning = bin;
     out->binning_bytes = bin_cap;
+#if LSR_SCATTER_PROBE
+    // measurement build: the probe scatter stores no keys, so give the sort
+    // and the render valid ids (all 0)
+    if (priv) LSR_HIP(hipMemsetAsync(bin + BL.keys, 0, (size_t)M * 8, st));
+#endif
     if (priv) {
         StageScope sc(ST_SCATTER, st);
         LSR_HIP(launch_bin_scatter(c, P, chunk, B, geom, out->radii, table, tile_start, (uint64_t*)(bin + BL.keys),

@@ -47,6 +47,11 @@ __device__ __forceinline__ float expf_det(float x)
 __device__ __forceinline__ uint64_t wave_ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
 __device__ __forceinline__ bool wave_any(bool b) { return __builtin_amdgcn_ballot_w64(b) != 0; }
 
+// Wait for the wave's outstanding LDS operations; the memory clobber keeps
+// the compiler from moving LDS accesses across it (wave-private LDS staging
+// needs no workgroup barrier).
+__device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 // float -> int truncating + saturating; NaN -> 0 (matches oracle f2i).
 __device__ __forceinline__ int f2i(float v)
 {

@@ -265,7 +265,6 @@ struct WaveStage {
     int pos[64];
 };
 
-__device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // Stage the candidates of one chunk: lane l holds instance (gid, A, B, pos) if
 // valid; instances that may touch the wave's 8x8 block are compacted (order

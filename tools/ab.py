@@ -15,8 +15,9 @@ import bench  # noqa: E402
 
 variants = [a.split("=", 1) for a in sys.argv[1:]]
 libs = {name: _lib.load(path) for name, path in variants}
-cfg = CONFIGS[3]
+cfg = CONFIGS[int(os.environ.get("LSR_CFG", "3"))]
 D = int(os.environ.get("LSR_D", cfg["lang_dim"]))
+FWD_ONLY = not cfg["backward"]
 dev = torch.device("cuda:0")
 cam = make_camera(cfg["W"], cfg["H"])
 g0 = make_gaussians(cfg["N"], cam, seed=0, sh_degree=3, lang_dim=D)
@@ -35,10 +36,12 @@ def run(lib, steps):
     for _ in range(steps):
         for p in g.values():
             p.grad = None
-        c, l, _ = r(means3D=g["means3D"], means2D=g["means2D"], opacities=g["opacities"], shs=g["shs"],
-                    language_feature_precomp=g["language_feature_precomp"], scales=g["scales"],
-                    rotations=g["rotations"])
-        torch.autograd.backward([c, l], [dc, dl])
+        with torch.set_grad_enabled(not FWD_ONLY):
+            c, l, _ = r(means3D=g["means3D"], means2D=g["means2D"], opacities=g["opacities"], shs=g["shs"],
+                        language_feature_precomp=g["language_feature_precomp"], scales=g["scales"],
+                        rotations=g["rotations"])
+        if not FWD_ONLY:
+            torch.autograd.backward([c, l], [dc, dl])
     torch.cuda.synchronize()
     lib.lsr_profile_enable(0)
     q = _lib.profile_query()
