@@ -100,7 +100,7 @@ typedef struct lsr_inputs {
  * the last pointer returned for a kind is the one the call uses. */
 typedef void* (*lsr_alloc_fn)(void* ctx, size_t bytes, int which);
 enum { LSR_BUF_GEOM = 0, LSR_BUF_BINNING = 1, LSR_BUF_IMAGE = 2, LSR_BUF_GRAD = 3, LSR_BUF_DECODE = 4,
-       LSR_BUF_KNN = 5 };
+       LSR_BUF_KNN = 5, LSR_BUF_LOSS = 6 };
 
 typedef struct lsr_fwd_out {
     float* out_color;     /* (3,H,W)  caller-allocated */
@@ -181,6 +181,28 @@ int lsr_topk_code_forward(const float* logits, int64_t N, int L, int K, int k, f
  * softmax_to_topk_soft_code (mask recomputed from the logits). */
 int lsr_topk_code_backward(const float* logits, const float* grad_dense, int64_t N, int L, int K, int k,
                            float* grad_logits, void* stream);
+
+/* Language-feature cosine loss of the feature-mode training step (SURVEY
+ * §8f rank 4; train.py:151-164 with vq_layer_num = 1, layer_idx = 0):
+ *   f[:, p]  = codebooks[0]^T w_p        compute_layer_feature_map,
+ *                                        scene/gaussian_model.py:533-543
+ *   gt[:, p] = features[seg[p]], mask[p] = seg[p] != -1
+ *                                        get_language_feature, scene/cameras.py:59-96
+ *   loss     = 1 - mean_p cos(f_p*mask_p, gt_p*mask_p)   cos_loss,
+ *                                        utils/loss_utils.py:24-25 (eps 1e-8)
+ * weight_map (K, H, W), codebooks (K, Df), features (S, Df) fp32; seg (H, W)
+ * int32 segment ids, -1 (or any id outside [0, S)) = masked.  K must be 64.
+ * Nothing of size Df x pixels is materialised (everything factors through
+ * the K-dim code space).  Forward writes loss[0].  Backward writes
+ * grad_weight_map (K, H, W) and grad_codebooks (K, Df), both scaled by the
+ * device scalar *grad_loss.  Workspace via alloc (LSR_BUF_LOSS). */
+int lsr_lang_loss_forward(const float* weight_map, const float* codebooks, int K, int Df, int H, int W,
+                          const int32_t* seg, const float* features, int S, float* loss, lsr_alloc_fn alloc,
+                          void* alloc_ctx, void* stream);
+int lsr_lang_loss_backward(const float* weight_map, const float* codebooks, int K, int Df, int H, int W,
+                           const int32_t* seg, const float* features, int S, const float* grad_loss,
+                           float* grad_weight_map, float* grad_codebooks, lsr_alloc_fn alloc, void* alloc_ctx,
+                           void* stream);
 
 /* simple_knn._C.distCUDA2 (scene/gaussian_model.py:20,194): for points
  * (N, 3) fp32, out[i] = mean of the three smallest squared distances

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSR_LIB", os.path.join(_HERE, "liblsr.so"))
 
 LSR_OK = 0
-LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_GRAD, LSR_BUF_DECODE, LSR_BUF_KNN = 0, 1, 2, 3, 4, 5
+LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_GRAD, LSR_BUF_DECODE, LSR_BUF_KNN, LSR_BUF_LOSS = 0, 1, 2, 3, 4, 5, 6
 LSR_INDEX_F32, LSR_INDEX_I32, LSR_INDEX_I64 = 0, 1, 2
 
 _vp = ctypes.c_void_p
@@ -104,7 +104,7 @@ class BwdOut(ctypes.Structure):
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
 
 EXPORTS = ("lsr_forward", "lsr_backward", "lsr_mark_visible", "lsr_quick_decode", "lsr_topk_code_forward",
-           "lsr_topk_code_backward", "lsr_knn_dist2", "lsr_strerror",
+           "lsr_topk_code_backward", "lsr_knn_dist2", "lsr_lang_loss_forward", "lsr_lang_loss_backward", "lsr_strerror",
            "lsr_abi_version", "lsr_max_lang_dim", "lsr_profile_enable", "lsr_profile_stages", "lsr_profile_reset",
            "lsr_profile_query")
 
@@ -142,6 +142,12 @@ def load(path: str | None = None):
     lib.lsr_topk_code_backward.restype = ctypes.c_int
     lib.lsr_knn_dist2.argtypes = [_vp, ctypes.c_int64, _vp, ALLOC_FN, _vp, _vp]
     lib.lsr_knn_dist2.restype = ctypes.c_int
+    _ci = ctypes.c_int
+    lib.lsr_lang_loss_forward.argtypes = [_vp, _vp, _ci, _ci, _ci, _ci, _vp, _vp, _ci, _vp, ALLOC_FN, _vp, _vp]
+    lib.lsr_lang_loss_forward.restype = ctypes.c_int
+    lib.lsr_lang_loss_backward.argtypes = [_vp, _vp, _ci, _ci, _ci, _ci, _vp, _vp, _ci, _vp, _vp, _vp, ALLOC_FN,
+                                           _vp, _vp]
+    lib.lsr_lang_loss_backward.restype = ctypes.c_int
     lib.lsr_strerror.argtypes = [ctypes.c_int]
     lib.lsr_strerror.restype = ctypes.c_char_p
     lib.lsr_abi_version.restype = ctypes.c_int

@@ -91,4 +91,11 @@ hipError_t launch_knn_dist2(const float* points, int64_t N, float* out, uint8_t*
 hipError_t launch_quick_decode(const float* wmap, const float* cb, int L, int K, int Df, int H, int W, int normalize,
                                float eps, float* G, float* out, hipStream_t st);
 
+// lang_loss.hip
+size_t lang_loss_workspace_bytes(int S, int W, int H, int* waves);
+// gw == nullptr: loss only; else dL/dweight_map and dL/dcodebooks scaled by *gscale
+hipError_t launch_lang_loss(const float* wmap, const float* cb, int Df, int H, int W, const int32_t* seg,
+                            const float* feat, int S, const float* gscale, float* loss, float* gw, float* dcb,
+                            float* ws, hipStream_t st);
+
 }  // namespace lsr

@@ -316,3 +316,42 @@ def topk_soft_code_backward(logits: np.ndarray, grad: np.ndarray, k: int, levels
         dy = np.where(m, gz, 0.0)
         out[:, sl] = y * (dy - (dy * y).sum(axis=1, keepdims=True))
     return out
+
+
+def lang_cos_loss(weight_map: np.ndarray, codebook: np.ndarray, seg: np.ndarray, features: np.ndarray,
+                  eps: float = 1e-8):
+    """The feature-mode training loss, materialised as the reference does it
+    (float64): f = codebook.T @ W (compute_layer_feature_map, layer 0,
+    scene/gaussian_model.py:533-543), gt[:, p] = features[seg[p]] with mask
+    seg != -1 (get_language_feature, scene/cameras.py:77-94), loss =
+    cos_loss(f*mask, gt*mask) = 1 - mean_p x.y / (max|x|,eps max|y|,eps)
+    (utils/loss_utils.py:24-25; torch cosine_similarity semantics).  Ids
+    outside [0, S) are masked.  Returns (loss, dL/dW (K, H, W), dL/dcodebook
+    (K, Df)) with the gradients differentiated directly in the Df-dim space
+    (the GPU kernel factorises through the code space instead)."""
+    Wm = np.asarray(weight_map, np.float64)
+    cb = np.asarray(codebook, np.float64)
+    F = np.asarray(features, np.float64)
+    K, H, W = Wm.shape
+    P = H * W
+    w = Wm.reshape(K, P)
+    s = np.asarray(seg).reshape(P).astype(np.int64)
+    m = (s >= 0) & (s < F.shape[0])
+    f = cb.T @ w                                          # (Df, P)
+    gt = np.zeros_like(f)
+    gt[:, m] = F[s[m]].T
+    x = f * m
+    y = gt * m
+    nx = np.sqrt((x * x).sum(0))
+    ny = np.sqrt((y * y).sum(0))
+    Nx, Ny = np.maximum(nx, eps), np.maximum(ny, eps)
+    dot = (x * y).sum(0)
+    cos = dot / (Nx * Ny)
+    loss = 1.0 - cos.mean()
+    # d(-mean cos)/dx, then through the mask and f = cb^T w
+    live = nx > eps
+    dcos_dx = y / (Nx * Ny) - np.where(live, dot / (np.where(live, nx, 1.0) ** 3 * Ny), 0.0) * x
+    gx = -dcos_dx / P * m
+    dW = (cb @ gx).reshape(K, H, W)
+    dcb = w @ gx.T
+    return loss, dW, dcb
