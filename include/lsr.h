@@ -191,18 +191,20 @@ int lsr_topk_code_backward(const float* logits, const float* grad_dense, int64_t
  *   loss     = 1 - mean_p cos(f_p*mask_p, gt_p*mask_p)   cos_loss,
  *                                        utils/loss_utils.py:24-25 (eps 1e-8)
  * weight_map (K, H, W), codebooks (K, Df), features (S, Df) fp32; seg (H, W)
- * int32 segment ids, -1 (or any id outside [0, S)) = masked.  K must be 64.
- * Nothing of size Df x pixels is materialised (everything factors through
- * the K-dim code space).  Forward writes loss[0].  Backward writes
- * grad_weight_map (K, H, W) and grad_codebooks (K, Df), both scaled by the
- * device scalar *grad_loss.  Workspace via alloc (LSR_BUF_LOSS). */
+ * int32 segment ids, -1 (or any id outside [0, S)) = masked.  K must be 64,
+ * Df a multiple of 16.  Nothing of size Df x pixels is materialised
+ * (everything factors through the K-dim code space).  Forward writes loss[0]
+ * and/or pixel_stats (2, H, W) (|f_p| and f_p.gt_p; either may be NULL).
+ * Backward writes grad_weight_map (K, H, W) and grad_codebooks (K, Df), both
+ * scaled by the device scalar *grad_loss, from the forward's pixel_stats
+ * (NULL: recomputed).  Workspace via alloc (LSR_BUF_LOSS). */
 int lsr_lang_loss_forward(const float* weight_map, const float* codebooks, int K, int Df, int H, int W,
-                          const int32_t* seg, const float* features, int S, float* loss, lsr_alloc_fn alloc,
-                          void* alloc_ctx, void* stream);
+                          const int32_t* seg, const float* features, int S, float* loss, float* pixel_stats,
+                          lsr_alloc_fn alloc, void* alloc_ctx, void* stream);
 int lsr_lang_loss_backward(const float* weight_map, const float* codebooks, int K, int Df, int H, int W,
-                           const int32_t* seg, const float* features, int S, const float* grad_loss,
-                           float* grad_weight_map, float* grad_codebooks, lsr_alloc_fn alloc, void* alloc_ctx,
-                           void* stream);
+                           const int32_t* seg, const float* features, int S, const float* pixel_stats,
+                           const float* grad_loss, float* grad_weight_map, float* grad_codebooks, lsr_alloc_fn alloc,
+                           void* alloc_ctx, void* stream);
 
 /* simple_knn._C.distCUDA2 (scene/gaussian_model.py:20,194): for points
  * (N, 3) fp32, out[i] = mean of the three smallest squared distances

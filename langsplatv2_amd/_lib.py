@@ -143,10 +143,10 @@ def load(path: str | None = None):
     lib.lsr_knn_dist2.argtypes = [_vp, ctypes.c_int64, _vp, ALLOC_FN, _vp, _vp]
     lib.lsr_knn_dist2.restype = ctypes.c_int
     _ci = ctypes.c_int
-    lib.lsr_lang_loss_forward.argtypes = [_vp, _vp, _ci, _ci, _ci, _ci, _vp, _vp, _ci, _vp, ALLOC_FN, _vp, _vp]
+    lib.lsr_lang_loss_forward.argtypes = [_vp, _vp, _ci, _ci, _ci, _ci, _vp, _vp, _ci, _vp, _vp, ALLOC_FN, _vp, _vp]
     lib.lsr_lang_loss_forward.restype = ctypes.c_int
-    lib.lsr_lang_loss_backward.argtypes = [_vp, _vp, _ci, _ci, _ci, _ci, _vp, _vp, _ci, _vp, _vp, _vp, ALLOC_FN,
-                                           _vp, _vp]
+    lib.lsr_lang_loss_backward.argtypes = [_vp, _vp, _ci, _ci, _ci, _ci, _vp, _vp, _ci, _vp, _vp, _vp, _vp,
+                                           ALLOC_FN, _vp, _vp]
     lib.lsr_lang_loss_backward.restype = ctypes.c_int
     lib.lsr_strerror.argtypes = [ctypes.c_int]
     lib.lsr_strerror.restype = ctypes.c_char_p

@@ -213,30 +213,30 @@ static int lang_loss_args(const float* wm, const float* cb, int K, int Df, int H
                           const float* feat, int S)
 {
     if (K <= 0 || Df <= 0 || H <= 0 || W <= 0 || S < 0) return LSR_EINVAL;
-    if (K != 64) return LSR_EUNSUPPORTED;
+    if (K != 64 || (Df % 16) != 0) return LSR_EUNSUPPORTED;
     if (!wm || !cb || !seg || (S > 0 && !feat)) return LSR_EINVAL;
     return LSR_OK;
 }
 
 int lsr_lang_loss_forward(const float* weight_map, const float* codebooks, int K, int Df, int H, int W,
-                          const int32_t* seg, const float* features, int S, float* loss, lsr_alloc_fn alloc,
-                          void* alloc_ctx, void* stream)
+                          const int32_t* seg, const float* features, int S, float* loss, float* pixel_stats,
+                          lsr_alloc_fn alloc, void* alloc_ctx, void* stream)
 {
     const int rc = lang_loss_args(weight_map, codebooks, K, Df, H, W, seg, features, S);
     if (rc != LSR_OK) return rc;
-    if (!loss || !alloc) return LSR_EINVAL;
+    if ((!loss && !pixel_stats) || !alloc) return LSR_EINVAL;
     float* ws = (float*)alloc(alloc_ctx, lsr::lang_loss_workspace_bytes(S, W, H, nullptr), LSR_BUF_LOSS);
     if (!ws) return LSR_ENOMEM;
     if (lsr::launch_lang_loss(weight_map, codebooks, Df, H, W, seg, features, S, nullptr, loss, nullptr, nullptr,
-                              ws, (hipStream_t)stream) != hipSuccess)
+                              pixel_stats, ws, (hipStream_t)stream) != hipSuccess)
         return LSR_EHIP;
     return LSR_OK;
 }
 
 int lsr_lang_loss_backward(const float* weight_map, const float* codebooks, int K, int Df, int H, int W,
-                           const int32_t* seg, const float* features, int S, const float* grad_loss,
-                           float* grad_weight_map, float* grad_codebooks, lsr_alloc_fn alloc, void* alloc_ctx,
-                           void* stream)
+                           const int32_t* seg, const float* features, int S, const float* pixel_stats,
+                           const float* grad_loss, float* grad_weight_map, float* grad_codebooks, lsr_alloc_fn alloc,
+                           void* alloc_ctx, void* stream)
 {
     const int rc = lang_loss_args(weight_map, codebooks, K, Df, H, W, seg, features, S);
     if (rc != LSR_OK) return rc;
@@ -244,7 +244,8 @@ int lsr_lang_loss_backward(const float* weight_map, const float* codebooks, int 
     float* ws = (float*)alloc(alloc_ctx, lsr::lang_loss_workspace_bytes(S, W, H, nullptr), LSR_BUF_LOSS);
     if (!ws) return LSR_ENOMEM;
     if (lsr::launch_lang_loss(weight_map, codebooks, Df, H, W, seg, features, S, grad_loss, nullptr,
-                              grad_weight_map, grad_codebooks, ws, (hipStream_t)stream) != hipSuccess)
+                              grad_weight_map, grad_codebooks, const_cast<float*>(pixel_stats), ws,
+                              (hipStream_t)stream) != hipSuccess)
         return LSR_EHIP;
     return LSR_OK;
 }

@@ -93,9 +93,11 @@ hipError_t launch_quick_decode(const float* wmap, const float* cb, int L, int K,
 
 // lang_loss.hip
 size_t lang_loss_workspace_bytes(int S, int W, int H, int* waves);
-// gw == nullptr: loss only; else dL/dweight_map and dL/dcodebooks scaled by *gscale
+// gw == nullptr: forward (loss and/or the per-pixel stats (2, H, W));
+// else dL/dweight_map and dL/dcodebooks scaled by *gscale, from the
+// forward's stats (recomputed when stats == nullptr)
 hipError_t launch_lang_loss(const float* wmap, const float* cb, int Df, int H, int W, const int32_t* seg,
                             const float* feat, int S, const float* gscale, float* loss, float* gw, float* dcb,
-                            float* ws, hipStream_t st);
+                            float* stats, float* ws, hipStream_t st);
 
 }  // namespace lsr

@@ -48,8 +48,8 @@ def _args(weight_map, codebooks, seg, features):
     K, H, W = weight_map.shape
     if cb.shape[0] != K:
         raise ValueError(f"language_cos_loss: weight_map has {K} channels, the codebook {cb.shape[0]} codes")
-    if K != 64:
-        raise ValueError("language_cos_loss: K must be 64 (codebook_size of train.sh)")
+    if K != 64 or cb.shape[1] % 16:
+        raise ValueError("language_cos_loss: K must be 64 (codebook_size of train.sh) and Df a multiple of 16")
     if tuple(seg.shape) != (H, W):
         raise ValueError(f"language_cos_loss: seg must be (H, W) = {(H, W)}, got {tuple(seg.shape)}")
     if features.dim() != 2 or features.shape[1] != cb.shape[1]:
@@ -66,25 +66,27 @@ class _LanguageCosLoss(torch.autograd.Function):
     def forward(ctx, weight_map, codebooks, seg, features):
         wm, cb, sg, ft, K, H, W = _args(weight_map, codebooks, seg, features)
         loss = torch.empty((1,), dtype=torch.float32, device=wm.device)
+        stats = torch.empty((2, H, W), dtype=torch.float32, device=wm.device)   # |f_p|, f_p.gt_p
         alloc = _Alloc(wm.device)
         _lib.check(_lib.load().lsr_lang_loss_forward(wm.data_ptr(), cb.data_ptr(), K, cb.shape[1], H, W,
                                                      sg.data_ptr(), ft.data_ptr(), ft.shape[0], loss.data_ptr(),
-                                                     alloc.fn, None, _stream(wm.device)), "lsr_lang_loss_forward")
-        ctx.save_for_backward(wm, cb, sg, ft)
+                                                     stats.data_ptr(), alloc.fn, None, _stream(wm.device)),
+                   "lsr_lang_loss_forward")
+        ctx.save_for_backward(wm, cb, sg, ft, stats)
         ctx.cb_shape = tuple(codebooks.shape)
         return loss[0]
 
     @staticmethod
     def backward(ctx, grad):
-        wm, cb, sg, ft = ctx.saved_tensors
+        wm, cb, sg, ft, stats = ctx.saved_tensors
         K, H, W = wm.shape
         g = grad.detach().reshape(1).contiguous().float()
         gw = torch.empty_like(wm)
         gcb = torch.empty_like(cb)
         alloc = _Alloc(wm.device)
         _lib.check(_lib.load().lsr_lang_loss_backward(wm.data_ptr(), cb.data_ptr(), K, cb.shape[1], H, W,
-                                                      sg.data_ptr(), ft.data_ptr(), ft.shape[0], g.data_ptr(),
-                                                      gw.data_ptr(), gcb.data_ptr(), alloc.fn, None,
+                                                      sg.data_ptr(), ft.data_ptr(), ft.shape[0], stats.data_ptr(),
+                                                      g.data_ptr(), gw.data_ptr(), gcb.data_ptr(), alloc.fn, None,
                                                       _stream(wm.device)), "lsr_lang_loss_backward")
         if len(ctx.cb_shape) == 3:   # layers > 0 take no part at layer_idx 0
             full = torch.zeros(ctx.cb_shape, dtype=gcb.dtype, device=gcb.device)
