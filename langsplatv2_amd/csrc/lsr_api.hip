@@ -550,6 +550,28 @@ int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* 
     hipStream_t st = (hipStream_t)stream;
     const Cam c = make_cam(s);
     const int P = in->P;
+    // Only dL/dlanguage requested (feature-mode training with frozen geometry
+    // and no means2D gradient): the language-only render backward writes the
+    // output directly; no gradient rows, no preprocess backward.
+    const bool lang_only = Dd > 0 && out->dL_dlang && !out->dL_dmeans2D && !out->dL_dcolors && !out->dL_dopacity &&
+                           !out->dL_dmeans3D && !out->dL_dcov3D && !out->dL_dsh && !out->dL_dscales &&
+                           !out->dL_drotations;
+    if (lang_only) {
+        RenderBwdArgs rb;
+        rb.f = make_render_args(s, in, c, (const uint8_t*)b->geom, (const uint8_t*)b->binning,
+                                (const uint8_t*)b->image, b->num_rendered);
+        rb.f.qw = nullptr;
+        rb.f.D = Dd;
+        rb.f.lang = in->language_feature_precomp;
+        rb.dout_color = b->dL_dout_color;
+        rb.dout_lang = b->dL_dout_lang;
+        rb.grad_acc = out->dL_dlang;
+        rb.VP = Dd;
+        { StageScope sc(ST_GZERO, st); LSR_HIP(hipMemsetAsync(out->dL_dlang, 0, (size_t)P * Dd * 4, st)); }
+        { StageScope sc(ST_RENDER_BWD, st); LSR_HIP(launch_render_bwd_lang(rb, st)); }
+        LSR_DEBUG_SYNC(s, st, "render_bwd_lang");
+        return LSR_OK;
+    }
     const int VP = grad_row_width(Dd);
     float* gacc = (float*)alloc(ctx, (size_t)P * VP * 4, LSR_BUF_GRAD);
     if (!gacc) return LSR_ENOMEM;

@@ -78,6 +78,9 @@ struct RenderBwdArgs {
 };
 int grad_row_width(int D);   // VP for a dense language dim
 hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t st);
+// language-only backward: grad_acc is the (P, D) dL/dlanguage output itself
+// (zeroed by the caller), VP = D
+hipError_t launch_render_bwd_lang(const RenderBwdArgs& a, hipStream_t st);
 int lang_set_for(int D);     // compiled channel set >= D, or -1
 
 // quick.hip

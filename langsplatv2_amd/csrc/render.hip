@@ -1050,9 +1050,15 @@ __device__ __forceinline__ float feature_at(const RenderArgs& a, uint32_t gid, i
 #else
 #define BWD_MFMA(a, b_, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b_), (c), 0, 0, 0)
 #endif
-template <int NL>
+// LO (language only): the autograd call needs dL/dlanguage alone (feature-mode
+// training: geometry frozen, scene/gaussian_model.py:238-243, and means2D not
+// requiring grad).  Then dL/dlang[j][c] = sum_p aT[j][p] dL/dout[c][p] is all
+// that is left: no dot products, no dL/dalpha recurrence, no moments, and the
+// rows go straight into the (N, D) output (b.grad_acc, b.VP = D).
+template <int NL, bool LO = false>
 __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArgs b)
 {
+    static_assert(!LO || (LSR_BWD_VMOM && NL > 0), "language-only backward needs the VMOM layout and D > 0");
     using FR = BwdFrags<NL>;
     constexpr int KS = FR::KS;
 #if LSR_BWD_VMOM
@@ -1067,7 +1073,8 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #endif
     constexpr int GS = LSR_GRP_STRIDE;
     __shared__ WaveStageG st;
-    constexpr int GRL = (LSR_GROW_LANG + NL + 15) / 16;   // 16-float lines per gradient row
+    constexpr int GCOL0 = LO ? 0 : LSR_GROW_LANG;          // first language column of a staged row
+    constexpr int GRL = (GCOL0 + NL + 15) / 16;            // 16-float lines per gradient row
     constexpr int GRS = 16 * GRL + 4;                     // staged row stride
 #if LSR_BWD_ALIAS
     // The gradient-row tile and the moments are written only after phase 3
@@ -1115,17 +1122,20 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     }
 
     float dotB[KS][4], chB[NBA][16];
+    if constexpr (!LO) {
 #pragma unroll
-    for (int t = 0; t < KS; t++)
+        for (int t = 0; t < KS; t++)
 #pragma unroll
-        for (int pb = 0; pb < 4; pb++) dotB[t][pb] = gd_at<NL>(b, 4 * t + lg, pb * 16 + li, pm.bx, pm.by);
+            for (int pb = 0; pb < 4; pb++) dotB[t][pb] = gd_at<NL>(b, 4 * t + lg, pb * 16 + li, pm.bx, pm.by);
+    }
 #if LSR_BWD_VMOM
 #pragma unroll
     for (int nb = 0; nb < NBC; nb++)
 #pragma unroll
         for (int t = 0; t < 16; t++) chB[nb][t] = gd_at<NL>(b, 3 + nb * 16 + li, 4 * t + lg, pm.bx, pm.by);
-    sDrgb[lane] = make_float4(gd_at<NL>(b, 0, lane, pm.bx, pm.by), gd_at<NL>(b, 1, lane, pm.bx, pm.by),
-                              gd_at<NL>(b, 2, lane, pm.bx, pm.by), 0.f);
+    if constexpr (!LO)
+        sDrgb[lane] = make_float4(gd_at<NL>(b, 0, lane, pm.bx, pm.by), gd_at<NL>(b, 1, lane, pm.bx, pm.by),
+                                  gd_at<NL>(b, 2, lane, pm.bx, pm.by), 0.f);
     // block-centred x of the pixels this lane's fragments cover: columns lg
     // (even K-steps) and 4 + lg (odd K-steps)
     const float lxe = (float)lg - 3.5f, lxo = (float)lg + 0.5f;
@@ -1137,8 +1147,9 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
         for (int t = 0; t < 16; t++) chB[nb][t] = gd_at<NL>(b, nb * 16 + li, 4 * t + lg, pm.bx, pm.by);
 #endif
     const float bg0 = c.bg[0], bg1 = c.bg[1], bg2 = c.bg[2];
-    const float bg_dot = inside ? bg0 * b.dout_color[pix] + bg1 * b.dout_color[HW + pix] + bg2 * b.dout_color[2 * HW + pix]
-                                : 0.f;   // 0 with a black background: the term below is then exact 0
+    const float bg_dot = (inside && !LO)
+                             ? bg0 * b.dout_color[pix] + bg1 * b.dout_color[HW + pix] + bg2 * b.dout_color[2 * HW + pix]
+                             : 0.f;   // 0 with a black background: the term below is then exact 0
 
     const bool has_bg = (bg0 != 0.f) || (bg1 != 0.f) || (bg2 != 0.f);   // uniform
     float T = T_final;
@@ -1195,7 +1206,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #if LSR_BWD_AF_PF
             if (!af_ready)
 #endif
-            {
+            if constexpr (!LO) {
                 const uint32_t gi = st.gid[g0 + (li < kn ? li : 0)];
 #pragma unroll
                 for (int t = 0; t < KS; t++)
@@ -1233,7 +1244,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 }
             }
             // dot[k][p] of the group's candidates on MFMA: (16 x C) . (C x 64)
-            {
+            if constexpr (!LO) {
                 f32x4 acc[4];
 #pragma unroll
                 for (int pb = 0; pb < 4; pb++) acc[pb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1264,7 +1275,16 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             //   dL/dalpha_k = (dot_k - S) T_k,   S <- alpha_k dot_k + (1 - alpha_k) S
             // G = 0 marks a non-contributing pair: alpha = 0, rcp(1) = 1 and the
             // S update is an exact identity, so no selects are needed.
-            if (has_bg) {
+            if constexpr (LO) {
+                // transmittance only: aT_k = alpha_k T_k (T_k recovered back to front)
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const float G = sAT[k * GS + lane];
+                    const float al = fminf(0.99f, st.B[g0 + k].y * G);
+                    T = T * __builtin_amdgcn_rcpf(1.f - al);
+                    sAT[k * GS + lane] = al * T;
+                }
+            } else if (has_bg) {
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
                     const float G = sAT[k * GS + lane];
@@ -1305,6 +1325,14 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             float M0 = 0.f, M1 = 0.f, M2 = 0.f, M3 = 0.f, M4 = 0.f, M5 = 0.f;
             float C0 = 0.f, C1 = 0.f, C2 = 0.f;
             float ue = 0.f;
+            if constexpr (LO) {
+#pragma unroll
+                for (int t = 0; t < 16; t++) {
+                    const float aa = sAT[li * GS + 4 * t + lg];
+#pragma unroll
+                    for (int nb = 0; nb < NBC; nb++) ch[nb] = BWD_MFMA(aa, chB[nb][t], ch[nb]);
+                }
+            } else {
 #pragma unroll
             for (int t = 0; t < 16; t++) {
                 const float au = sDU[li * GS + 4 * t + lg];
@@ -1336,6 +1364,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             M0 += xor_f32<32>(M0); M1 += xor_f32<32>(M1); M2 += xor_f32<32>(M2);
             M3 += xor_f32<32>(M3); M4 += xor_f32<32>(M4); M5 += xor_f32<32>(M5);
             C0 += xor_f32<32>(C0); C1 += xor_f32<32>(C1); C2 += xor_f32<32>(C2);
+            }
             // Gradient rows of the group staged in LDS (row layout of lsr_device.h:
             // [0..5] geometry, [6..8] colour, [12..) language), then added with
             // line-coalesced atomics: each 16-lane group covers one 64-B line of
@@ -1345,10 +1374,10 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 const int chn = nb * 16 + li;
                 if (chn < NL) {
 #pragma unroll
-                    for (int r = 0; r < 4; r++) sGr[(4 * lg + r) * GRS + LSR_GROW_LANG + chn] = ch[nb][r];
+                    for (int r = 0; r < 4; r++) sGr[(4 * lg + r) * GRS + GCOL0 + chn] = ch[nb][r];
                 }
             }
-            if (lane < kn) {   // lane = candidate li (lg = 0)
+            if (!LO && lane < kn) {   // lane = candidate li (lg = 0)
                 const int j = g0 + lane;
                 const float4 A = st.A[j];
                 const float4 B = st.B[j];
@@ -1439,7 +1468,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #pragma unroll
             for (int h = 0; h < GRL; h++) {
                 const int f = 16 * h + li;
-                const bool fcol = (f < 9) | ((f >= LSR_GROW_LANG) & (f < LSR_GROW_LANG + D));
+                const bool fcol = LO ? (f < D) : ((f < 9) | ((f >= LSR_GROW_LANG) & (f < LSR_GROW_LANG + D)));
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const int slot = 4 * q + lg;
@@ -2041,6 +2070,21 @@ __global__ void __launch_bounds__(64 * NS) k_render_fwd_quick_wg(RenderArgs a)
                 }
         }
     }
+}
+
+hipError_t launch_render_bwd_lang(const RenderBwdArgs& b, hipStream_t st)
+{
+    const int T = b.f.cam.gx * b.f.cam.gy;
+    if (T == 0) return hipSuccess;
+    switch (lang_set_for(b.f.D)) {
+        case 4: k_render_bwd_mf<4, true><<<4 * T, 64, 0, st>>>(b); break;
+        case 8: k_render_bwd_mf<8, true><<<4 * T, 64, 0, st>>>(b); break;
+        case 16: k_render_bwd_mf<16, true><<<4 * T, 64, 0, st>>>(b); break;
+        case 32: k_render_bwd_mf<32, true><<<4 * T, 64, 0, st>>>(b); break;
+        case 64: k_render_bwd_mf<64, true><<<4 * T, 64, 0, st>>>(b); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_render_bwd(const RenderBwdArgs& b, hipStream_t st)

@@ -224,12 +224,15 @@ class _RasterizeGaussians(torch.autograd.Function):
         def mk(shape, flag):
             return torch.empty(shape, dtype=torch.float32, device=dev) if flag else None
 
-        g_means2D = torch.empty((N, 3), dtype=torch.float32, device=dev)
-        g_means3D = mk((N, 3), True)
+        # only what autograd asks for: with the language input alone requiring
+        # grad (feature mode, means2D without grad) the library runs its
+        # language-only backward
+        g_means2D = mk((N, 3), need[1])
+        g_means3D = mk((N, 3), need[0])
         g_sh = mk(tuple(sh.shape), need[2]) if sh is not None else None
         g_col = mk((N, 3), need[3]) if col is not None else None
         g_lang = mk((N, D), need[4]) if lang is not None else None
-        g_opac = mk((N, 1), True)
+        g_opac = mk((N, 1), need[7])
         g_sc = mk((N, 3), need[8]) if sc is not None else None
         g_rot = mk((N, 4), need[9]) if rot is not None else None
         g_cov = mk((N, 6), need[10]) if cov is not None else None

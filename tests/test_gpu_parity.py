@@ -81,6 +81,33 @@ def test_backward_vs_oracle(name, gpu, oracle_lib):
         assert_grad_close("language_feature_precomp", got["grad_language_feature_precomp"], rb["dlang"])
 
 
+@pytest.mark.parametrize("name", ["sh3_lang16_ragged", "rgb_lang3", "cov_precomp_lang8", "lang64_feature_mode",
+                                  "yaw_sh3_lang32"])
+def test_language_only_backward(name, gpu, oracle_lib):
+    """Feature-mode autograd: only the language input requires grad (geometry
+    frozen, scene/gaussian_model.py:238-243; means2D without grad), so the
+    library runs its language-only backward.  dL/dlanguage vs the oracle."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    from harness import settings_for
+    case = make_case(**CASES[name])
+    pb = oracle_problem(case)
+    ref = oracle_lib.forward(pb)
+    rng = np.random.default_rng(1)
+    H, W = case["cam"]["H"], case["cam"]["W"]
+    dcol = rng.standard_normal((3, H, W)).astype(np.float32)
+    dlang = rng.standard_normal((pb.D, H, W)).astype(np.float32)
+    rb = oracle_lib.backward(pb, ref, dcol, dlang)
+    t = {k: v.to(gpu) for k, v in case["g"].items() if isinstance(v, torch.Tensor)}
+    lang = t["language_feature_precomp"].clone().requires_grad_(True)
+    kw = {k: t[k] for k in ("shs", "colors_precomp", "scales", "rotations", "cov3D_precomp") if k in t}
+    r = GaussianRasterizer(settings_for(case, gpu))
+    color, lo, _ = r(means3D=t["means3D"], means2D=torch.zeros_like(t["means3D"]), opacities=t["opacities"],
+                     language_feature_precomp=lang, **kw)
+    torch.autograd.backward([color, lo], [torch.from_numpy(dcol).to(gpu), torch.from_numpy(dlang).to(gpu)])
+    np.testing.assert_array_equal(lo.detach().cpu().numpy(), ref["lang"])
+    assert_grad_close("language_feature_precomp", lang.grad.cpu().numpy(), rb["dlang"])
+
+
 def test_empty_and_all_culled(gpu, oracle_lib):
     for N, behind in ((0, False), (300, True)):
         case = make_case(N=max(N, 1) if N else 0, W=64, H=48, sh_degree=None, seed=11) if N else None
