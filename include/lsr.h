@@ -206,6 +206,15 @@ int lsr_lang_loss_backward(const float* weight_map, const float* codebooks, int 
                            const float* grad_loss, float* grad_weight_map, float* grad_codebooks, lsr_alloc_fn alloc,
                            void* alloc_ctx, void* stream);
 
+/* Fused Adam step: the update of torch.optim.Adam as the
+ * reference builds it (scene/gaussian_model.py:234-255, no amsgrad), one pass
+ * over n fp32 elements of params / grads / exp_avg / exp_avg_sq (device
+ * pointers, same layout).  step is the 1-based step count after increment;
+ * the scalars are doubles (Python floats) and the bias corrections are
+ * formed in double on the host, as torch does. */
+int lsr_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, double lr,
+                  double beta1, double beta2, double eps, double weight_decay, int64_t step, void* stream);
+
 /* simple_knn._C.distCUDA2 (scene/gaussian_model.py:20,194): for points
  * (N, 3) fp32, out[i] = mean of the three smallest squared distances
  * dx*dx + dy*dy + dz*dz to points j != i (exact; FLT_MAX for missing

@@ -104,7 +104,7 @@ class BwdOut(ctypes.Structure):
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
 
 EXPORTS = ("lsr_forward", "lsr_backward", "lsr_mark_visible", "lsr_quick_decode", "lsr_topk_code_forward",
-           "lsr_topk_code_backward", "lsr_knn_dist2", "lsr_lang_loss_forward", "lsr_lang_loss_backward", "lsr_strerror",
+           "lsr_topk_code_backward", "lsr_knn_dist2", "lsr_lang_loss_forward", "lsr_lang_loss_backward", "lsr_adam_step", "lsr_strerror",
            "lsr_abi_version", "lsr_max_lang_dim", "lsr_profile_enable", "lsr_profile_stages", "lsr_profile_reset",
            "lsr_profile_query")
 
@@ -148,6 +148,9 @@ def load(path: str | None = None):
     lib.lsr_lang_loss_backward.argtypes = [_vp, _vp, _ci, _ci, _ci, _ci, _vp, _vp, _ci, _vp, _vp, _vp, _vp,
                                            ALLOC_FN, _vp, _vp]
     lib.lsr_lang_loss_backward.restype = ctypes.c_int
+    _cd = ctypes.c_double
+    lib.lsr_adam_step.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_int64, _cd, _cd, _cd, _cd, _cd, ctypes.c_int64, _vp]
+    lib.lsr_adam_step.restype = ctypes.c_int
     lib.lsr_strerror.argtypes = [ctypes.c_int]
     lib.lsr_strerror.restype = ctypes.c_char_p
     lib.lsr_abi_version.restype = ctypes.c_int

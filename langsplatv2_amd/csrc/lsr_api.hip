@@ -8,6 +8,7 @@
 //   -> render (dense or quick)
 // Backward: zero gradient rows -> render bwd (wave-reduced atomics)
 //   -> preprocess bwd (chain rule, writes every requested output).
+#include <math.h>
 #include <stdio.h>
 #include <string.h>
 #include <utility>
@@ -246,6 +247,28 @@ int lsr_lang_loss_backward(const float* weight_map, const float* codebooks, int 
     if (lsr::launch_lang_loss(weight_map, codebooks, Df, H, W, seg, features, S, grad_loss, nullptr,
                               grad_weight_map, grad_codebooks, const_cast<float*>(pixel_stats), ws,
                               (hipStream_t)stream) != hipSuccess)
+        return LSR_EHIP;
+    return LSR_OK;
+}
+
+int lsr_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n, double lr,
+                  double beta1, double beta2, double eps, double weight_decay, int64_t step, void* stream)
+{
+    if (n < 0 || step < 1 || !(beta1 >= 0.0 && beta1 < 1.0) || !(beta2 >= 0.0 && beta2 < 1.0)) return LSR_EINVAL;
+    if (n == 0) return LSR_OK;
+    if (!params || !grads || !exp_avg || !exp_avg_sq) return LSR_EINVAL;
+    // scalars as torch forms them: Python doubles, rounded once to fp32
+    const double bc1 = 1.0 - pow(beta1, (double)step);
+    const double bc2 = 1.0 - pow(beta2, (double)step);
+    lsr::AdamArgs a;
+    a.one_minus_b1 = (float)(1.0 - beta1);
+    a.b2 = (float)beta2;
+    a.one_minus_b2 = (float)(1.0 - beta2);
+    a.eps = (float)eps;
+    a.step_size = (float)(lr / bc1);
+    a.bc2_sqrt = (float)sqrt(bc2);
+    a.weight_decay = (float)weight_decay;
+    if (lsr::launch_adam(params, grads, exp_avg, exp_avg_sq, n, a, (hipStream_t)stream) != hipSuccess)
         return LSR_EHIP;
     return LSR_OK;
 }

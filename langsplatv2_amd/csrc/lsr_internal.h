@@ -103,4 +103,10 @@ hipError_t launch_lang_loss(const float* wmap, const float* cb, int Df, int H, i
                             const float* feat, int S, const float* gscale, float* loss, float* gw, float* dcb,
                             float* stats, float* ws, hipStream_t st);
 
+// adam.hip
+struct AdamArgs {
+    float one_minus_b1, b2, one_minus_b2, eps, step_size, bc2_sqrt, weight_decay;
+};
+hipError_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, const AdamArgs& a, hipStream_t st);
+
 }  // namespace lsr

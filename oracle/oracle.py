@@ -355,3 +355,25 @@ def lang_cos_loss(weight_map: np.ndarray, codebook: np.ndarray, seg: np.ndarray,
     dW = (cb @ gx).reshape(K, H, W)
     dcb = w @ gx.T
     return loss, dW, dcb
+
+
+def adam_steps(param: np.ndarray, grads: list, lr: float, betas=(0.9, 0.999), eps: float = 1e-8,
+               weight_decay: float = 0.0):
+    """torch.optim.Adam's update (no amsgrad; the reference's optimizer,
+    scene/gaussian_model.py:255) applied for each gradient in `grads`, in
+    float64: m = lerp(m, g, 1-b1); v = b2 v + (1-b2) g^2;
+    p -= lr/(1-b1^t) * m / (sqrt(v)/sqrt(1-b2^t) + eps).  Returns (p, m, v)."""
+    p = np.asarray(param, np.float64).copy()
+    m = np.zeros_like(p)
+    v = np.zeros_like(p)
+    b1, b2 = betas
+    for t, g in enumerate(grads, start=1):
+        g = np.asarray(g, np.float64)
+        if weight_decay:
+            g = g + weight_decay * p
+        m = m + (1.0 - b1) * (g - m)
+        v = b2 * v + (1.0 - b2) * g * g
+        step_size = lr / (1.0 - b1 ** t)
+        denom = np.sqrt(v) / np.sqrt(1.0 - b2 ** t) + eps
+        p = p - step_size * m / denom
+    return p, m, v

@@ -10,11 +10,12 @@ Per rank and iteration (one view per rank, views sharded across ranks):
   loss = language_cos_loss(weight_map, codebooks, seg, feat)             fused loss (HIP)
   loss.backward()                                           -> logits.grad, codebooks.grad
   all-reduce(SUM) of the two gradients in one bucket        (RCCL, world > 1)
-  Adam step (torch, lr 0.0025 on both, eps 1e-15 as scene/gaussian_model.py:234-255)
+  Adam step (FusedAdam, HIP; lr 0.0025 on both, eps 1e-15 as scene/gaussian_model.py:234-255)
 
 --reference runs the same iteration with the reference's torch formulation of
 the producer (utils/vq_utils.py:9-24) and of the loss (materialised features +
 gathered ground truth + cos_loss), the rasterizer unchanged.
+--torch-adam steps with torch.optim.Adam instead of FusedAdam.
 --means2d-grad gives means2D requires_grad as render() does
 (gaussian_renderer/__init__.py:27-31): the rasterizer then runs its full
 backward; feature mode never reads that gradient (train.py:247), and without
@@ -38,6 +39,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer  # noqa: E402
 from langsplatv2_amd import _lib, dp, lang_codes  # noqa: E402
 from langsplatv2_amd.lang_loss import language_cos_loss  # noqa: E402
+from langsplatv2_amd.optim import FusedAdam  # noqa: E402
 from langsplatv2_amd.scenes import CONFIGS, make_camera, make_gaussians, softmax_to_topk_soft_code  # noqa: E402
 
 
@@ -57,6 +59,7 @@ def main():
     ap.add_argument("--segments", type=int, default=200)
     ap.add_argument("--reference", action="store_true")
     ap.add_argument("--means2d-grad", action="store_true")
+    ap.add_argument("--torch-adam", action="store_true")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -76,8 +79,8 @@ def main():
     gen = torch.Generator(device="cpu").manual_seed(7)
     logits = torch.randn(N, K, generator=gen).to(dev).requires_grad_(True)
     codebooks = torch.randn(1, K, Df, generator=gen).to(dev).requires_grad_(True)
-    opt = torch.optim.Adam([{"params": [logits, codebooks], "lr": 0.0025, "name": "language_feature"}], lr=0.0,
-                           eps=1e-15)
+    adam = torch.optim.Adam if (a.torch_adam or a.reference) else FusedAdam
+    opt = adam([{"params": [logits, codebooks], "lr": 0.0025, "name": "language_feature"}], lr=0.0, eps=1e-15)
     # this rank's view: segment ids in coherent regions, a per-view feature table
     vg = torch.Generator(device="cpu").manual_seed(100 + rank)
     S = a.segments
@@ -136,7 +139,8 @@ def main():
         print(json.dumps({
             "workload": "feature-mode training iteration (cfg4 step shape), synthetic: 1M Gaussians, 1920x1080, "
                         "64 codes x 512-d codebook, top-4 soft codes, cos loss, Adam; 1 view per GPU",
-            "variant": "reference torch ops for producer + loss" if a.reference else "fused HIP producer + loss",
+            "variant": "reference torch ops for producer + loss + torch Adam" if a.reference else
+                       "fused HIP producer + loss + " + ("torch Adam" if a.torch_adam else "FusedAdam"),
             "means2d_grad": a.means2d_grad, "n_gpus": world, "steps": a.steps,
             "ms_per_iteration": round(el / a.steps * 1e3, 4), "iterations_per_s": round(a.steps / el, 2),
             "views_per_s": round(world * a.steps / el, 2), "rasterizer_stages_ms": stages,
