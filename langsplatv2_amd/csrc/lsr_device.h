@@ -41,6 +41,32 @@ __device__ __forceinline__ float expf_det(float x)
     return p * __uint_as_float((__float_as_uint(t) << 23) + 0x3f800000u);
 }
 
+// Two expf_det at once on packed f32 (v_pk_fma/add/mul: each half rounds
+// exactly as the scalar instruction), bitwise equal to expf_det for
+// x >= -87.  No range guard: the render loops only consume exponents of
+// pairs that passed the power >= cut test, i.e. x in [-5.6, 0]; lanes outside
+// are discarded (their alpha is never selected).
+typedef float lsr_f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t lsr_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ lsr_f32x2 expf_det2(lsr_f32x2 x)
+{
+    const lsr_f32x2 t = __builtin_elementwise_fma(x, lsr_f32x2{1.44269504088896341f, 1.44269504088896341f},
+                                                  lsr_f32x2{12582912.0f, 12582912.0f});
+    const lsr_f32x2 n = t - lsr_f32x2{12582912.0f, 12582912.0f};
+    lsr_f32x2 r = __builtin_elementwise_fma(n, lsr_f32x2{-0.693145751953125f, -0.693145751953125f}, x);
+    r = __builtin_elementwise_fma(n, lsr_f32x2{-1.428606765330187e-06f, -1.428606765330187e-06f}, r);
+    lsr_f32x2 p = lsr_f32x2{0x1.6aea1ap-10f, 0x1.6aea1ap-10f};
+    p = __builtin_elementwise_fma(p, r, lsr_f32x2{0x1.1267d2p-7f, 0x1.1267d2p-7f});
+    p = __builtin_elementwise_fma(p, r, lsr_f32x2{0x1.555820p-5f, 0x1.555820p-5f});
+    p = __builtin_elementwise_fma(p, r, lsr_f32x2{0x1.555418p-3f, 0x1.555418p-3f});
+    p = __builtin_elementwise_fma(p, r, lsr_f32x2{0x1.fffffcp-2f, 0x1.fffffcp-2f});
+    p = __builtin_elementwise_fma(p, r, lsr_f32x2{1.0f, 1.0f});
+    p = __builtin_elementwise_fma(p, r, lsr_f32x2{1.0f, 1.0f});
+    const lsr_u32x2 tb = __builtin_bit_cast(lsr_u32x2, t);
+    const lsr_u32x2 sb = (tb << 23) + lsr_u32x2{0x3f800000u, 0x3f800000u};
+    return p * __builtin_bit_cast(lsr_f32x2, sb);
+}
+
 // Wave votes on a bool.  HIP's __ballot/__any take an int, which makes the
 // compiler round-trip an SGPR lane mask through a VGPR (v_cndmask + v_cmp,
 // 2 VALU per vote); the builtin on i1 stays on the scalar unit.
