@@ -310,15 +310,51 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // j >> 1, component j & 1, so the blend loop reads candidates (2i, 2i+1) of
 // each field with one ds_read_b64 and evaluates both exponents with packed
 // f32 instructions (bitwise identical to the scalar ones).
-template <int F4>
+#ifndef LSR_FWD_SFEAT
+#define LSR_FWD_SFEAT 32    // fwd: from this many language channels up, feature rows are read with scalar
+                            // loads at blend time instead of staged in LDS (cfg5 D = 32: 2.46 -> 2.02 ms;
+                            // at D = 16 the SGPR pressure makes it slower: 0.36 -> 0.61 ms)
+#endif
+#ifndef LSR_FWD_SFEAT_LAZY
+#define LSR_FWD_SFEAT_LAZY 0   // 1: fetch the second row just before its blend (fewer SGPRs live, measured slower)
+#endif
+template <int NL>
+constexpr bool fwd_sfeat() { return LSR_FWD_SFEAT > 0 && NL >= LSR_FWD_SFEAT; }
+template <int F4, bool SF>
 struct WaveStageP {
     f32x2 X[32], Y[32], CA[32], CB[32], CC[32], OP[32], CUT[32];
-    float4 F[64 * F4];
+    float4 F[SF ? 1 : 64 * F4];
+    uint32_t gid[SF ? 64 : 1];
     int pos[64];
 };
 
+// Feature row (rgb + dense language, zero-padded) of a wave-uniform Gaussian:
+// the address is uniform, so these are scalar loads through the constant
+// cache, off the LDS path the blend is otherwise bound by (every lane reads
+// the same row).
+typedef const float __attribute__((address_space(4)))* lsr_cfptr;   // constant address space: scalar loads
 template <int NL, int F4>
-__device__ __forceinline__ int stage_candidates_p(WaveStageP<F4>& st, bool valid, uint32_t gid, int pos, int bx,
+__device__ __forceinline__ void feature_row_uniform(float (&row)[F4 * 4], const float* __restrict__ rgb_g,
+                                                    const float* __restrict__ lang_g, int D, uint32_t gid)
+{
+    const lsr_cfptr rgb = (lsr_cfptr)rgb_g;
+    const lsr_cfptr lang = (lsr_cfptr)lang_g;
+    row[0] = rgb[3 * gid];
+    row[1] = rgb[3 * gid + 1];
+    row[2] = rgb[3 * gid + 2];
+    if (NL > 0 && D == NL) {
+#pragma unroll
+        for (int k = 0; k < NL; k++) row[3 + k] = lang[(size_t)gid * NL + k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < NL; k++) row[3 + k] = (k < D) ? lang[(size_t)gid * D + k] : 0.f;
+    }
+#pragma unroll
+    for (int k = 3 + NL; k < F4 * 4; k++) row[k] = 0.f;
+}
+
+template <int NL, int F4>
+__device__ __forceinline__ int stage_candidates_p(WaveStageP<F4, fwd_sfeat<NL>()>& st, bool valid, uint32_t gid, int pos, int bx,
                                                   int by, const float4* __restrict__ splatA,
                                                   const float4* __restrict__ splatB, const float* __restrict__ rgb,
                                                   const float* __restrict__ lang, int D)
@@ -344,7 +380,10 @@ __device__ __forceinline__ int stage_candidates_p(WaveStageP<F4>& st, bool valid
         base[5 * 64 + e] = B.y;
         base[6 * 64 + e] = B.z;
         st.pos[r] = pos;
-        stage_features<NL, F4>(&st.F[r * F4], rgb, lang, D, gid);
+        if constexpr (fwd_sfeat<NL>())
+            st.gid[r] = gid;
+        else
+            stage_features<NL, F4>(&st.F[r * F4], rgb, lang, D, gid);
     }
     wave_lds_fence();
     return cnt;
@@ -356,7 +395,8 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
     constexpr int C = 3 + NL;
     constexpr int F4 = (C + 3) / 4;  // float4 per feature row
 #if LSR_FWD_PK
-    __shared__ WaveStageP<F4> st;
+    constexpr bool SF = fwd_sfeat<NL>();
+    __shared__ WaveStageP<F4, SF> st;
 #else
     __shared__ WaveStage<F4> st;
 #endif
@@ -404,6 +444,13 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
             // both candidates' exponents at once (splat_power, lane-wise);
             // a missing second candidate reads a stale slot: ok1 masks it
             const int e = j0 >> 1;
+            // SF: the pair's feature rows (scalar loads; uniform ids)
+            float fr0[F4 * 4], fr1[F4 * 4];
+            if constexpr (SF) {
+                feature_row_uniform<NL, F4>(fr0, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j0]));
+                if (!LSR_FWD_SFEAT_LAZY)
+                    feature_row_uniform<NL, F4>(fr1, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j1]));
+            }
             const f32x2 dx = st.X[e] - f32x2{pfx, pfx}, dy = st.Y[e] - f32x2{pfy, pfy};
             const f32x2 P = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f},
                                                       __builtin_elementwise_fma(st.CA[e] * dx, dx, (st.CC[e] * dy) * dy),
@@ -441,13 +488,21 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 ok0 = ok0 && !term;
                 ok1 = ok1 && !term;
                 const float aT = ok0 ? al0 * T : 0.f;
+#if LSR_FWD_PK
+                if constexpr (SF) {
 #pragma unroll
-                for (int f = 0; f < F4; f++) {
-                    const float4 v = st.F[j0 * F4 + f];
-                    acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
-                    acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
-                    acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
-                    acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
+                    for (int k = 0; k < F4 * 4; k++) acc[k] = fmaf(fr0[k], aT, acc[k]);
+                } else
+#endif
+                {
+#pragma unroll
+                    for (int f = 0; f < F4; f++) {
+                        const float4 v = st.F[j0 * F4 + f];
+                        acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
+                        acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
+                        acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
+                        acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
+                    }
                 }
                 T = ok0 ? test_T : T;
                 last = ok0 ? (uint32_t)st.pos[j0] : last;
@@ -458,13 +513,23 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 done = done || term;
                 ok1 = ok1 && !term;
                 const float aT = ok1 ? al1 * T : 0.f;
+#if LSR_FWD_PK
+                if constexpr (SF) {
+                    if (LSR_FWD_SFEAT_LAZY)   // second row fetched here: half the SGPRs live
+                        feature_row_uniform<NL, F4>(fr1, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j1]));
 #pragma unroll
-                for (int f = 0; f < F4; f++) {
-                    const float4 v = st.F[j1 * F4 + f];
-                    acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
-                    acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
-                    acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
-                    acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
+                    for (int k = 0; k < F4 * 4; k++) acc[k] = fmaf(fr1[k], aT, acc[k]);
+                } else
+#endif
+                {
+#pragma unroll
+                    for (int f = 0; f < F4; f++) {
+                        const float4 v = st.F[j1 * F4 + f];
+                        acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
+                        acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
+                        acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
+                        acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
+                    }
                 }
                 T = ok1 ? test_T : T;
                 last = ok1 ? (uint32_t)st.pos[j1] : last;
