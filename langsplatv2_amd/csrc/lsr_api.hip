@@ -595,10 +595,18 @@ int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* 
         LSR_DEBUG_SYNC(s, st, "render_bwd_lang");
         return LSR_OK;
     }
-    const int VP = grad_row_width(Dd);
+    // D = 16 / 32 with dL/dlang requested: the render backward adds the
+    // language gradients straight into the output; the rows keep geometry +
+    // colour (one 64-B line) and preprocess_bwd no longer copies language
+    const bool lang_direct = Dd > 0 && out->dL_dlang && bwd_lang_direct(Dd);
+    const int VP = lang_direct ? 16 : grad_row_width(Dd);
     float* gacc = (float*)alloc(ctx, (size_t)P * VP * 4, LSR_BUF_GRAD);
     if (!gacc) return LSR_ENOMEM;
-    { StageScope sc(ST_GZERO, st); LSR_HIP(hipMemsetAsync(gacc, 0, (size_t)P * VP * 4, st)); }
+    {
+        StageScope sc(ST_GZERO, st);
+        LSR_HIP(hipMemsetAsync(gacc, 0, (size_t)P * VP * 4, st));
+        if (lang_direct) LSR_HIP(hipMemsetAsync(out->dL_dlang, 0, (size_t)P * Dd * 4, st));
+    }
 
     RenderBwdArgs rb;
     rb.f = make_render_args(s, in, c, (const uint8_t*)b->geom, (const uint8_t*)b->binning, (const uint8_t*)b->image,
@@ -610,13 +618,14 @@ int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* 
     rb.dout_lang = Dd ? b->dL_dout_lang : nullptr;
     rb.grad_acc = gacc;
     rb.VP = VP;
+    rb.lang_acc = lang_direct ? out->dL_dlang : nullptr;
     { StageScope sc(ST_RENDER_BWD, st); LSR_HIP(launch_render_bwd(rb, st)); }
     LSR_DEBUG_SYNC(s, st, "render_bwd");
 
     lsr_inputs in2 = *in;
     in2.lang_dim = Dd;
     lsr_bwd_out o2 = *out;
-    if (!Dd) o2.dL_dlang = nullptr;
+    if (!Dd || lang_direct) o2.dL_dlang = nullptr;
     { StageScope sc(ST_PRE_BWD, st); LSR_HIP(launch_preprocess_bwd(c, in2, (const uint8_t*)b->geom, b->radii, gacc, VP, o2, st)); }
     LSR_DEBUG_SYNC(s, st, "preprocess_bwd");
     return LSR_OK;

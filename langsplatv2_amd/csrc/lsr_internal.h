@@ -75,7 +75,11 @@ struct RenderBwdArgs {
     const float* dout_lang;
     float* grad_acc;   // (P, VP) atomically accumulated
     int VP;
+    // non-null: dL/dlanguage is accumulated straight into this (P, D) output
+    // (zeroed by the caller) and the gradient rows hold geometry + colour only
+    float* lang_acc = nullptr;
 };
+bool bwd_lang_direct(int D);  // D for which the full backward supports lang_acc
 int grad_row_width(int D);   // VP for a dense language dim
 hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t st);
 // language-only backward: grad_acc is the (P, D) dL/dlanguage output itself

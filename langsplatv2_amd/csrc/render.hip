@@ -1048,6 +1048,9 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
 #ifndef LSR_BWD_VMOM
 #define LSR_BWD_VMOM 1      // bwd: geometry moments and RGB sums on the VALU, MFMA only for dot + language
 #endif
+#ifndef LSR_BWD_LANG_DIRECT
+#define LSR_BWD_LANG_DIRECT 1   // bwd, D = 16 / 32: dL/dlang atomics straight into the output (no row copy)
+#endif
 #ifndef LSR_BWD_ALIAS
 #define LSR_BWD_ALIAS 1
 #endif
@@ -1130,10 +1133,11 @@ __device__ __forceinline__ float feature_at(const RenderArgs& a, uint32_t gid, i
 // requiring grad).  Then dL/dlang[j][c] = sum_p aT[j][p] dL/dout[c][p] is all
 // that is left: no dot products, no dL/dalpha recurrence, no moments, and the
 // rows go straight into the (N, D) output (b.grad_acc, b.VP = D).
-template <int NL, bool LO = false>
+template <int NL, bool LO = false, bool LD = false>
 __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArgs b)
 {
     static_assert(!LO || (LSR_BWD_VMOM && NL > 0), "language-only backward needs the VMOM layout and D > 0");
+    static_assert(!LD || (LSR_BWD_VMOM && !LO && NL % 16 == 0), "direct dL/dlang needs VMOM and whole 16-channel lines");
     using FR = BwdFrags<NL>;
     constexpr int KS = FR::KS;
 #if LSR_BWD_VMOM
@@ -1148,7 +1152,9 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #endif
     constexpr int GS = LSR_GRP_STRIDE;
     __shared__ WaveStageG st;
-    constexpr int GCOL0 = LO ? 0 : LSR_GROW_LANG;          // first language column of a staged row
+    // first language column of a staged row; LD: the language lines start at
+    // 16 and go to b.lang_acc, the first line (geometry + colour) to the row
+    constexpr int GCOL0 = LO ? 0 : (LD ? 16 : LSR_GROW_LANG);
     constexpr int GRL = (GCOL0 + NL + 15) / 16;            // 16-float lines per gradient row
     constexpr int GRS = 16 * GRL + 4;                     // staged row stride
 #if LSR_BWD_ALIAS
@@ -1543,13 +1549,19 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #pragma unroll
             for (int h = 0; h < GRL; h++) {
                 const int f = 16 * h + li;
-                const bool fcol = LO ? (f < D) : ((f < 9) | ((f >= LSR_GROW_LANG) & (f < LSR_GROW_LANG + D)));
+                const bool fcol = LO ? (f < D)
+                                  : LD ? (h == 0 ? (f < 9) : (f - 16 < D))
+                                       : ((f < 9) | ((f >= LSR_GROW_LANG) & (f < LSR_GROW_LANG + D)));
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const int slot = 4 * q + lg;
                     const float v = sGr[slot * GRS + f];
-                    if (fcol & (slot < kn) & (v != 0.f))
-                        LSR_MF_ATOMIC(b.grad_acc + (size_t)st.gid[g0 + slot] * VP + f, v);
+                    if (fcol & (slot < kn) & (v != 0.f)) {
+                        if (LD && h > 0)
+                            LSR_MF_ATOMIC(b.lang_acc + (size_t)st.gid[g0 + slot] * D + (f - 16), v);
+                        else
+                            LSR_MF_ATOMIC(b.grad_acc + (size_t)st.gid[g0 + slot] * VP + f, v);
+                    }
                 }
             }
             wave_lds_fence();
@@ -2162,10 +2174,25 @@ hipError_t launch_render_bwd_lang(const RenderBwdArgs& b, hipStream_t st)
     return hipGetLastError();
 }
 
+bool bwd_lang_direct(int D)
+{
+    return LSR_BWD_MF && LSR_BWD_VMOM && LSR_BWD_LANG_DIRECT && (D == 16 || (D == 32 && LSR_BWD_MF_WIDE));
+}
+
 hipError_t launch_render_bwd(const RenderBwdArgs& b, hipStream_t st)
 {
     const int T = b.f.cam.gx * b.f.cam.gy;
     if (T == 0) return hipSuccess;
+    if (b.lang_acc) {
+        if (!bwd_lang_direct(b.f.D)) return hipErrorInvalidValue;
+#if LSR_BWD_MF && LSR_BWD_VMOM
+        if (b.f.D == 16) k_render_bwd_mf<16, false, true><<<4 * T, 64, 0, st>>>(b);
+#if LSR_BWD_MF_WIDE
+        else k_render_bwd_mf<32, false, true><<<4 * T, 64, 0, st>>>(b);
+#endif
+#endif
+        return hipGetLastError();
+    }
     switch (lang_set_for(b.f.D)) {
 #if LSR_BWD_MF
         case 0: k_render_bwd_mf<0><<<4 * T, 64, 0, st>>>(b); break;
