@@ -97,7 +97,10 @@ def pmc_traffic(stage):
     profiles/r*_pmc_traffic.json (tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE
     rocprofv3 passes over tools/pmc_step.py = this workload, gfx950-corrected)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    import re
+    # natural order: r01v10 after r01v9
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")),
+                   key=lambda f: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(f))])
     if not files:
         return None, None
     with open(files[-1]) as f:
