@@ -7,22 +7,30 @@ backward through the drop-in `diff_gaussian_rasterization` surface with EVERY in
 requiring grad, upstream gradients ~ N(0,1).
 
 One step = one view per GPU: forward + backward (+ for N > 1 the RCCL all-reduce(SUM) of
-all per-Gaussian gradients — the data-parallel exchange of SURVEY.md §8e).  Views shard
-one per rank (camera yaw depends on the rank), Gaussians are replicated: weak scaling.
+all per-Gaussian gradients — the data-parallel exchange of SURVEY.md §8e, written straight
+into the all-reduce buckets, the language bucket started while preprocess_bwd still runs).
+Views shard one per rank (camera yaw depends on the rank), Gaussians are replicated: weak
+scaling.
 
   python bench.py [--gpus N --steps K --warmup W]
+      N > 1 without WORLD_SIZE in the environment: bench.py starts N ranks itself (a
+      torch.distributed.run child, before any GPU call) and exits with its status
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+  python bench.py --gpus 2 --dry-run     # ranks come up on gloo, agree on the world size; no GPU
 
 Rank 0 prints ONE JSON line.  Extra fields: per-stage HIP-event times (stages_ms), the
-roofline of the dominant kernel, whole-step algorithmic HBM GB/s, forward FPS at 1.0 Mpix
-(1280x800, the >=450 FPS target), and the CPU baseline (the oracle, timed on this host).
+roofline of the dominant kernel (SURVEY §8d algorithmic bytes / HIP-event time), whole-step
+algorithmic HBM GB/s, forward FPS at 1.0 Mpix (1280x800, the >=450 FPS target), the quick
+(sparse 192-channel) render + codebook decode FPS at 1 Mpix, and the CPU baseline (the
+oracle's C restatement on the host's cores).
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -41,18 +49,29 @@ METRIC = "frames/s fwd+bwd @ 1M Gaussians 1080p 3+16ch; achieved HBM GB/s"
 HBM_PEAK_GBPS = 8000.0   # MI355X spec (MI355X_MICROARCH.md chip table)
 
 
-def settings(cam, dev, sh_degree, include_feature):
+def settings(cam, dev, sh_degree, include_feature, quick=False, quick_dim=None):
     return GaussianRasterizationSettings(
         image_height=cam["H"], image_width=cam["W"], tanfovx=cam["tanfovx"], tanfovy=cam["tanfovy"],
         bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=cam["viewmatrix"].to(dev),
         projmatrix=cam["projmatrix"].to(dev), sh_degree=sh_degree, campos=cam["campos"].to(dev),
-        prefiltered=False, debug=False, include_feature=include_feature, quick_render=False)
+        prefiltered=False, debug=False, include_feature=include_feature, quick_render=quick,
+        language_feature_dim=quick_dim)
 
 
 def algorithmic_bytes(g, rs, D, S):
-    """Per-stage algorithmic HBM bytes of one forward+backward (with this
-    build's record layout).  Instance terms use the instances the blend must visit:
-    per tile, up to its largest n_contrib (+1 terminating), rounded to the 256-batch."""
+    """Per-stage algorithmic HBM bytes of one forward+backward, SURVEY.md §8d's formula
+    (M = measured num_rendered, C = 3 + D, S SH floats), mapped onto this build's stages:
+      preprocess     N(44+4S) + 75N
+      bin_count      8N [scan] + 20N [duplicate's per-Gaussian reads]
+      bin_scatter    12M [duplicate's per-instance key/value writes]
+      tile_sort      24M [sort] + 8M [ranges]
+      scan_tile_counts 8T [ranges]
+      render_fwd     M(28+4C) + P(4C+8)
+      render_bwd     M(28+4C) + 8T + P(4C+8) + N(24+4C)
+      preprocess_bwd N(12+12+16+4S+4+24+12+8+12+3) + N(12+12+16+4S+12)
+      grad_zero      0 (an implementation memset, no §8d term)
+    Also returns the instances the blend actually visits ("staged": per tile up to its
+    largest n_contrib, rounded to the 256-batch) for context."""
     N = g["means3D"].shape[0]
     e = torch.empty(0, device=g["means3D"].device)
     _, _, radii, M, bufs, _, _ = rasterizer._run_forward(
@@ -72,21 +91,16 @@ def algorithmic_bytes(g, rs, D, S):
     P = W * H
     T = gx * gy
     C = 3 + D
-    inst = 4 + 32 + 4 * C     # point_list id + splat record + feature row
-    VP = ((12 + D) + 31) // 32 * 32
-    chunk = max(1024, (N + 511) // 512)
-    chunk = (chunk + 255) // 256 * 256
-    B = (N + chunk - 1) // chunk
     b = {
-        "preprocess": N * (12 + 12 + 16 + 4 + 4 * S) + N * (16 + 16 + 12 + 4 + 4 + 4 + 4),
-        "bin_count": N * 4 + vis * 16 + B * T * 4 * 3 + T * 4,
-        "scan_tile_counts": T * 12,
-        "bin_scatter": N * 4 + vis * (16 + 4) + B * T * 4 + T * 4 + M * 8,
-        "tile_sort": M * (8 + 4),
-        "render_fwd": staged_f * inst + T * 8 + P * (4 * C + 8),
-        "grad_zero": N * VP * 4,
-        "render_bwd": staged_b * inst + T * 8 + P * (4 * C + 8) + vis * (9 + D) * 4,
-        "preprocess_bwd": N * ((9 + D) * 4 + 12 + 12 + 16 + 4 * S + 4 + 4) + N * (12 + 4 + 4 * D + 12 + 4 * S + 12 + 16),
+        "preprocess": N * (44 + 4 * S) + N * 75,
+        "bin_count": N * 8 + N * 20,
+        "scan_tile_counts": T * 8,
+        "bin_scatter": M * 12,
+        "tile_sort": M * 24 + M * 8,
+        "render_fwd": M * (28 + 4 * C) + P * (4 * C + 8),
+        "grad_zero": 0,
+        "render_bwd": M * (28 + 4 * C) + T * 8 + P * (4 * C + 8) + N * (24 + 4 * C),
+        "preprocess_bwd": N * (12 + 12 + 16 + 4 * S + 4 + 24 + 12 + 8 + 12 + 3) + N * (12 + 12 + 16 + 4 * S + 12),
     }
     return b, dict(num_rendered=M, visible=vis, staged_fwd=staged_f, staged_bwd=staged_b,
                    mean_n_contrib=float(nc.float().mean().item()))
@@ -106,66 +120,152 @@ def pmc_traffic(stage):
     with open(files[-1]) as f:
         doc = json.load(f)
     ks = [v for k, v in doc["kernels"].items()
-          if k == "k_" + stage or k.startswith("k_" + stage + "<") or k.startswith("k_" + stage + "_mf<")]
+          if k == "k_" + stage or k.startswith("k_" + stage + "<") or k.startswith("k_" + stage + "_")]
     if not ks:
         return None, None
     return int(sum(v["traffic_bytes"] for v in ks)), os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(cam, gcpu, D, budget_tiles=2048):
-    """The oracle (C restatement, single thread) on a bounded sample of the same frame:
-    full preprocess + binning + preprocess-bwd, render fwd+bwd on `budget_tiles` seeded
-    tiles, the render part extrapolated by T / budget_tiles."""
+def host_threads() -> int:
+    """CPU threads this process may use: the box's share (OMP_NUM_THREADS is set to it on the
+    GPU pool; os.cpu_count() reports the whole machine there), else the affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        return os.cpu_count() or 1
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cam, gcpu, D):
+    """The oracle (oracle/lsr_oracle.c: the naive per-pixel serial blend, per-tile loops) on
+    the host's cores, the WHOLE frame: preprocess + binning (single-threaded in the oracle),
+    render forward over all tiles on `threads` OpenMP threads, render backward on the same
+    threads (fp64 atomic accumulation) + preprocess backward.  kind "port": the reference's
+    CUDA rasterizer source is absent, this is its restatement."""
     from oracle import oracle as O
     O.build()
+    threads = host_threads()
     pb = O.Problem(cam, gcpu)
-    lib = O.load()
-    T = pb.gx * pb.gy
     rng = np.random.default_rng(0)
-    tiles = np.sort(rng.choice(T, size=min(budget_tiles, T), replace=False)).astype(np.int32)
-    t0 = time.perf_counter()
-    f = O.forward(pb, nthreads=1, tiles=np.zeros(0, np.int32))   # preprocess + binning only
-    t1 = time.perf_counter()
-    f2 = O.forward(pb, nthreads=1, tiles=tiles)
-    t2 = time.perf_counter()
-    t_pre_bin = t1 - t0
-    t_rf = (t2 - t1) - t_pre_bin        # f2 repeats preprocess+binning; subtract it
     dcol = rng.standard_normal((3, pb.H, pb.W)).astype(np.float32)
     dlang = rng.standard_normal((pb.D, pb.H, pb.W)).astype(np.float32) if pb.D else None
+    t0 = time.perf_counter()
+    O.forward(pb, nthreads=threads, tiles=np.zeros(0, np.int32))   # preprocess + binning only
+    t1 = time.perf_counter()
+    f = O.forward(pb, nthreads=threads)
+    t2 = time.perf_counter()
+    O.backward(pb, f, dcol, dlang, nthreads=threads)
     t3 = time.perf_counter()
-    O.backward(pb, f2, dcol, dlang, tiles=tiles)
-    t4 = time.perf_counter()
-    t_bwd_sample = t4 - t3              # render bwd on the sample + full preprocess bwd
-    scale = T / len(tiles)
-    t_frame = t_pre_bin + max(t_rf, 0.0) * scale + t_bwd_sample * scale
-    del f
-    return dict(value=1.0 / t_frame, unit="frames/s", cores=1, kind="port",
-                sample=f"oracle/lsr_oracle.c single-threaded: full preprocess+binning ({t_pre_bin:.2f}s), render "
-                       f"fwd {len(tiles)}/{T} seeded tiles ({max(t_rf, 0):.2f}s), render bwd + preprocess bwd on "
-                       f"the same tiles ({t_bwd_sample:.2f}s); render + bwd extrapolated x{scale:.1f}",
-                seconds_per_frame=t_frame)
+    t_pre_bin = t1 - t0
+    t_fwd = t2 - t1
+    t_bwd = t3 - t2
+    t_frame = t_fwd + t_bwd
+    return dict(value=round(1.0 / t_frame, 5), unit="frames/s", cores=threads, kind="port",
+                cpu_model=cpu_model(), host_cpus=os.cpu_count(),
+                sample=f"whole cfg3 frame, oracle/lsr_oracle.c on {threads} OpenMP threads: forward {t_fwd:.2f}s "
+                       f"(of which preprocess + binning {t_pre_bin:.2f}s, single-threaded), backward {t_bwd:.2f}s "
+                       f"(render bwd on {threads} threads + preprocess bwd)",
+                seconds_per_frame=round(t_frame, 3), stages_s=dict(preprocess_binning=round(t_pre_bin, 3),
+                                                                  forward=round(t_fwd, 3), backward=round(t_bwd, 3)))
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters
 
 
 def fwd_fps(g, dev, sh_degree, D, W=1280, H=800, iters=20):
     cam = make_camera(W, H)
     rs = settings(cam, dev, sh_degree, D > 0)
     r = GaussianRasterizer(rs)
-    with torch.no_grad():
-        for _ in range(3):
+
+    def run():
+        with torch.no_grad():
             r(means3D=g["means3D"], means2D=g["means2D"], opacities=g["opacities"], shs=g["shs"],
               language_feature_precomp=g.get("language_feature_precomp"), scales=g["scales"],
               rotations=g["rotations"])
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            r(means3D=g["means3D"], means2D=g["means2D"], opacities=g["opacities"], shs=g["shs"],
-              language_feature_precomp=g.get("language_feature_precomp"), scales=g["scales"],
-              rotations=g["rotations"])
-        torch.cuda.synchronize()
-    return iters / (time.perf_counter() - t0)
+    return 1.0 / timeit(run, iters)
 
 
-def main():
+def quick_fps(N, dev, W=1280, H=800, iters=20):
+    """The evaluation path behind the reference's "450+ FPS" (README.md:1, eval_lerf.py:210-220):
+    quick render of 3 levels x top-4 codes into 192 channels, then the 3 x 64 x 512 codebook
+    decode + L2 normalise, at 1.0 Mpix."""
+    from langsplatv2_amd import quick
+    cam = make_camera(W, H)
+    g = make_gaussians(N, cam, seed=0, sh_degree=3, quick_k=4)
+    t = {k: v.to(dev) for k, v in g.items() if isinstance(v, torch.Tensor)}
+    r = GaussianRasterizer(settings(cam, dev, 3, False, quick=True))
+    z = torch.zeros_like(t["means3D"])
+    cb = torch.randn(3, 64, 512, device=dev)
+
+    def render():
+        with torch.no_grad():
+            return r(means3D=t["means3D"], means2D=z, opacities=t["opacities"], shs=t["shs"],
+                     language_feature_weights_quick=t["language_feature_weights_quick"],
+                     language_feature_indices=t["language_feature_indices"], scales=t["scales"],
+                     rotations=t["rotations"])[1]
+
+    def both():
+        quick.decode_language_features(render(), cb)
+    s_render = timeit(render, iters)
+    s_total = timeit(both, iters)
+    return dict(workload=f"{N} Gaussians {W}x{H}, quick 3x top-4 -> 192 ch + 3x64x512 decode + L2 norm",
+                render_fps=round(1.0 / s_render, 1), render_decode_fps=round(1.0 / s_total, 1),
+                render_ms=round(s_render * 1e3, 4), decode_ms=round((s_total - s_render) * 1e3, 4))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args) -> int:
+    """--gpus N > 1 without a launcher: start N ranks as a torch.distributed.run child (no
+    GPU call has happened in this process) and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(world, rank) -> int:
+    """Rank bring-up only (gloo, no GPU): every rank reports (rank, world size) to rank 0."""
+    if world > 1:
+        dist.init_process_group("gloo")
+        seen = [None] * world
+        dist.all_gather_object(seen, (rank, dist.get_world_size()))
+        dist.destroy_process_group()
+    else:
+        seen = [(0, 1)]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": sorted(r for r, _ in seen),
+                          "world_sizes_seen": sorted({w for _, w in seen})}), flush=True)
+    return 0
+
+
+def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -173,13 +273,23 @@ def main():
     ap.add_argument("--config", type=int, default=3, choices=[3])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fwd-1mpix", action="store_true")
+    ap.add_argument("--no-quick", action="store_true")
+    ap.add_argument("--dry-run", action="store_true", help="bring the ranks up on gloo and exit (no GPU)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if args.dry_run:
+        return dry_run(world, rank)
     if world > 1:
         dist.init_process_group("nccl")
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: RCCL sees {dist.get_world_size()} ranks, expected {args.gpus}")
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     _lib.load()
@@ -194,37 +304,48 @@ def main():
     leaf_keys = ("means3D", "shs", "opacities", "scales", "rotations", "language_feature_precomp")
     g = {k: gcpu[k].to(dev).requires_grad_(True) for k in leaf_keys}
     g["means2D"] = torch.zeros_like(g["means3D"], requires_grad=True)
-    params = [g[k] for k in leaf_keys] + [g["means2D"]]
+    leaves = [g[k] for k in leaf_keys]
+    inputs = leaves + [g["means2D"]]
     gen = torch.Generator(device="cpu").manual_seed(1 + rank)
     dcolor = torch.randn((3, H, W), generator=gen).to(dev)
     dlang = torch.randn((D, H, W), generator=gen).to(dev)
     rs = settings(cam, dev, deg, True)
     rast = GaussianRasterizer(rs)
-    leaves = [g[k] for k in leaf_keys]
-    exch = dp.ViewShardedExchange(leaves, with_stats=True) if world > 1 else None
+    exch = dp.ViewShardedExchange(leaves, with_stats=True, names=leaf_keys) if world > 1 else None
+    xev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+    xms = [0.0, 0]
 
-    def step():
-        for p in params:
-            p.grad = None
+    def step(timed_exchange=False):
         color, lang, radii = rast(means3D=g["means3D"], means2D=g["means2D"], opacities=g["opacities"],
                                   shs=g["shs"], language_feature_precomp=g["language_feature_precomp"],
                                   scales=g["scales"], rotations=g["rotations"])
-        torch.autograd.backward([color, lang], [dcolor, dlang])
-        if exch is not None:
-            # one flat all-reduce(SUM) of every gradient + densification stats, one MAX of radii
-            exch.exchange([p.grad for p in leaves], g["means2D"].grad, radii)
+        if exch is None:
+            return torch.autograd.grad([color, lang], inputs, [dcolor, dlang])
+        # gradients land in the all-reduce buckets; the language bucket's all-reduce
+        # starts on a side stream as soon as the render backward has finished it
+        with exch.sink():
+            grads = torch.autograd.grad([color, lang], inputs, [dcolor, dlang])
+        if timed_exchange:
+            xev[0].record()
+        red, _, _ = exch.finish(grads[-1], radii, grads[:-1])
+        if timed_exchange:
+            xev[1].record()
+            xev[1].synchronize()
+            xms[0] += xev[0].elapsed_time(xev[1])
+            xms[1] += 1
+        return red
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # per-stage breakdown: a separate untimed pass with every stage bracketed
-    # by events (each bracket idles the stream a few us, so the timed region
+    # per-stage breakdown (+ the exposed exchange time): a separate untimed pass with every
+    # stage bracketed by events (each bracket idles the stream a few us, so the timed region
     # below brackets only the dominant stage, for the live roofline)
     _lib.profile_stages(None)
     _lib.profile_reset()
     _lib.profile_enable(True)
     for _ in range(max(2, min(args.steps, 5))):
-        step()
+        step(timed_exchange=True)
     torch.cuda.synchronize()
     _lib.profile_enable(False)
     stages = _lib.profile_query()
@@ -286,7 +407,11 @@ def main():
                 "global_batch": world, "parallelism": f"dp{world} (views sharded, RCCL all-reduce of grads)"
                 if world > 1 else "single GPU",
             },
-            "exchange": ({"bucket_bytes": exch.bucket.nbytes, **dp.allreduce_bound_ms(exch.bucket.nbytes, world)}
+            "ranks_seen": dist.get_world_size() if world > 1 else 1,
+            "exchange": ({"bucket_bytes": exch.bucket_bytes,
+                          "early_bucket_bytes": exch.early.nbytes if exch.early is not None else 0,
+                          "exposed_ms_per_step": round(xms[0] / max(xms[1], 1), 4),
+                          **{k: round(v, 4) for k, v in dp.allreduce_bound_ms(exch.bucket_bytes, world).items()}}
                          if exch is not None else None),
             "roofline": {
                 "bound": "hbm",
@@ -298,27 +423,30 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": int(bytes_[dom]),
+                "bytes_formula": "SURVEY.md §8d (bench.py:algorithmic_bytes)",
                 "ms_per_launch": round(dom_ms, 4),
                 "launches_timed": dom_calls,
             },
             "hbm_step": {"algorithmic_bytes": int(total_bytes),
                          "GBps_over_kernels": round(total_bytes / (kernel_ms * 1e-3) / 1e9, 1) if kernel_ms else 0,
-                         "GBps_over_step": round(total_bytes / (step_ms * 1e-3) / 1e9, 1)},
+                         "GBps_over_step": round(total_bytes / (step_ms * 1e-3) / 1e9, 1),
+                         "frac_over_step": round(total_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)},
             "stages_ms": {k: round(v["ms_per_launch"], 4) for k, v in per_stage.items()},
             "stage_bytes": {k: int(v) for k, v in bytes_.items()},
             "workload_stats": info,
         }
         if world == 1 and not args.no_fwd_1mpix:
-            gg = dict(g)
-            out["fwd_fps_1mpix"] = round(fwd_fps({k: v.detach() for k, v in gg.items()}, dev, deg, D), 1)
+            out["fwd_fps_1mpix"] = round(fwd_fps({k: v.detach() for k, v in g.items()}, dev, deg, D), 1)
+        if world == 1 and not args.no_quick:
+            out["quick_1mpix"] = quick_fps(N, dev)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cam, gcpu, D)
-            out["cpu_baseline"]["value"] = round(out["cpu_baseline"]["value"], 5)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 3
+#define LSR_ABI_VERSION 4
 
 enum {
     LSR_OK = 0,
@@ -50,7 +50,8 @@ enum {
     LSR_EUNSUPPORTED = 2,  /* e.g. language dim beyond the compiled channel sets */
     LSR_EHIP = 3,          /* HIP launch / runtime failure */
     LSR_ENOMEM = 4,        /* alloc callback returned NULL */
-    LSR_EOVERFLOW = 5      /* num_rendered does not fit 32-bit instance indices */
+    LSR_EOVERFLOW = 5,     /* num_rendered does not fit 32-bit instance indices */
+    LSR_ENONFINITE = 6     /* debug guard: NaN/Inf in an input or output */
 };
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:37-52),
@@ -100,7 +101,7 @@ typedef struct lsr_inputs {
  * the last pointer returned for a kind is the one the call uses. */
 typedef void* (*lsr_alloc_fn)(void* ctx, size_t bytes, int which);
 enum { LSR_BUF_GEOM = 0, LSR_BUF_BINNING = 1, LSR_BUF_IMAGE = 2, LSR_BUF_GRAD = 3, LSR_BUF_DECODE = 4,
-       LSR_BUF_KNN = 5, LSR_BUF_LOSS = 6 };
+       LSR_BUF_KNN = 5, LSR_BUF_LOSS = 6, LSR_BUF_GUARD = 7, LSR_BUF_SPARSE = 8 };
 
 typedef struct lsr_fwd_out {
     float* out_color;     /* (3,H,W)  caller-allocated */
@@ -114,7 +115,9 @@ typedef struct lsr_fwd_out {
 } lsr_fwd_out;
 
 /* _C.rasterize_gaussians: preprocess → binning (tile buckets + per-tile depth
- * sort) → per-pixel alpha blend of RGB + language channels. */
+ * sort) → per-pixel alpha blend of RGB + language channels.  With
+ * settings.debug set, inputs and outputs are also scanned for NaN/Inf
+ * (LSR_ENONFINITE). */
 int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out,
                 lsr_alloc_fn alloc, void* alloc_ctx, void* stream);
 
@@ -140,9 +143,20 @@ typedef struct lsr_bwd_out {
     float* dL_dsh;          /* (N,M,3) */
     float* dL_dscales;      /* (N,3) */
     float* dL_drotations;   /* (N,4) */
+    /* Quick (sparse) language input with a gradient: with
+     * quick_render set, dL/dlanguage_feature_weights_quick (N,K),
+     *   dL/dw[j][m] = sum_p alpha_j(p) T_j(p) dL/dout_lang[idx[j][m]][p];
+     * the indices are not differentiable. */
+    float* dL_dlang_weights;
+    /* Optional hipEvent_t, recorded on `stream` as soon as dL_dlang /
+     * dL_dlang_weights are final (before the preprocess backward), so a
+     * data-parallel caller can start their all-reduce early (§8e). */
+    void* lang_ready_event;
 } lsr_bwd_out;
 
-/* _C.rasterize_gaussians_backward. */
+/* _C.rasterize_gaussians_backward.  With settings.debug set, every stage is
+ * synchronised and checked, and inputs / outputs are scanned for NaN/Inf
+ * (LSR_ENONFINITE; the offending array is named on stderr). */
 int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* b,
                  lsr_bwd_out* out, lsr_alloc_fn alloc, void* alloc_ctx, void* stream);
 
@@ -181,6 +195,12 @@ int lsr_topk_code_forward(const float* logits, int64_t N, int L, int K, int k, f
  * softmax_to_topk_soft_code (mask recomputed from the logits). */
 int lsr_topk_code_backward(const float* logits, const float* grad_dense, int64_t N, int L, int K, int k,
                            float* grad_logits, void* stream);
+/* dL/dlogits (N, L*K) from dL/dsparse_w (N, L*k): the gradient of the packed
+ * weights (ascending channel order, as lsr_topk_code_forward's sparse_w),
+ * e.g. lsr_bwd_out.dL_dlang_weights of a quick-mode render; the dense code
+ * gradient is never formed (the sparse training path). */
+int lsr_topk_code_backward_sparse(const float* logits, const float* grad_weights, int64_t N, int L, int K, int k,
+                                  float* grad_logits, void* stream);
 
 /* Language-feature cosine loss of the feature-mode training step (SURVEY
  * §8f rank 4; train.py:151-164 with vq_layer_num = 1, layer_idx = 0):
@@ -229,7 +249,9 @@ int lsr_abi_version(void);
 int lsr_max_lang_dim(void);
 
 /* Diagnostics: per-stage HIP-event timing on the caller's stream (used by
- * bench.py for the live roofline).  Not thread-safe; off by default.
+ * bench.py for the live roofline).  The timing state is per host thread
+ * (thread_local): each thread enables, resets and queries its own stages;
+ * off by default.
  * lsr_profile_query fills up to max_stages (name, total ms, call count)
  * triples since the last reset and returns the number filled. */
 void lsr_profile_enable(int on);

@@ -14,7 +14,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSR_LIB", os.path.join(_HERE, "liblsr.so"))
 
 LSR_OK = 0
+LSR_ENONFINITE = 6
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_GRAD, LSR_BUF_DECODE, LSR_BUF_KNN, LSR_BUF_LOSS = 0, 1, 2, 3, 4, 5, 6
+LSR_BUF_GUARD, LSR_BUF_SPARSE = 7, 8
 LSR_INDEX_F32, LSR_INDEX_I32, LSR_INDEX_I64 = 0, 1, 2
 
 _vp = ctypes.c_void_p
@@ -98,13 +100,15 @@ class BwdOut(ctypes.Structure):
         ("dL_dsh", _vp),
         ("dL_dscales", _vp),
         ("dL_drotations", _vp),
+        ("dL_dlang_weights", _vp),
+        ("lang_ready_event", _vp),
     ]
 
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
 
 EXPORTS = ("lsr_forward", "lsr_backward", "lsr_mark_visible", "lsr_quick_decode", "lsr_topk_code_forward",
-           "lsr_topk_code_backward", "lsr_knn_dist2", "lsr_lang_loss_forward", "lsr_lang_loss_backward", "lsr_adam_step", "lsr_strerror",
+           "lsr_topk_code_backward", "lsr_topk_code_backward_sparse", "lsr_knn_dist2", "lsr_lang_loss_forward", "lsr_lang_loss_backward", "lsr_adam_step", "lsr_strerror",
            "lsr_abi_version", "lsr_max_lang_dim", "lsr_profile_enable", "lsr_profile_stages", "lsr_profile_reset",
            "lsr_profile_query")
 
@@ -140,6 +144,9 @@ def load(path: str | None = None):
     lib.lsr_topk_code_backward.argtypes = [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp,
                                            _vp]
     lib.lsr_topk_code_backward.restype = ctypes.c_int
+    lib.lsr_topk_code_backward_sparse.argtypes = [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                  _vp, _vp]
+    lib.lsr_topk_code_backward_sparse.restype = ctypes.c_int
     lib.lsr_knn_dist2.argtypes = [_vp, ctypes.c_int64, _vp, ALLOC_FN, _vp, _vp]
     lib.lsr_knn_dist2.restype = ctypes.c_int
     _ci = ctypes.c_int

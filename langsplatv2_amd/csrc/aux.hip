@@ -1,0 +1,84 @@
+// aux.hip — small streaming kernels around the render path:
+//
+//  * k_nonfinite: the debug-mode NaN/Inf guard (SURVEY.md §5 "Failure
+//    detection": C-ABI status codes + a NaN/Inf guard option).  With
+//    settings.debug the driver scans every input and output array once per
+//    call and returns LSR_ENONFINITE naming the first offending array; the
+//    reference's nearest hooks are pipe.debug (gaussian_renderer/__init__.py:49)
+//    and --detect_anomaly (train.py:362).
+//  * k_sparse_expand / k_sparse_gather: the quick (sparse) language input
+//    (weights (N,K), indices (N,K), utils/vq_utils.py:26-40) expanded to dense
+//    (N,Dq) rows, and the dense language gradient gathered back to dL/dweights.
+//    Used only by the geometry-and-language backward in quick mode; the
+//    language-only quick backward (the training path) never forms dense rows.
+// All HBM-streaming, grid-stride, one pass.
+#include "lsr_internal.h"
+
+namespace lsr {
+
+__global__ void __launch_bounds__(256) k_nonfinite(const float* __restrict__ p, size_t n, uint32_t* __restrict__ flag)
+{
+    const size_t stride = (size_t)gridDim.x * 256;
+    bool bad = false;
+    const size_t n4 = ((uintptr_t)p & 15) == 0 ? n / 4 : 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+        const float4 v = reinterpret_cast<const float4*>(p)[i];
+        bad |= !(isfinite(v.x) && isfinite(v.y) && isfinite(v.z) && isfinite(v.w));
+    }
+    for (size_t i = 4 * n4 + (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) bad |= !isfinite(p[i]);
+    if (wave_any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
+hipError_t launch_nonfinite(const float* p, size_t n, uint32_t* flag, hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    const size_t blocks = (n / 4 + 255) / 256;
+    k_nonfinite<<<(unsigned)(blocks < 2048 ? (blocks > 0 ? blocks : 1) : 2048), 256, 0, st>>>(p, n, flag);
+    return hipGetLastError();
+}
+
+// dense[j][q] = sum over m with idx[j][m] == q of w[j][m] (out-of-range codes
+// dropped, as the quick forward drops them); one thread per row.
+__global__ void __launch_bounds__(256) k_sparse_expand(const float* __restrict__ qw, const void* __restrict__ qi,
+                                                       int dtype, int N, int K, int Dq, float* __restrict__ dense)
+{
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= N) return;
+    float* row = dense + (size_t)j * Dq;
+    for (int q = 0; q < Dq; q++) row[q] = 0.f;
+    for (int m = 0; m < K; m++) {
+        const size_t off = (size_t)j * K + m;
+        const int q = quick_index(qi, dtype, off);
+        if (q >= 0 && q < Dq) row[q] += qw[off];
+    }
+}
+
+// dw[j][m] = dense_grad[j][idx[j][m]] (0 for out-of-range codes)
+__global__ void __launch_bounds__(256) k_sparse_gather(const float* __restrict__ g, const void* __restrict__ qi,
+                                                       int dtype, int64_t NK, int K, int Dq, float* __restrict__ dw)
+{
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= NK) return;
+    const int64_t j = e / K;
+    const int q = quick_index(qi, dtype, (size_t)e);
+    dw[e] = (q >= 0 && q < Dq) ? g[(size_t)j * Dq + q] : 0.f;
+}
+
+hipError_t launch_sparse_expand(const float* qw, const void* qi, int dtype, int N, int K, int Dq, float* dense,
+                                hipStream_t st)
+{
+    if (N == 0) return hipSuccess;
+    k_sparse_expand<<<(N + 255) / 256, 256, 0, st>>>(qw, qi, dtype, N, K, Dq, dense);
+    return hipGetLastError();
+}
+
+hipError_t launch_sparse_gather(const float* g, const void* qi, int dtype, int N, int K, int Dq, float* dw,
+                                hipStream_t st)
+{
+    const int64_t NK = (int64_t)N * K;
+    if (NK == 0) return hipSuccess;
+    k_sparse_gather<<<(unsigned)((NK + 255) / 256), 256, 0, st>>>(g, qi, dtype, NK, K, Dq, dw);
+    return hipGetLastError();
+}
+
+}  // namespace lsr

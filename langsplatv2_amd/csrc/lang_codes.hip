@@ -202,7 +202,10 @@ __global__ void __launch_bounds__(256) k_topk_code_fwd(const float* __restrict__
 //   d = s + 1e-10, code_j = mask_j y_j / d
 //   dL/dy_j = mask_j (g_j / d - sum_i g_i code_i / d)      (division + sum)
 //   dL/dx   = y (dL/dy - sum_i dL/dy_i y_i)                  (softmax)
-template <int Q>
+// SPARSE: g is dL/dweights of the packed form (rows, k), the selected
+// channels in ascending channel order (the forward's sparse output order);
+// the dense (rows, K) code gradient is never formed.
+template <int Q, bool SPARSE>
 __global__ void __launch_bounds__(256) k_topk_code_bwd(const float* __restrict__ logits, const float* __restrict__ g,
                                                         int64_t rows, int k, float* __restrict__ dlogits)
 {
@@ -213,10 +216,28 @@ __global__ void __launch_bounds__(256) k_topk_code_bwd(const float* __restrict__
     CodeRow<Q> cr;
     cr.build(logits + (live ? row : 0) * K, j, k, live);
     float gv[Q][4];
+    if constexpr (SPARSE) {
+        int before = 0;
 #pragma unroll
-    for (int q = 0; q < Q; q++) {
-        const float4 v = live ? reinterpret_cast<const float4*>(g + row * K + 64 * q)[j] : make_float4(0.f, 0.f, 0.f, 0.f);
-        gv[q][0] = v.x; gv[q][1] = v.y; gv[q][2] = v.z; gv[q][3] = v.w;
+        for (int q = 0; q < Q; q++) {
+            const uint64_t bits = grp_or64((uint64_t)cr.sel[q] << (4 * j));
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                gv[q][r] = 0.f;
+                if (live && ((cr.sel[q] >> r) & 1u)) {
+                    const int w = 4 * j + r;
+                    const int rank = before + __popcll(bits & ((1ull << w) - 1ull));
+                    gv[q][r] = g[row * k + rank];
+                }
+            }
+            before += __popcll(bits);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            const float4 v = live ? reinterpret_cast<const float4*>(g + row * K + 64 * q)[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+            gv[q][0] = v.x; gv[q][1] = v.y; gv[q][2] = v.z; gv[q][3] = v.w;
+        }
     }
     const float d = cr.s + 1e-10f;
     float gc = 0.f;
@@ -265,18 +286,22 @@ hipError_t launch_topk_code_fwd(const float* logits, int64_t N, int L, int K, in
 }
 
 hipError_t launch_topk_code_bwd(const float* logits, const float* g, int64_t N, int L, int K, int k, float* dlogits,
-                                hipStream_t st)
+                                hipStream_t st, bool sparse)
 {
     const int64_t rows = N * L;
     if (rows == 0) return hipSuccess;
     const unsigned nb = (unsigned)((rows + CODE_ROWS_PER_BLOCK - 1) / CODE_ROWS_PER_BLOCK);
+#define LSR_TOPK_BWD(Q)                                                                          \
+    (sparse ? (k_topk_code_bwd<Q, true><<<nb, 256, 0, st>>>(logits, g, rows, k, dlogits), 0)      \
+            : (k_topk_code_bwd<Q, false><<<nb, 256, 0, st>>>(logits, g, rows, k, dlogits), 0))
     switch (K / 64) {
-        case 1: k_topk_code_bwd<1><<<nb, 256, 0, st>>>(logits, g, rows, k, dlogits); break;
-        case 2: k_topk_code_bwd<2><<<nb, 256, 0, st>>>(logits, g, rows, k, dlogits); break;
-        case 3: k_topk_code_bwd<3><<<nb, 256, 0, st>>>(logits, g, rows, k, dlogits); break;
-        case 4: k_topk_code_bwd<4><<<nb, 256, 0, st>>>(logits, g, rows, k, dlogits); break;
+        case 1: LSR_TOPK_BWD(1); break;
+        case 2: LSR_TOPK_BWD(2); break;
+        case 3: LSR_TOPK_BWD(3); break;
+        case 4: LSR_TOPK_BWD(4); break;
         default: return hipErrorInvalidValue;
     }
+#undef LSR_TOPK_BWD
     return hipGetLastError();
 }
 

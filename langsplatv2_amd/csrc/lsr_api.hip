@@ -61,7 +61,7 @@ struct Prof {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[ST_N];
     size_t used[ST_N] = {};
 };
-Prof g_prof;
+thread_local Prof g_prof;   // per host thread: no state shared between callers
 
 struct StageScope {
     Stage s;
@@ -85,6 +85,60 @@ struct StageScope {
         g_prof.used[s]++;
     }
 };
+
+// Debug-mode NaN/Inf guard: one streaming scan per array, a
+// synchronous read of the flag, LSR_ENONFINITE naming the array.  Off unless
+// settings.debug (which already synchronises after every stage).
+struct Guard {
+    const lsr_settings* s;
+    lsr_alloc_fn alloc;
+    void* ctx;
+    hipStream_t st;
+    uint32_t* flag = nullptr;
+    Guard(const lsr_settings* s_, lsr_alloc_fn a_, void* c_, hipStream_t st_) : s(s_), alloc(a_), ctx(c_), st(st_) {}
+    int check(const char* what, const float* p, size_t n)
+    {
+        if (!s->debug || !p || n == 0) return LSR_OK;
+        if (!flag) {
+            if (!alloc) return LSR_EINVAL;
+            flag = (uint32_t*)alloc(ctx, 256, LSR_BUF_GUARD);
+            if (!flag) return LSR_ENOMEM;
+        }
+        uint32_t h = 0;
+        LSR_HIP(hipMemsetAsync(flag, 0, 4, st));
+        LSR_HIP(launch_nonfinite(p, n, flag, st));
+        LSR_HIP(hipMemcpyAsync(&h, flag, 4, hipMemcpyDeviceToHost, st));
+        LSR_HIP(hipStreamSynchronize(st));
+        if (h) {
+            fprintf(stderr, "[lsr] non-finite values (NaN/Inf) in %s\n", what);
+            return LSR_ENONFINITE;
+        }
+        return LSR_OK;
+    }
+};
+
+#define LSR_GUARD(g, what, p, n)                          \
+    do {                                                  \
+        const int _rc = (g).check((what), (p), (n));      \
+        if (_rc != LSR_OK) return _rc;                    \
+    } while (0)
+
+int guard_inputs(Guard& g, const lsr_settings* s, const lsr_inputs* in)
+{
+    const size_t P = (size_t)in->P;
+    LSR_GUARD(g, "means3D", in->means3D, P * 3);
+    LSR_GUARD(g, "opacities", in->opacities, P);
+    LSR_GUARD(g, "shs", in->shs, P * (size_t)in->max_coeffs * 3);
+    LSR_GUARD(g, "colors_precomp", in->colors_precomp, P * 3);
+    LSR_GUARD(g, "scales", in->scales, P * 3);
+    LSR_GUARD(g, "rotations", in->rotations, P * 4);
+    LSR_GUARD(g, "cov3D_precomp", in->cov3D_precomp, P * 6);
+    if (s->include_feature && !s->quick_render)
+        LSR_GUARD(g, "language_feature_precomp", in->language_feature_precomp, P * (size_t)in->lang_dim);
+    if (s->quick_render)
+        LSR_GUARD(g, "language_feature_weights_quick", in->language_feature_weights_quick, P * (size_t)in->quick_k);
+    return LSR_OK;
+}
 
 int dense_dim(const lsr_settings* s, const lsr_inputs* in)
 {
@@ -187,6 +241,7 @@ const char* lsr_strerror(int code)
         case LSR_EHIP: return "HIP runtime or kernel launch failure";
         case LSR_ENOMEM: return "workspace allocation failed";
         case LSR_EOVERFLOW: return "num_rendered exceeds 32-bit instance indexing";
+        case LSR_ENONFINITE: return "non-finite (NaN/Inf) values in an input or output (debug guard)";
         default: return "unknown error";
     }
 }
@@ -299,6 +354,18 @@ int lsr_topk_code_backward(const float* logits, const float* grad_dense, int64_t
     if (N == 0) return LSR_OK;
     if (!logits || !grad_dense || !grad_logits) return LSR_EINVAL;
     if (lsr::launch_topk_code_bwd(logits, grad_dense, N, L, K, k, grad_logits, (hipStream_t)stream) != hipSuccess)
+        return LSR_EHIP;
+    return LSR_OK;
+}
+
+int lsr_topk_code_backward_sparse(const float* logits, const float* grad_weights, int64_t N, int L, int K, int k,
+                                  float* grad_logits, void* stream)
+{
+    if (!topk_code_args_ok(N, L, K, k)) return (K % 64 || K > 256) && K > 0 ? LSR_EUNSUPPORTED : LSR_EINVAL;
+    if (N == 0) return LSR_OK;
+    if (!logits || !grad_weights || !grad_logits) return LSR_EINVAL;
+    if (lsr::launch_topk_code_bwd(logits, grad_weights, N, L, K, k, grad_logits, (hipStream_t)stream, true) !=
+        hipSuccess)
         return LSR_EHIP;
     return LSR_OK;
 }
@@ -440,6 +507,10 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     const int T = c.gx * c.gy;
     const size_t NPIX = (size_t)c.W * c.H;
 
+    Guard guard(s, alloc, ctx, st);
+    rc = guard_inputs(guard, s, in);
+    if (rc != LSR_OK) return rc;
+
     const GeomLayout GL = geom_layout((size_t)P);
     const ImageLayout IL = image_layout(NPIX, (size_t)T);
     // privatised binning needs a B x T table (tail of the image workspace)
@@ -557,7 +628,119 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     ra.out_lang = out->out_lang;
     { StageScope sc(ST_RENDER, st); LSR_HIP(launch_render_fwd(ra, st)); }
     LSR_DEBUG_SYNC(s, st, "render");
+    LSR_GUARD(guard, "out_color", out->out_color, 3 * NPIX);
+    LSR_GUARD(guard, "out_lang", out->out_lang, (size_t)(s->quick_render ? quick_dim(s) : Dd) * NPIX);
     return LSR_OK;
+}
+
+static int guard_bwd_outputs(Guard& g, const lsr_inputs* in, const lsr_bwd_out* o, int D)
+{
+    const size_t P = (size_t)in->P;
+    LSR_GUARD(g, "dL_dmeans2D", o->dL_dmeans2D, P * 3);
+    LSR_GUARD(g, "dL_dcolors", o->dL_dcolors, P * 3);
+    LSR_GUARD(g, "dL_dlang", o->dL_dlang, P * (size_t)D);
+    LSR_GUARD(g, "dL_dopacity", o->dL_dopacity, P);
+    LSR_GUARD(g, "dL_dmeans3D", o->dL_dmeans3D, P * 3);
+    LSR_GUARD(g, "dL_dcov3D", o->dL_dcov3D, P * 6);
+    LSR_GUARD(g, "dL_dsh", o->dL_dsh, P * (size_t)in->max_coeffs * 3);
+    LSR_GUARD(g, "dL_dscales", o->dL_dscales, P * 3);
+    LSR_GUARD(g, "dL_drotations", o->dL_drotations, P * 4);
+    LSR_GUARD(g, "dL_dlang_weights", o->dL_dlang_weights, P * (size_t)in->quick_k);
+    return LSR_OK;
+}
+
+static bool geometry_requested(const lsr_bwd_out* o)
+{
+    return o->dL_dmeans2D || o->dL_dcolors || o->dL_dopacity || o->dL_dmeans3D || o->dL_dcov3D || o->dL_dsh ||
+           o->dL_dscales || o->dL_drotations;
+}
+
+static int record_lang_ready(const lsr_bwd_out* out, hipStream_t st)
+{
+    if (out->lang_ready_event) LSR_HIP(hipEventRecord((hipEvent_t)out->lang_ready_event, st));
+    return LSR_OK;
+}
+
+// Quick (sparse) language input: weights (P,K) + codes (P,K) rendered into
+// Dq channels.  dL/dweights[j][m] = sum_p aT_j(p) dL/dout_lang[idx[j][m]][p].
+//  - weights alone requested (feature-mode training, geometry frozen): the
+//    language-only render backward gathers the channel gradients at the codes
+//    (no dense (P,Dq) rows anywhere);
+//  - geometry requested too: the quick channels take part in dL/dalpha when
+//    their upstream gradient is given, so the sparse rows are expanded to
+//    dense (P,Dq) rows and the dense backward runs (Dq <= 64), dL/dweights
+//    gathered from its dL/dlang; without an upstream language gradient the
+//    backward is the RGB-only one.
+static int backward_quick(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* b, lsr_bwd_out* out,
+                          lsr_alloc_fn alloc, void* ctx, hipStream_t st, Guard& guard)
+{
+    const int P = in->P;
+    const int Dq = quick_dim(s);
+    float* dw = out->dL_dlang_weights;
+    const bool geom = geometry_requested(out);
+    if (!dw && !geom) return record_lang_ready(out, st);
+    if (dw && !b->dL_dout_lang) return LSR_EINVAL;
+    if (dw && !geom) {
+        if (lang_set_for(Dq) < 0) return LSR_EUNSUPPORTED;
+        const Cam c = make_cam(s);
+        RenderBwdArgs rb;
+        rb.f = make_render_args(s, in, c, (const uint8_t*)b->geom, (const uint8_t*)b->binning,
+                                (const uint8_t*)b->image, b->num_rendered);
+        rb.f.D = Dq;
+        rb.f.lang = nullptr;
+        rb.dout_color = b->dL_dout_color;
+        rb.dout_lang = b->dL_dout_lang;
+        rb.grad_acc = nullptr;
+        rb.VP = Dq;
+        rb.qw_acc = dw;
+        { StageScope sc(ST_GZERO, st); LSR_HIP(hipMemsetAsync(dw, 0, (size_t)P * in->quick_k * 4, st)); }
+        { StageScope sc(ST_RENDER_BWD, st); LSR_HIP(launch_render_bwd_lang_sparse(rb, st)); }
+        LSR_DEBUG_SYNC(s, st, "render_bwd_lang_sparse");
+        int rc = record_lang_ready(out, st);
+        if (rc != LSR_OK) return rc;
+        return guard_bwd_outputs(guard, in, out, 0);
+    }
+    lsr_settings s2 = *s;
+    s2.quick_render = 0;
+    s2.quick_dim = 0;
+    lsr_inputs in2 = *in;
+    in2.quick_k = 0;
+    in2.language_feature_weights_quick = nullptr;
+    in2.language_feature_indices = nullptr;
+    lsr_bwd_out o2 = *out;
+    o2.dL_dlang_weights = nullptr;
+    o2.lang_ready_event = nullptr;
+    lsr_bwd_in b2 = *b;
+    float* dense_grad = nullptr;
+    if (b->dL_dout_lang) {
+        if (lang_set_for(Dq) < 0) return LSR_EUNSUPPORTED;
+        const size_t row = (size_t)P * Dq * 4;
+        uint8_t* ws = (uint8_t*)alloc(ctx, align256(row) + (dw ? row : 0), LSR_BUF_SPARSE);
+        if (!ws) return LSR_ENOMEM;
+        float* dense = (float*)ws;
+        dense_grad = dw ? (float*)(ws + align256(row)) : nullptr;
+        LSR_HIP(launch_sparse_expand(in->language_feature_weights_quick, in->language_feature_indices,
+                                     in->quick_index_dtype, P, in->quick_k, Dq, dense, st));
+        s2.include_feature = 1;
+        in2.lang_dim = Dq;
+        in2.language_feature_precomp = dense;
+        o2.dL_dlang = dense_grad;
+    } else {
+        s2.include_feature = 0;
+        in2.lang_dim = 0;
+        in2.language_feature_precomp = nullptr;
+        o2.dL_dlang = nullptr;
+        b2.dL_dout_lang = nullptr;
+        if (dw) LSR_HIP(hipMemsetAsync(dw, 0, (size_t)P * in->quick_k * 4, st));
+    }
+    int rc = lsr_backward(&s2, &in2, &b2, &o2, alloc, ctx, st);
+    if (rc != LSR_OK) return rc;
+    if (dw && dense_grad)
+        LSR_HIP(launch_sparse_gather(dense_grad, in->language_feature_indices, in->quick_index_dtype, P, in->quick_k,
+                                     Dq, dw, st));
+    rc = record_lang_ready(out, st);
+    if (rc != LSR_OK) return rc;
+    return guard_bwd_outputs(guard, in, out, 0);
 }
 
 int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* b, lsr_bwd_out* out,
@@ -568,17 +751,22 @@ int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* 
     if (!b || !out || !alloc || !b->geom || !b->image || !b->binning || !b->dL_dout_color) return LSR_EINVAL;
     const int Dd = dense_dim(s, in);
     if (Dd > 0 && !b->dL_dout_lang) return LSR_EINVAL;
+    if (out->dL_dlang_weights && !s->quick_render) return LSR_EINVAL;
+    if (s->quick_render && out->dL_dlang) return LSR_EINVAL;   // the quick input has no dense rows
     if (in->P == 0) return LSR_OK;
     if (!b->radii) return LSR_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     const Cam c = make_cam(s);
     const int P = in->P;
+    const size_t NPIX = (size_t)c.W * c.H;
+    Guard guard(s, alloc, ctx, st);
+    LSR_GUARD(guard, "dL_dout_color", b->dL_dout_color, 3 * NPIX);
+    LSR_GUARD(guard, "dL_dout_lang", b->dL_dout_lang, (size_t)(s->quick_render ? quick_dim(s) : Dd) * NPIX);
+    if (s->quick_render) return backward_quick(s, in, b, out, alloc, ctx, st, guard);
     // Only dL/dlanguage requested (feature-mode training with frozen geometry
     // and no means2D gradient): the language-only render backward writes the
     // output directly; no gradient rows, no preprocess backward.
-    const bool lang_only = Dd > 0 && out->dL_dlang && !out->dL_dmeans2D && !out->dL_dcolors && !out->dL_dopacity &&
-                           !out->dL_dmeans3D && !out->dL_dcov3D && !out->dL_dsh && !out->dL_dscales &&
-                           !out->dL_drotations;
+    const bool lang_only = Dd > 0 && out->dL_dlang && !geometry_requested(out);
     if (lang_only) {
         RenderBwdArgs rb;
         rb.f = make_render_args(s, in, c, (const uint8_t*)b->geom, (const uint8_t*)b->binning,
@@ -593,7 +781,9 @@ int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* 
         { StageScope sc(ST_GZERO, st); LSR_HIP(hipMemsetAsync(out->dL_dlang, 0, (size_t)P * Dd * 4, st)); }
         { StageScope sc(ST_RENDER_BWD, st); LSR_HIP(launch_render_bwd_lang(rb, st)); }
         LSR_DEBUG_SYNC(s, st, "render_bwd_lang");
-        return LSR_OK;
+        rc = record_lang_ready(out, st);
+        if (rc != LSR_OK) return rc;
+        return guard_bwd_outputs(guard, in, out, Dd);
     }
     // D = 16 / 32 with dL/dlang requested: the render backward adds the
     // language gradients straight into the output; the rows keep geometry +
@@ -611,7 +801,7 @@ int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* 
     RenderBwdArgs rb;
     rb.f = make_render_args(s, in, c, (const uint8_t*)b->geom, (const uint8_t*)b->binning, (const uint8_t*)b->image,
                             b->num_rendered);
-    rb.f.qw = nullptr;  // quick language channels are not differentiated
+    rb.f.qw = nullptr;
     rb.f.D = Dd;
     rb.f.lang = Dd ? in->language_feature_precomp : nullptr;
     rb.dout_color = b->dL_dout_color;
@@ -621,6 +811,11 @@ int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* 
     rb.lang_acc = lang_direct ? out->dL_dlang : nullptr;
     { StageScope sc(ST_RENDER_BWD, st); LSR_HIP(launch_render_bwd(rb, st)); }
     LSR_DEBUG_SYNC(s, st, "render_bwd");
+    // the language gradient is final here unless preprocess_bwd copies it out
+    if (lang_direct || !out->dL_dlang) {
+        rc = record_lang_ready(out, st);
+        if (rc != LSR_OK) return rc;
+    }
 
     lsr_inputs in2 = *in;
     in2.lang_dim = Dd;
@@ -628,7 +823,11 @@ int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* 
     if (!Dd || lang_direct) o2.dL_dlang = nullptr;
     { StageScope sc(ST_PRE_BWD, st); LSR_HIP(launch_preprocess_bwd(c, in2, (const uint8_t*)b->geom, b->radii, gacc, VP, o2, st)); }
     LSR_DEBUG_SYNC(s, st, "preprocess_bwd");
-    return LSR_OK;
+    if (!(lang_direct || !out->dL_dlang)) {
+        rc = record_lang_ready(out, st);
+        if (rc != LSR_OK) return rc;
+    }
+    return guard_bwd_outputs(guard, in, out, Dd);
 }
 
 int lsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, uint8_t* present,

@@ -87,6 +87,16 @@ __device__ __forceinline__ int f2i(float v)
     return (int)v;
 }
 
+// Quick-path code index m of a Gaussian's sparse language row: fp32-encoded
+// integers round half up (u5), int32 as is, int64 outside [0, 2^31) -> -1.
+__device__ __forceinline__ int quick_index(const void* qi, int dtype, size_t off)
+{
+    if (dtype == 0) return f2i(((const float*)qi)[off] + 0.5f);
+    if (dtype == 1) return ((const int32_t*)qi)[off];
+    const int64_t v = ((const int64_t*)qi)[off];
+    return (v < 0 || v > 0x7fffffff) ? -1 : (int)v;
+}
+
 __device__ __forceinline__ float ndc2pix(float v, int S)
 {
     return (float)((((double)v + 1.0) * (double)S - 1.0) * 0.5);

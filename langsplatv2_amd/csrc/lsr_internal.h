@@ -78,6 +78,10 @@ struct RenderBwdArgs {
     // non-null: dL/dlanguage is accumulated straight into this (P, D) output
     // (zeroed by the caller) and the gradient rows hold geometry + colour only
     float* lang_acc = nullptr;
+    // non-null (language-only backward in quick mode): dL/dweights (P, K) of
+    // the sparse input f.qw / f.qi, accumulated with the channel gradient
+    // gathered at each Gaussian's codes (zeroed by the caller)
+    float* qw_acc = nullptr;
 };
 bool bwd_lang_direct(int D);  // D for which the full backward supports lang_acc
 int grad_row_width(int D);   // VP for a dense language dim
@@ -85,13 +89,17 @@ hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t st);
 // language-only backward: grad_acc is the (P, D) dL/dlanguage output itself
 // (zeroed by the caller), VP = D
 hipError_t launch_render_bwd_lang(const RenderBwdArgs& a, hipStream_t st);
+// language-only backward of the quick (sparse) input: a.qw_acc (P, K) from
+// the Dq-channel gradient (Dq must be a compiled channel set, <= 64)
+hipError_t launch_render_bwd_lang_sparse(const RenderBwdArgs& a, hipStream_t st);
 int lang_set_for(int D);     // compiled channel set >= D, or -1
 
 // quick.hip
 hipError_t launch_topk_code_fwd(const float* logits, int64_t N, int L, int K, int k, float* dense, float* sw,
                                 void* sidx, int idx_dtype, int level_offset, hipStream_t st);
+// sparse: g is dL/dweights of the packed (N, L*k) form (ascending channel order)
 hipError_t launch_topk_code_bwd(const float* logits, const float* g, int64_t N, int L, int K, int k, float* dlogits,
-                                hipStream_t st);
+                                hipStream_t st, bool sparse = false);
 size_t knn_workspace_bytes(int64_t N, size_t sort_temp);
 hipError_t knn_sort_temp_bytes(int64_t N, size_t* bytes);
 hipError_t launch_knn_dist2(const float* points, int64_t N, float* out, uint8_t* ws, size_t sort_temp, hipStream_t st);
@@ -106,6 +114,14 @@ size_t lang_loss_workspace_bytes(int S, int W, int H, int* waves);
 hipError_t launch_lang_loss(const float* wmap, const float* cb, int Df, int H, int W, const int32_t* seg,
                             const float* feat, int S, const float* gscale, float* loss, float* gw, float* dcb,
                             float* stats, float* ws, hipStream_t st);
+
+// aux.hip: debug NaN/Inf guard (flag |= 1 if any element of p[0..n) is not
+// finite) and the quick-input dense expansion / gradient gather
+hipError_t launch_nonfinite(const float* p, size_t n, uint32_t* flag, hipStream_t st);
+hipError_t launch_sparse_expand(const float* qw, const void* qi, int dtype, int N, int K, int Dq, float* dense,
+                                hipStream_t st);
+hipError_t launch_sparse_gather(const float* g, const void* qi, int dtype, int N, int K, int Dq, float* dw,
+                                hipStream_t st);
 
 // adam.hip
 struct AdamArgs {

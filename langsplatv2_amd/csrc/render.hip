@@ -1133,10 +1133,14 @@ __device__ __forceinline__ float feature_at(const RenderArgs& a, uint32_t gid, i
 // requiring grad).  Then dL/dlang[j][c] = sum_p aT[j][p] dL/dout[c][p] is all
 // that is left: no dot products, no dL/dalpha recurrence, no moments, and the
 // rows go straight into the (N, D) output (b.grad_acc, b.VP = D).
-template <int NL, bool LO = false, bool LD = false>
+// SP (with LO): the language input is the quick path's sparse (weights,
+// codes) rows; the per-channel gradient rows are gathered at each Gaussian's
+// codes into dL/dweights (b.qw_acc, (P, K)) instead of being added densely.
+template <int NL, bool LO = false, bool LD = false, bool SP = false>
 __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArgs b)
 {
     static_assert(!LO || (LSR_BWD_VMOM && NL > 0), "language-only backward needs the VMOM layout and D > 0");
+    static_assert(!SP || LO, "the sparse-input gradient is a language-only backward");
     static_assert(!LD || (LSR_BWD_VMOM && !LO && NL % 16 == 0), "direct dL/dlang needs VMOM and whole 16-channel lines");
     using FR = BwdFrags<NL>;
     constexpr int KS = FR::KS;
@@ -1152,6 +1156,10 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #endif
     constexpr int GS = LSR_GRP_STRIDE;
     __shared__ WaveStageG st;
+#ifdef LSR_BWD_LDS_PAD   // occupancy experiment only: extra LDS per wave
+    __shared__ float lds_pad[LSR_BWD_LDS_PAD];
+    if (b.VP == -12345) lds_pad[blockIdx.x % LSR_BWD_LDS_PAD] = 0.f;
+#endif
     // first language column of a staged row; LD: the language lines start at
     // 16 and go to b.lang_acc, the first line (geometry + colour) to the row
     constexpr int GCOL0 = LO ? 0 : (LD ? 16 : LSR_GROW_LANG);
@@ -1546,6 +1554,21 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             }
 #endif
             wave_lds_fence();
+            if constexpr (SP) {
+                // (slot, code) pairs: dL/dw[gid][m] += row[slot][idx[gid][m]]
+                const int K = a.K;
+                for (int e = lane; e < 16 * K; e += 64) {
+                    const int slot = e / K, m = e - slot * K;
+                    if (slot < kn) {
+                        const size_t off = (size_t)st.gid[g0 + slot] * K + m;
+                        const int q = quick_index(a.qi, a.qidx_dtype, off);
+                        if (q >= 0 && q < D) {
+                            const float v = sGr[slot * GRS + GCOL0 + q];
+                            if (v != 0.f) LSR_MF_ATOMIC(b.qw_acc + off, v);
+                        }
+                    }
+                }
+            } else
 #pragma unroll
             for (int h = 0; h < GRL; h++) {
                 const int f = 16 * h + li;
@@ -2169,6 +2192,22 @@ hipError_t launch_render_bwd_lang(const RenderBwdArgs& b, hipStream_t st)
         case 16: k_render_bwd_mf<16, true><<<4 * T, 64, 0, st>>>(b); break;
         case 32: k_render_bwd_mf<32, true><<<4 * T, 64, 0, st>>>(b); break;
         case 64: k_render_bwd_mf<64, true><<<4 * T, 64, 0, st>>>(b); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_render_bwd_lang_sparse(const RenderBwdArgs& b, hipStream_t st)
+{
+    const int T = b.f.cam.gx * b.f.cam.gy;
+    if (T == 0) return hipSuccess;
+    if (!b.qw_acc || !b.f.qi || b.f.K <= 0) return hipErrorInvalidValue;
+    switch (lang_set_for(b.f.D)) {
+        case 4: k_render_bwd_mf<4, true, false, true><<<4 * T, 64, 0, st>>>(b); break;
+        case 8: k_render_bwd_mf<8, true, false, true><<<4 * T, 64, 0, st>>>(b); break;
+        case 16: k_render_bwd_mf<16, true, false, true><<<4 * T, 64, 0, st>>>(b); break;
+        case 32: k_render_bwd_mf<32, true, false, true><<<4 * T, 64, 0, st>>>(b); break;
+        case 64: k_render_bwd_mf<64, true, false, true><<<4 * T, 64, 0, st>>>(b); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -74,7 +74,13 @@ def quick_inputs(logits: torch.Tensor, k: int, levels: int = 1, level_offset: bo
     """Packed sparse codes of every level: (weights (N, levels*k) fp32, indices
     (N, levels*k) of index_dtype), indices + K*level when level_offset —
     the language_feature_weights_quick / language_feature_indices pair of
-    eval_lerf.py:340-348.  Not differentiable (every quick caller is no_grad)."""
+    eval_lerf.py:340-348.  Not differentiable (every quick caller is no_grad;
+    `sparse_codes` is the differentiable form)."""
+    with torch.no_grad():
+        return _quick_inputs_impl(logits, k, levels, level_offset, index_dtype)
+
+
+def _quick_inputs_impl(logits, k, levels, level_offset, index_dtype):
     x, N, K = _check_logits(logits, levels, "quick_inputs")
     codes = {torch.float32: _lib.LSR_INDEX_F32, torch.int32: _lib.LSR_INDEX_I32, torch.int64: _lib.LSR_INDEX_I64}
     if index_dtype not in codes:
@@ -86,6 +92,44 @@ def quick_inputs(logits: torch.Tensor, k: int, levels: int = 1, level_offset: bo
                                          codes[index_dtype], int(bool(level_offset)), _stream(x.device)),
                "lsr_topk_code_forward")
     return w, idx
+
+
+class _TopkSparse(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, k, levels, level_offset, index_dtype):
+        w, idx = _quick_inputs_impl(logits, k, levels, level_offset, index_dtype)
+        ctx.save_for_backward(logits.contiguous().float())
+        ctx.k, ctx.levels = int(k), levels
+        ctx.mark_non_differentiable(idx)
+        return w, idx
+
+    @staticmethod
+    def backward(ctx, gw, _gidx):
+        (x,) = ctx.saved_tensors
+        N, LK = x.shape
+        dx = torch.empty_like(x)
+        if gw is None:
+            return dx.zero_(), None, None, None, None
+        g = gw.contiguous().float()
+        lib = _lib.load()
+        _lib.check(lib.lsr_topk_code_backward_sparse(x.data_ptr(), g.data_ptr(), N, ctx.levels, LK // ctx.levels,
+                                                     ctx.k, dx.data_ptr(), _stream(x.device)),
+                   "lsr_topk_code_backward_sparse")
+        return dx, None, None, None, None
+
+
+def sparse_codes(logits: torch.Tensor, k: int, levels: int = 1, level_offset: bool = True,
+                 index_dtype: torch.dtype = torch.int32):
+    """The packed top-k codes as a DIFFERENTIABLE rasterizer input:
+    (weights (N, levels*k) fp32 with grad w.r.t. logits, indices (N, levels*k)), the
+    language_feature_weights_quick / language_feature_indices pair rendered with
+    quick_render=True and language_feature_dim = levels*K.  Feature-mode training
+    then never forms the dense (N, K) codes (get_render_weights, scene/gaussian_model.py:
+    510-518): the rasterizer returns dL/dweights (N, levels*k) and the producer's
+    sparse backward turns it into dL/dlogits.  Mathematically the same gradient as
+    the dense path: dL/dw[j][m] = dL/dcode[j][idx[j][m]] and the unselected codes
+    are constant zeros."""
+    return _TopkSparse.apply(logits, k, levels, level_offset, index_dtype)
 
 
 def get_weights_and_indices(logits: torch.Tensor, k: int):

@@ -48,7 +48,19 @@ def decode_language_features(weight_map: torch.Tensor, codebooks: torch.Tensor, 
 
 
 def compute_final_feature_map(weight_map: torch.Tensor, codebooks: torch.Tensor) -> torch.Tensor:
-    """scene/gaussian_model.py:545-550: codebooks.view(-1, Df).T @ weight_map.view(D, -1) -> (Df, H, W)."""
+    """scene/gaussian_model.py:545-550: codebooks.view(-1, Df).T @ weight_map.view(R, -1) -> (Df, H, W)
+    for any number of levels / codes R = codebooks.numel() // Df (the reference accepts any R).  The
+    codes are decoded in 64-code blocks on the matrix cores (R padded with zero codes to a multiple of
+    64) and the per-block maps summed."""
     Df = codebooks.shape[-1]
-    cb = codebooks.reshape(1, -1, Df)
-    return decode_language_features(weight_map, cb, normalize=False)[0]
+    cb = codebooks.reshape(-1, Df)
+    R = cb.shape[0]
+    if weight_map.dim() != 3 or weight_map.shape[0] != R:
+        raise ValueError(f"compute_final_feature_map: weight_map must be ({R}, H, W), got {tuple(weight_map.shape)}")
+    Rp = (R + 63) // 64 * 64
+    wm = weight_map
+    if Rp != R:
+        cb = torch.cat([cb, cb.new_zeros((Rp - R, Df))], 0)
+        wm = torch.cat([wm, wm.new_zeros((Rp - R,) + tuple(wm.shape[1:]))], 0)
+    out = decode_language_features(wm, cb.reshape(Rp // 64, 64, Df), normalize=False)
+    return out[0] if out.shape[0] == 1 else out.sum(0)

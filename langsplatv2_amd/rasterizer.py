@@ -25,20 +25,68 @@ Behaviour kept from the reference:
 Language modes (gaussian_renderer/__init__.py:87-103):
   include_feature=True  -> dense (N,D) coefficients, output (D,H,W);
   quick_render=True     -> sparse (N,K) weights + (N,K) indices (fp32-encoded
-                           integers, or int32/int64), output (Dq,H,W), no grad;
+                           integers, or int32/int64), output (Dq,H,W); the
+                           weights are differentiable (the
+                           fused top-k producer feeds training sparse codes),
+                           the indices are not;
   neither               -> output (0,H,W).
+Data-parallel hook: `GradSink` (a context manager) hands the backward
+preallocated gradient destinations (views of an all-reduce bucket, so no pack
+copy) and an event the library records once the language gradient is final.
 All compute runs in liblsr.so (hand-written HIP, gfx950); this module only
 moves pointers.  There is no CPU path.
 """
 from __future__ import annotations
 
 import ctypes
+import threading
 from typing import NamedTuple, Optional
 
 import torch
 import torch.nn as nn
 
 from . import _lib
+
+
+_SINKS = threading.local()
+
+
+class GradSink:
+    """Destinations for the gradients of the rasterizer backward(s) run while
+    the context is active (on this thread):
+
+      buffers     {input name: tensor}: preallocated fp32 outputs, used when
+                  shape / device match (the library writes every element), e.g.
+                  views of a flat all-reduce bucket (langsplatv2_amd/dp.py);
+      lang_ready  optional torch.cuda.Event, recorded on the backward's stream
+                  as soon as dL/dlanguage is final (before the preprocess
+                  backward), so a collective on another stream can start early;
+      on_lang_ready  optional callable run right after the library call has
+                  been enqueued (host side), e.g. to launch that collective.
+
+    Input names: means3D, means2D, shs, colors_precomp, language_feature_precomp,
+    language_feature_weights_quick, opacities, scales, rotations, cov3D_precomp."""
+
+    def __init__(self, buffers=None, lang_ready=None, on_lang_ready=None):
+        self.buffers = dict(buffers or {})
+        self.lang_ready = lang_ready
+        self.on_lang_ready = on_lang_ready
+
+    def __enter__(self):
+        st = getattr(_SINKS, "stack", None)
+        if st is None:
+            st = _SINKS.stack = []
+        st.append(self)
+        return self
+
+    def __exit__(self, *exc):
+        _SINKS.stack.pop()
+        return False
+
+
+def _sink() -> Optional[GradSink]:
+    st = getattr(_SINKS, "stack", None)
+    return st[-1] if st else None
 
 
 class GaussianRasterizationSettings(NamedTuple):
@@ -175,7 +223,7 @@ def _run_forward(means3D, sh, colors_precomp, language_feature_precomp, language
             _dump("snapshot_fw.dump", [means3D, sh, colors_precomp, opacities, scales, rotations,
                                        cov3Ds_precomp, language_feature_precomp, rs.viewmatrix, rs.projmatrix])
         _lib.check(rc, "rasterize_gaussians (forward)")
-    saved = (means3D_c, opac_c, sh_c, col_c, sc_c, rot_c, cov_c, lang_c)
+    saved = (means3D_c, opac_c, sh_c, col_c, sc_c, rot_c, cov_c, lang_c, qw_c, qi_c)
     return color, lang_out, radii, int(out.num_rendered), alloc.bufs, saved, (N, M, D, K)
 
 
@@ -201,11 +249,12 @@ class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_color, grad_lang, _grad_radii):
         rs = ctx.raster_settings
-        (means3D, opac, sh, col, sc, rot, cov, lang, radii, geom, binning, image) = ctx.saved_tensors
+        (means3D, opac, sh, col, sc, rot, cov, lang, qw, qi, radii, geom, binning, image) = ctx.saved_tensors
         N, M, D, K = ctx.dims
         dev = means3D.device
         lib = _lib.load()
         need = ctx.needs_input_grad
+        quick = bool(rs.quick_render)
         # inputs: 0 means3D 1 means2D 2 sh 3 colors 4 lang 5 qw 6 qi 7 opac 8 scales 9 rot 10 cov 11 settings
         grad_color = grad_color.contiguous() if grad_color is not None else torch.zeros(
             (3, rs.image_height, rs.image_width), device=dev)
@@ -213,39 +262,55 @@ class _RasterizeGaussians(torch.autograd.Function):
         if lang is not None:
             gl = grad_lang.contiguous() if grad_lang is not None else torch.zeros(
                 (D, rs.image_height, rs.image_width), device=dev)
+        elif quick and grad_lang is not None:
+            # the quick channels take part in the backward only when a gradient reaches them
+            gl = grad_lang.contiguous()
         s, keep = _settings_struct(rs, dev)
-        ins = _lib.Inputs(N, M, D, 0, 0, means3D.data_ptr(), _ptr(sh), _ptr(col), opac.data_ptr(), _ptr(sc),
-                          _ptr(rot), _ptr(cov), _ptr(lang), None, None)
-        # quick-path language channels are not differentiated: run the backward in dense/RGB mode
-        s.quick_render = 0
+        ins = _lib.Inputs(N, M, D, K if quick else 0, _index_dtype(qi) if quick else 0, means3D.data_ptr(), _ptr(sh),
+                          _ptr(col), opac.data_ptr(), _ptr(sc), _ptr(rot), _ptr(cov), _ptr(lang),
+                          _ptr(qw) if quick else None, _ptr(qi) if quick else None)
         bin_ = _lib.BwdIn(geom.data_ptr(), binning.data_ptr(), image.data_ptr(), ctx.num_rendered, radii.data_ptr(),
                           grad_color.data_ptr(), _ptr(gl))
+        sink = _sink()
 
-        def mk(shape, flag):
-            return torch.empty(shape, dtype=torch.float32, device=dev) if flag else None
+        def mk(name, shape, flag):
+            if not flag:
+                return None
+            if sink is not None:
+                t = sink.buffers.get(name)
+                if (t is not None and tuple(t.shape) == tuple(shape) and t.dtype == torch.float32
+                        and t.device == dev and t.is_contiguous()):
+                    return t
+            return torch.empty(shape, dtype=torch.float32, device=dev)
 
         # only what autograd asks for: with the language input alone requiring
         # grad (feature mode, means2D without grad) the library runs its
-        # language-only backward
-        g_means2D = mk((N, 3), need[1])
-        g_means3D = mk((N, 3), need[0])
-        g_sh = mk(tuple(sh.shape), need[2]) if sh is not None else None
-        g_col = mk((N, 3), need[3]) if col is not None else None
-        g_lang = mk((N, D), need[4]) if lang is not None else None
-        g_opac = mk((N, 1), need[7])
-        g_sc = mk((N, 3), need[8]) if sc is not None else None
-        g_rot = mk((N, 4), need[9]) if rot is not None else None
-        g_cov = mk((N, 6), need[10]) if cov is not None else None
+        # language-only backward (dense rows, or the quick weights)
+        g_means2D = mk("means2D", (N, 3), need[1])
+        g_means3D = mk("means3D", (N, 3), need[0])
+        g_sh = mk("shs", tuple(sh.shape), need[2]) if sh is not None else None
+        g_col = mk("colors_precomp", (N, 3), need[3]) if col is not None else None
+        g_lang = mk("language_feature_precomp", (N, D), need[4]) if lang is not None else None
+        g_qw = mk("language_feature_weights_quick", (N, K), need[5]) if (quick and qw is not None) else None
+        g_opac = mk("opacities", (N, 1), need[7])
+        g_sc = mk("scales", (N, 3), need[8]) if sc is not None else None
+        g_rot = mk("rotations", (N, 4), need[9]) if rot is not None else None
+        g_cov = mk("cov3D_precomp", (N, 6), need[10]) if cov is not None else None
+        ev = sink.lang_ready if sink is not None else None
+        if ev is not None and not ev.cuda_event:
+            ev.record(torch.cuda.current_stream(dev))   # materialise the event handle
         bout = _lib.BwdOut(_ptr(g_means2D), _ptr(g_col), _ptr(g_lang), _ptr(g_opac), _ptr(g_means3D), _ptr(g_cov),
-                           _ptr(g_sh), _ptr(g_sc), _ptr(g_rot))
+                           _ptr(g_sh), _ptr(g_sc), _ptr(g_rot), _ptr(g_qw), ev.cuda_event if ev is not None else None)
         alloc = _Alloc(dev)
         rc = lib.lsr_backward(ctypes.byref(s), ctypes.byref(ins), ctypes.byref(bin_), ctypes.byref(bout), alloc.fn,
                               None, _stream(dev))
         if rc != _lib.LSR_OK:
             if rs.debug:
-                _dump("snapshot_bw.dump", [grad_color, gl, means3D, sh, col, opac, sc, rot, cov, lang])
+                _dump("snapshot_bw.dump", [grad_color, gl, means3D, sh, col, opac, sc, rot, cov, lang, qw, qi])
             _lib.check(rc, "rasterize_gaussians_backward")
-        return (g_means3D if need[0] else None, g_means2D if need[1] else None, g_sh, g_col, g_lang, None, None,
+        if sink is not None and sink.on_lang_ready is not None:
+            sink.on_lang_ready()
+        return (g_means3D if need[0] else None, g_means2D if need[1] else None, g_sh, g_col, g_lang, g_qw, None,
                 g_opac if need[7] else None, g_sc, g_rot, g_cov, None)
 
 

@@ -456,10 +456,22 @@ typedef struct {
     double* dmean2D; double* dconic; double* dopacity; double* dcolor; double* dlang;
 } dacc_t;
 
+/* atomic: tiles rendered by several threads at once (the multi-threaded CPU
+ * baseline); the sequential path (the parity checker) keeps plain adds */
+static inline void acc_add(double* p, double v, int atomic)
+{
+    if (atomic) {
+#pragma omp atomic update
+        *p += v;
+    } else {
+        *p += v;
+    }
+}
+
 static void render_tile_bwd(const lso_settings* s, const lso_inputs* in, const lso_geom* g,
                             const uint32_t* point_list, const uint32_t* ranges, int tile,
                             const float* final_Ts, const uint32_t* n_contrib,
-                            const float* dout_color, const float* dout_lang, dacc_t* A)
+                            const float* dout_color, const float* dout_lang, dacc_t* A, int atomic)
 {
     const int W = s->W, H = s->H;
     const int gx = (W + TILE - 1) / TILE;
@@ -503,27 +515,27 @@ static void render_tile_bwd(const lso_settings* s, const lso_inputs* in, const l
                 dL_dalpha = fmaf(-T_final / (1.f - alpha), bg_dot, dL_dalpha);
                 last_alpha = alpha;
                 last_dot = dot;
-                for (int ch = 0; ch < 3; ch++) A->dcolor[3 * (size_t)j + ch] += (double)(aT * Gc[ch]);
-                for (int k = 0; k < D; k++) A->dlang[(size_t)j * D + k] += (double)(aT * Gl[k]);
+                for (int ch = 0; ch < 3; ch++) acc_add(&A->dcolor[3 * (size_t)j + ch], (double)(aT * Gc[ch]), atomic);
+                for (int k = 0; k < D; k++) acc_add(&A->dlang[(size_t)j * D + k], (double)(aT * Gl[k]), atomic);
                 const float dL_dG = co[3] * dL_dalpha;
                 const float gdx = G * dx, gdy = G * dy;
                 const float dG_ddelx = -gdx * co[0] - gdy * co[1];
                 const float dG_ddely = -gdy * co[2] - gdx * co[1];
-                A->dmean2D[3 * (size_t)j + 0] += (double)(dL_dG * dG_ddelx * ddelx_dx);
-                A->dmean2D[3 * (size_t)j + 1] += (double)(dL_dG * dG_ddely * ddely_dy);
-                A->dconic[3 * (size_t)j + 0] += (double)(-0.5f * gdx * dx * dL_dG);
-                A->dconic[3 * (size_t)j + 1] += (double)(-gdx * dy * dL_dG);
-                A->dconic[3 * (size_t)j + 2] += (double)(-0.5f * gdy * dy * dL_dG);
-                A->dopacity[j] += (double)(G * dL_dalpha);
+                acc_add(&A->dmean2D[3 * (size_t)j + 0], (double)(dL_dG * dG_ddelx * ddelx_dx), atomic);
+                acc_add(&A->dmean2D[3 * (size_t)j + 1], (double)(dL_dG * dG_ddely * ddely_dy), atomic);
+                acc_add(&A->dconic[3 * (size_t)j + 0], (double)(-0.5f * gdx * dx * dL_dG), atomic);
+                acc_add(&A->dconic[3 * (size_t)j + 1], (double)(-gdx * dy * dL_dG), atomic);
+                acc_add(&A->dconic[3 * (size_t)j + 2], (double)(-0.5f * gdy * dy * dL_dG), atomic);
+                acc_add(&A->dopacity[j], (double)(G * dL_dalpha), atomic);
             }
         }
     free(Gl);
 }
 
-void lso_render_bwd_tiles(const lso_settings* s, const lso_inputs* in, const lso_geom* g,
-                          const uint32_t* point_list, const uint32_t* ranges, const int32_t* tiles, int ntiles,
-                          const float* final_T, const uint32_t* n_contrib, const float* dout_color,
-                          const float* dout_lang, lso_render_grads* rg)
+void lso_render_bwd_tiles_mt(const lso_settings* s, const lso_inputs* in, const lso_geom* g,
+                             const uint32_t* point_list, const uint32_t* ranges, const int32_t* tiles, int ntiles,
+                             const float* final_T, const uint32_t* n_contrib, const float* dout_color,
+                             const float* dout_lang, lso_render_grads* rg, int nthreads)
 {
     const int N = in->N;
     const int D = s->include_feature ? in->D : 0;
@@ -533,8 +545,14 @@ void lso_render_bwd_tiles(const lso_settings* s, const lso_inputs* in, const lso
     A.dopacity = (double*)calloc((size_t)N + 1, sizeof(double));
     A.dcolor = (double*)calloc((size_t)N * 3 + 1, sizeof(double));
     A.dlang = (double*)calloc((size_t)N * (D > 0 ? D : 1) + 1, sizeof(double));
-    for (int k = 0; k < ntiles; k++)
-        render_tile_bwd(s, in, g, point_list, ranges, tiles[k], final_T, n_contrib, dout_color, dout_lang, &A);
+    if (nthreads <= 1) {
+        for (int k = 0; k < ntiles; k++)
+            render_tile_bwd(s, in, g, point_list, ranges, tiles[k], final_T, n_contrib, dout_color, dout_lang, &A, 0);
+    } else {
+#pragma omp parallel for schedule(dynamic, 4) num_threads(nthreads)
+        for (int k = 0; k < ntiles; k++)
+            render_tile_bwd(s, in, g, point_list, ranges, tiles[k], final_T, n_contrib, dout_color, dout_lang, &A, 1);
+    }
     for (size_t i = 0; i < (size_t)N * 3; i++) {
         rg->dmean2D[i] = (i % 3 == 2) ? 0.f : (float)A.dmean2D[i];
         rg->dconic[i] = (float)A.dconic[i];
@@ -544,6 +562,15 @@ void lso_render_bwd_tiles(const lso_settings* s, const lso_inputs* in, const lso
     if (rg->dlang && D)
         for (size_t i = 0; i < (size_t)N * D; i++) rg->dlang[i] = (float)A.dlang[i];
     free(A.dmean2D); free(A.dconic); free(A.dopacity); free(A.dcolor); free(A.dlang);
+}
+
+void lso_render_bwd_tiles(const lso_settings* s, const lso_inputs* in, const lso_geom* g,
+                          const uint32_t* point_list, const uint32_t* ranges, const int32_t* tiles, int ntiles,
+                          const float* final_T, const uint32_t* n_contrib, const float* dout_color,
+                          const float* dout_lang, lso_render_grads* rg)
+{
+    lso_render_bwd_tiles_mt(s, in, g, point_list, ranges, tiles, ntiles, final_T, n_contrib, dout_color, dout_lang,
+                            rg, 1);
 }
 
 void lso_render_bwd(const lso_settings* s, const lso_inputs* in, const lso_geom* g, const uint32_t* point_list,

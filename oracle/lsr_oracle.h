@@ -120,6 +120,14 @@ void lso_render_bwd_tiles(const lso_settings* s, const lso_inputs* in, const lso
                           const float* final_T, const uint32_t* n_contrib,
                           const float* dout_color, const float* dout_lang,
                           lso_render_grads* rg);
+/* as lso_render_bwd_tiles on nthreads OpenMP threads (tiles in parallel, fp64
+ * atomic accumulation): the multi-threaded CPU baseline of bench.py */
+void lso_render_bwd_tiles_mt(const lso_settings* s, const lso_inputs* in, const lso_geom* g,
+                             const uint32_t* point_list, const uint32_t* ranges,
+                             const int32_t* tiles, int ntiles,
+                             const float* final_T, const uint32_t* n_contrib,
+                             const float* dout_color, const float* dout_lang,
+                             lso_render_grads* rg, int nthreads);
 
 typedef struct {
     float* dmeans3D;  /* N*3 */

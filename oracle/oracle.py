@@ -161,18 +161,31 @@ def forward(pb: Problem, nthreads: int = 1, tiles=None) -> dict:
     return out
 
 
-def backward(pb: Problem, fwd: dict, dout_color: np.ndarray, dout_lang: np.ndarray | None = None, tiles=None) -> dict:
+def backward(pb: Problem, fwd: dict, dout_color: np.ndarray, dout_lang: np.ndarray | None = None, tiles=None,
+             nthreads: int = 1) -> dict:
     lib = load()
     N, D = pb.N, pb.D
     g, geom = fwd["_keep"]
     s, i = pb._structs()
+    qdense = qcodes = None
     if pb.quick:
-        # quick-path language channels are not differentiated (as the GPU path)
+        # quick (sparse) language input: with an upstream language gradient the
+        # rows are expanded to dense (N, Dq) coefficients (duplicates summed) and
+        # the dense backward runs; dL/dweights[j][m] = dL/dlang[j][code[j][m]]
+        # (lsr_bwd_out.dL_dlang_weights).  Without one, RGB only.
         s.quick_render = 0
-        s.include_feature = 0
-        i.D = 0
-        i.lang = None
-        D = 0
+        if dout_lang is None:
+            s.include_feature = 0
+            i.D = 0
+            i.lang = None
+            D = 0
+        else:
+            qcodes = quick_codes(pb.qi)
+            qdense = expand_quick(pb.qw, qcodes, pb.quick_dim)
+            D = pb.quick_dim
+            s.include_feature = 1
+            i.D = D
+            i.lang = _p(qdense)
     dcol = _np(dout_color)
     dlang = _np(dout_lang) if (D and dout_lang is not None) else None
     rg = dict(dmean2D=np.zeros((N, 3), np.float32), dconic=np.zeros((N, 3), np.float32),
@@ -182,14 +195,14 @@ def backward(pb: Problem, fwd: dict, dout_color: np.ndarray, dout_lang: np.ndarr
                   _p(rg["dlang"]) if D else None)
     pl = fwd["point_list"] if fwd["num_rendered"] > 0 else np.zeros(1, np.uint32)
     pl = np.ascontiguousarray(pl)
-    if tiles is None:
+    if tiles is None and nthreads <= 1:
         lib.lso_render_bwd(ctypes.byref(s), ctypes.byref(i), ctypes.byref(geom), _p(pl), _p(fwd["ranges"]),
                            _p(fwd["final_T"]), _p(fwd["n_contrib"]), _p(dcol), _p(dlang), ctypes.byref(rgs))
     else:
-        tl = np.ascontiguousarray(tiles, dtype=np.int32)
-        lib.lso_render_bwd_tiles(ctypes.byref(s), ctypes.byref(i), ctypes.byref(geom), _p(pl), _p(fwd["ranges"]),
-                                 _p(tl), len(tl), _p(fwd["final_T"]), _p(fwd["n_contrib"]), _p(dcol), _p(dlang),
-                                 ctypes.byref(rgs))
+        tl = np.ascontiguousarray(np.arange(pb.gx * pb.gy) if tiles is None else tiles, dtype=np.int32)
+        lib.lso_render_bwd_tiles_mt(ctypes.byref(s), ctypes.byref(i), ctypes.byref(geom), _p(pl),
+                                    _p(fwd["ranges"]), _p(tl), len(tl), _p(fwd["final_T"]), _p(fwd["n_contrib"]),
+                                    _p(dcol), _p(dlang), ctypes.byref(rgs), int(nthreads))
     pgd = dict(dmeans3D=np.zeros((N, 3), np.float32), dcolors=np.zeros((N, 3), np.float32))
     if pb.shs is not None:
         pgd["dsh"] = np.zeros_like(pb.shs)
@@ -204,7 +217,32 @@ def backward(pb: Problem, fwd: dict, dout_color: np.ndarray, dout_lang: np.ndarr
     out = dict(rg)
     out["dlang"] = rg["dlang"][:, :D] if D else None
     out.update(pgd)
+    if qdense is not None:
+        ok = (qcodes >= 0) & (qcodes < D)
+        rows = np.repeat(np.arange(N)[:, None], qcodes.shape[1], 1)
+        out["dlang_weights"] = np.where(ok, out["dlang"][rows, np.clip(qcodes, 0, D - 1)], 0.0).astype(np.float32)
+        out["dlang"] = None
     return out
+
+
+def quick_codes(qi: np.ndarray) -> np.ndarray:
+    """Integer codes of quick indices: fp32-encoded integers round half up (u5)."""
+    qi = np.asarray(qi)
+    if qi.dtype.kind == "f":
+        return np.floor(qi.astype(np.float32) + np.float32(0.5)).astype(np.int64)
+    return qi.astype(np.int64)
+
+
+def expand_quick(qw: np.ndarray, codes: np.ndarray, Dq: int) -> np.ndarray:
+    """Dense (N, Dq) rows of the quick input: row[j][code] += w in code order; out-of-range codes dropped."""
+    N, K = qw.shape
+    dense = np.zeros((N, Dq), np.float32)
+    for m in range(K):
+        c = codes[:, m]
+        ok = (c >= 0) & (c < Dq)
+        r = np.nonzero(ok)[0]
+        dense[r, c[ok]] += qw[r, m].astype(np.float32)
+    return dense
 
 
 def expf(x: float) -> float:

@@ -1,0 +1,42 @@
+"""bench.py's launch contract on CPU: `--gpus N` without a launcher starts N ranks
+itself (a torch.distributed.run child, before any GPU call), the ranks agree on
+the world size, and a launcher/flag mismatch fails instead of silently timing
+one GPU.  --dry-run stops after rank bring-up (gloo), so no GPU is touched."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env=None):
+    e = dict(os.environ)
+    e.update(env or {})
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        if not env or k not in env:
+            e.pop(k, None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=240, env=e, cwd=ROOT)
+
+
+def _last_json(out):
+    return json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+
+
+def test_gpus2_self_launches_two_ranks():
+    p = _run(["--gpus", "2", "--dry-run"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    j = _last_json(p.stdout)
+    assert j["dry_run"] and j["n_gpus"] == 2 and j["ranks"] == [0, 1] and j["world_sizes_seen"] == [2]
+
+
+def test_gpus1_dry_run_is_single_rank():
+    p = _run(["--dry-run"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert _last_json(p.stdout)["n_gpus"] == 1
+
+
+def test_launcher_mismatch_fails_loudly():
+    p = _run(["--gpus", "2", "--dry-run"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode != 0 and "WORLD_SIZE=1" in (p.stderr + p.stdout)

@@ -111,3 +111,44 @@ def test_rank_yaw_and_bounds():
     assert ys[0] == -20.0 and ys[-1] == 20.0 and ys == sorted(ys)
     b = dp.allreduce_bound_ms(256 << 20, 8)
     assert 2.5 < b["ring_1link_ms"] < 3.2 and b["all_links_ms"] < b["ring_1link_ms"]
+
+
+def test_view_schedule_wraps_when_world_does_not_divide():
+    for n, world in ((10, 4), (7, 8), (64, 3)):
+        got = [dp.view_schedule(n, world, r, seed=1) for r in range(world)]
+        steps = -(-n // world)
+        assert all(len(g) == steps for g in got)
+        assert sorted(set(v for g in got for v in g)) == list(range(n))   # every view at least once
+
+
+def _finish_worker(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        names = ["means3D", "shs", "opacities", "language_feature_precomp"]
+        params = [torch.zeros(6, 3), torch.zeros(6, 16, 3), torch.zeros(6, 1), torch.zeros(6, 16)]
+        ex = dp.ViewShardedExchange(params, with_stats=True, names=names)
+        assert ex.early is not None and ex.early_idx == [3]
+        g = torch.Generator().manual_seed(rank)
+        grads = [torch.randn(p.shape, generator=g) for p in params]
+        grads[1] = None                                    # a parameter without gradient this step
+        m2d = torch.randn(6, 3, generator=g)
+        radii = torch.tensor([0, 1, 2, 3, 4, 5], dtype=torch.int32) * (rank + 1)
+        red, stats, max_r = ex.finish(m2d, radii, grads)   # the zero-copy path with foreign tensors
+        exp = [torch.zeros_like(p) for p in params]
+        for r in range(world):
+            gr = torch.Generator().manual_seed(r)
+            gg = [torch.randn(p.shape, generator=gr) for p in params]
+            for i in (0, 2, 3):
+                exp[i] += gg[i]
+        for i in range(4):
+            assert torch.allclose(red[i], exp[i], rtol=0, atol=1e-6), names[i]
+        assert torch.equal(max_r, radii // (rank + 1) * world)
+        assert float(stats[:, 1].max()) == world
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_finish_two_buckets_gloo_world2():
+    mp.spawn(_finish_worker, args=(2, _free_port()), nprocs=2, join=True)

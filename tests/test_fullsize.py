@@ -9,11 +9,19 @@ cfg3 (1M Gaussians, 1920x1080, SH3 + 16 language channels):
     renders;
   * backward: with dL/dout zero outside those tiles, the GPU's full backward
     equals the oracle's tile-restricted backward (GRAD_RTOL).
-cfg5 (5M Gaussians, 3840x2160, SH3 + 32 language channels), GPU only:
-  size-independent properties of the binning (every instance once, lists in
-  strict (depth, id) order per tile, ranges partition the list) and of the
+cfg2 (100k Gaussians, 800x800, RGB colours + 3 language channels,
+  forward-only): the WHOLE frame bit-exactly against the oracle (every tile
+  rendered on the host's cores): radii, the full binning, colour, language,
+  final_T, n_contrib.
+cfg5 (5M Gaussians, 3840x2160, SH3 + 32 language channels, 120M instances):
+  the WHOLE binning (ranges + point list) and per-Gaussian records
+  bit-exactly, images / final_T / n_contrib bit-exactly on 32 seeded tiles;
+  plus size-independent properties of the binning (every instance once, lists
+  in strict (depth, id) order per tile, ranges partition the list) and of the
   images (finite, final_T in [0, 1], colour >= 0 with a black background).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -67,6 +75,58 @@ def test_cfg3_forward_full_binning_and_sampled_tiles(gpu, oracle_lib):
     np.testing.assert_array_equal(got["final_T"][ys, xs], ref["final_T"][ys, xs])
     np.testing.assert_array_equal(got["color"][:, ys, xs], ref["color"][:, ys, xs])
     np.testing.assert_array_equal(got["lang"][:, ys, xs], ref["lang"][:, ys, xs])
+
+
+def _threads():
+    env = os.environ.get("OMP_NUM_THREADS")
+    return int(env) if env and env.isdigit() else min(16, os.cpu_count() or 1)
+
+
+def _compare_forward(got, ref, sh, tiles=None, gx=None, W=None, H=None):
+    assert got["num_rendered"] == ref["num_rendered"]
+    np.testing.assert_array_equal(got["radii"], ref["radii"])
+    np.testing.assert_array_equal(got["tiles_touched"], ref["tiles_touched"].astype(np.int32))
+    vis = ref["radii"] > 0
+    np.testing.assert_array_equal(got["xy"][vis], ref["xy"][vis])
+    np.testing.assert_array_equal(got["conic_opacity"][vis], ref["conic_opacity"][vis])
+    if sh:   # with colors_precomp the renderer reads the caller's colours, no rgb record is written
+        np.testing.assert_array_equal(got["rgb"][vis], ref["rgb"][vis])
+    np.testing.assert_array_equal(got["ranges"], ref["ranges"].astype(np.int32))
+    np.testing.assert_array_equal(got["point_list"], ref["point_list"].astype(np.int32))
+    if tiles is None:
+        np.testing.assert_array_equal(got["n_contrib"], ref["n_contrib"].astype(np.int32))
+        np.testing.assert_array_equal(got["final_T"], ref["final_T"])
+        np.testing.assert_array_equal(got["color"], ref["color"])
+        np.testing.assert_array_equal(got["lang"], ref["lang"])
+    else:
+        ys, xs = _tile_pixels(tiles, gx, W, H)
+        np.testing.assert_array_equal(got["n_contrib"][ys, xs], ref["n_contrib"][ys, xs].astype(np.int32))
+        np.testing.assert_array_equal(got["final_T"][ys, xs], ref["final_T"][ys, xs])
+        np.testing.assert_array_equal(got["color"][:, ys, xs], ref["color"][:, ys, xs])
+        np.testing.assert_array_equal(got["lang"][:, ys, xs], ref["lang"][:, ys, xs])
+
+
+def test_cfg2_whole_frame_bit_exact(gpu, oracle_lib):
+    case = _case(2)
+    assert case["g"]["means3D"].shape[0] == 100_000 and case["cam"]["W"] == 800 and case["cam"]["H"] == 800
+    assert "colors_precomp" in case["g"] and case["g"]["language_feature_precomp"].shape[1] == 3
+    ref = oracle_lib.forward(oracle_problem(case), nthreads=_threads())
+    got = run_gpu_forward(case, gpu)
+    assert got["lang"].shape == (3, 800, 800)
+    _compare_forward(got, ref, sh=False)
+    # the frame is not trivially empty
+    assert ref["num_rendered"] > 100_000 and float(np.abs(ref["lang"]).max()) > 0.1
+
+
+def test_cfg5_full_binning_and_sampled_tiles(gpu, oracle_lib):
+    case = _case(5)
+    W, H = case["cam"]["W"], case["cam"]["H"]
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    tiles = _sample_tiles(gx, gy, n=32, seed=7)
+    ref = oracle_lib.forward(oracle_problem(case), nthreads=_threads(), tiles=tiles)
+    got = run_gpu_forward(case, gpu)
+    assert got["lang"].shape[0] == 32
+    _compare_forward(got, ref, True, tiles, gx, W, H)
 
 
 def test_cfg3_backward_sampled_tiles(gpu, oracle_lib):

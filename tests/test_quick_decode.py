@@ -70,3 +70,20 @@ def test_render_then_decode_end_to_end(gpu, oracle_lib):
     cb = np.random.default_rng(3).standard_normal((3, 64, 512)).astype(np.float32)
     feats = quick.decode_language_features(torch.from_numpy(got_f["lang"]).to(gpu), torch.from_numpy(cb).to(gpu))
     np.testing.assert_allclose(feats.cpu().numpy(), ref_decode(ref_f["lang"], cb), atol=DEC_ATOL, rtol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(3, 64, 32), (1, 40, 48), (2, 96, 16)])
+def test_final_feature_map_any_level_count(gpu, shape):
+    """compute_final_feature_map accepts any number of levels / codes like the reference's
+    codebooks.view(-1, Df).T @ W (scene/gaussian_model.py:545-550): 64-code blocks summed,
+    R padded with zero codes to a multiple of 64."""
+    g = np.random.default_rng(sum(shape))
+    L, K, Df = shape
+    wmap = g.random((L * K, 24, 40)).astype(np.float32)
+    cb = g.standard_normal((L, K, Df)).astype(np.float32)
+    got = quick.compute_final_feature_map(torch.from_numpy(wmap).to(gpu), torch.from_numpy(cb).to(gpu))
+    ref = (cb.reshape(-1, Df).T.astype(np.float64) @ wmap.reshape(L * K, -1).astype(np.float64)).reshape(Df, 24, 40)
+    scale = np.abs(ref).max()
+    assert got.shape == (Df, 24, 40)
+    np.testing.assert_allclose(got.cpu().numpy() / scale, ref / scale, atol=DEC_ATOL, rtol=0)
