@@ -249,9 +249,10 @@ int lsr_abi_version(void);
 int lsr_max_lang_dim(void);
 
 /* Diagnostics: per-stage HIP-event timing on the caller's stream (used by
- * bench.py for the live roofline).  The timing state is per host thread
- * (thread_local): each thread enables, resets and queries its own stages;
- * off by default.
+ * bench.py for the live roofline).  One process-wide, thread-safe timer
+ * (atomic switch, mutex-guarded event pool; autograd runs the backward on its
+ * own thread): off by default, and while off the entry points above read one
+ * atomic flag per stage and nothing else.
  * lsr_profile_query fills up to max_stages (name, total ms, call count)
  * triples since the last reset and returns the number filled. */
 void lsr_profile_enable(int on);

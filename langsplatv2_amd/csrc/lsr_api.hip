@@ -11,6 +11,8 @@
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
+#include <atomic>
+#include <mutex>
 #include <utility>
 #include <vector>
 #include "lsr_internal.h"
@@ -55,34 +57,43 @@ enum Stage { ST_PRE, ST_SCAN, ST_DUP, ST_SCAN_T, ST_SCATTER, ST_SORT, ST_RENDER,
 const char* kStageNames[ST_N] = {"preprocess", "scan_tiles", "bin_count", "scan_tile_counts", "bin_scatter",
                                  "tile_sort", "render_fwd", "grad_zero", "render_bwd", "preprocess_bwd"};
 
+// Process-wide (the autograd engine runs backward on its own thread, and the
+// caller enables timing on its thread), thread-safe: the switch and mask are
+// atomics read once per stage; the event pool is guarded by a mutex that is
+// only taken while timing is on.  Off, the product path touches nothing.
 struct Prof {
-    bool on = false;
-    unsigned mask = ~0u;   // stages bracketed when on (lsr_profile_stages)
+    std::atomic<bool> on{false};
+    std::atomic<unsigned> mask{~0u};   // stages bracketed when on (lsr_profile_stages)
+    std::mutex mu;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[ST_N];
     size_t used[ST_N] = {};
 };
-thread_local Prof g_prof;   // per host thread: no state shared between callers
+Prof g_prof;
 
 struct StageScope {
     Stage s;
     hipStream_t st;
     bool on;
-    StageScope(Stage s_, hipStream_t st_) : s(s_), st(st_), on(g_prof.on && ((g_prof.mask >> s_) & 1u))
+    size_t slot = 0;
+    StageScope(Stage s_, hipStream_t st_) : s(s_), st(st_), on(g_prof.on.load(std::memory_order_relaxed) &&
+                                                                 ((g_prof.mask.load(std::memory_order_relaxed) >> s_) & 1u))
     {
         if (!on) return;
+        std::lock_guard<std::mutex> lk(g_prof.mu);
         auto& v = g_prof.ev[s];
         if (g_prof.used[s] == v.size()) {
             hipEvent_t a, b;
             if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) { on = false; return; }
             v.push_back({a, b});
         }
-        (void)hipEventRecord(v[g_prof.used[s]].first, st);
+        slot = g_prof.used[s]++;
+        (void)hipEventRecord(v[slot].first, st);
     }
     ~StageScope()
     {
         if (!on) return;
-        (void)hipEventRecord(g_prof.ev[s][g_prof.used[s]].second, st);
-        g_prof.used[s]++;
+        std::lock_guard<std::mutex> lk(g_prof.mu);
+        (void)hipEventRecord(g_prof.ev[s][slot].second, st);
     }
 };
 
@@ -389,12 +400,12 @@ int lsr_max_lang_dim(void) { return 64; }
 
 void lsr_profile_enable(int on)
 {
-    g_prof.on = on != 0;
+    g_prof.on.store(on != 0);
 }
 
 int lsr_profile_stages(const char* names)
 {
-    if (!names || !*names) { g_prof.mask = ~0u; return LSR_OK; }
+    if (!names || !*names) { g_prof.mask.store(~0u); return LSR_OK; }
     unsigned m = 0;
     const char* p = names;
     while (*p) {
@@ -407,17 +418,19 @@ int lsr_profile_stages(const char* names)
         m |= 1u << hit;
         p = *e ? e + 1 : e;
     }
-    g_prof.mask = m;
+    g_prof.mask.store(m);
     return LSR_OK;
 }
 
 void lsr_profile_reset(void)
 {
+    std::lock_guard<std::mutex> lk(g_prof.mu);
     for (int k = 0; k < ST_N; k++) g_prof.used[k] = 0;
 }
 
 int lsr_profile_query(const char** names, double* ms, int64_t* calls, int max_stages)
 {
+    std::lock_guard<std::mutex> lk(g_prof.mu);
     int n = 0;
     for (int k = 0; k < ST_N && n < max_stages; k++, n++) {
         double tot = 0.0;
