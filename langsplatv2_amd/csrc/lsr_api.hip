@@ -265,13 +265,14 @@ int lsr_quick_decode(const float* weight_map, const float* codebooks, int L, int
     if (L == 0 || H == 0 || W == 0) return LSR_OK;
     if (!weight_map || !codebooks || !out) return LSR_EINVAL;
     hipStream_t st = (hipStream_t)stream;
-    float* G = nullptr;
-    if (normalize) {
+    void* ws = nullptr;
+    const size_t wsb = lsr::quick_decode_workspace_bytes(L, K, Df, normalize);
+    if (wsb) {
         if (!alloc) return LSR_EINVAL;
-        G = (float*)alloc(alloc_ctx, sizeof(float) * (size_t)L * K * K, LSR_BUF_DECODE);
-        if (!G) return LSR_ENOMEM;
+        ws = alloc(alloc_ctx, wsb, LSR_BUF_DECODE);
+        if (!ws) return LSR_ENOMEM;
     }
-    if (lsr::launch_quick_decode(weight_map, codebooks, L, K, Df, H, W, normalize, eps, G, out, st) != hipSuccess)
+    if (lsr::launch_quick_decode(weight_map, codebooks, L, K, Df, H, W, normalize, eps, ws, out, st) != hipSuccess)
         return LSR_EHIP;
     return LSR_OK;
 }

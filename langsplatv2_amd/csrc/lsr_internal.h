@@ -103,8 +103,9 @@ hipError_t launch_topk_code_bwd(const float* logits, const float* g, int64_t N, 
 size_t knn_workspace_bytes(int64_t N, size_t sort_temp);
 hipError_t knn_sort_temp_bytes(int64_t N, size_t* bytes);
 hipError_t launch_knn_dist2(const float* points, int64_t N, float* out, uint8_t* ws, size_t sort_temp, hipStream_t st);
+size_t quick_decode_workspace_bytes(int L, int K, int Df, int normalize);
 hipError_t launch_quick_decode(const float* wmap, const float* cb, int L, int K, int Df, int H, int W, int normalize,
-                               float eps, float* G, float* out, hipStream_t st);
+                               float eps, void* ws, float* out, hipStream_t st);
 
 // lang_loss.hip
 size_t lang_loss_workspace_bytes(int S, int W, int H, int* waves);

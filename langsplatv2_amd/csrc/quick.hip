@@ -138,16 +138,268 @@ __global__ void __launch_bounds__(64) k_quick_decode(const float* __restrict__ w
     }
 }
 
+// ---------------------------------------------------------------------------
+// Split-f16 decode (default).  The f32 MFMA above runs at 1/16 of the f16 rate
+// and made the decode matrix-core bound (3.7 ms at 1 Mpix, 3 levels; the
+// output is 6.3 GB, 1.05 ms at 6 TB/s).  Here every f32 operand x is split
+// into x_hi = f16(x), x_lo = f16(x - x_hi) (22 significant bits together) and
+//   F = W_hi C_hi + W_hi C_lo + W_lo C_hi
+// runs on v_mfma_f32_16x16x32_f16 with f32 accumulation: the products are
+// exact in f32, the dropped W_lo C_lo term is <= 2^-22 |W||C|, i.e. within a
+// few f32 ulps of the exact-f32 decode.  The codebook is scaled per level by a
+// power of two into [0.5, 1) before the split (f16 range; exact) and the
+// scale is applied to the results.
+//
+// Orientation: A = W^T (rows = 16 pixels along x, K = codes), B = codebook
+// (K = codes, cols = 16 output dims), so a lane's result is 4 CONSECUTIVE
+// pixels of one output dim: one 16-B store per lane, each store instruction a
+// full 64-B segment per dim.  The L2 norm needs |F_p| before any dim of pixel
+// p is written: |F_p|^2 = w_p^T G w_p with the level's Gram matrix
+// G = CB CB^T (64 x 64, exact f32, k_codebook_gram), H^T = W^T G on the same
+// split-f16 MFMA with the same A fragments (1/8 of the decode's matrix work),
+// then sum_m W[m][p] H[m][p] with W re-read as 16-B rows and a 16-lane sum.
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+#ifndef LSR_DEC_PB
+#define LSR_DEC_PB 4      // 16-pixel blocks whose A fragments stay in registers across the dim blocks
+#endif
+#ifndef LSR_DEC_WAVES
+#define LSR_DEC_WAVES 2   // min waves per SIMD (caps VGPRs at 256; 176 used); uncapped it took 214 = 1 wave
+#endif
+
+// Fragments: frag[(((l * NDB + db) * 2 + s) * 64 + lane) * 2 + {0: hi, 1: lo}] holds, for lane
+// (li = lane & 15, lg = lane >> 4), B[k = 8 lg + j][col li] of K-step s and dim block db:
+// scale_l * CB[l][32 s + 8 lg + j][16 db + li], j = 0..7, split into f16 hi / lo.
+// scales[l] = 1 / scale_l.  One workgroup per level.
+__global__ void __launch_bounds__(256) k_codebook_frag(const float* __restrict__ cb, int K, int Df,
+                                                       uint4* __restrict__ frag, float* __restrict__ scales)
+{
+    const int l = blockIdx.x;
+    const float* c = cb + (size_t)l * K * Df;
+    __shared__ float red[256];
+    float m = 0.f;
+    for (int i = threadIdx.x; i < K * Df; i += 256) m = fmaxf(m, fabsf(c[i]));
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + w]);
+        __syncthreads();
+    }
+    const float mx = red[0];
+    int e = 0;
+    if (mx > 0.f && mx < 3.0e38f) (void)frexpf(mx, &e);   // mx = f 2^e, f in [0.5, 1)
+    const float scale = ldexpf(1.f, -e);
+    if (threadIdx.x == 0) scales[l] = ldexpf(1.f, e);
+    const int NDB = Df / 16;
+    for (int idx = threadIdx.x; idx < NDB * 128; idx += 256) {
+        const int lane = idx & 63, s = (idx >> 6) & 1, db = idx >> 7;
+        const int li = lane & 15, lg = lane >> 4;
+        h8 hi, lo;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const float v = c[(size_t)(32 * s + 8 * lg + j) * Df + 16 * db + li] * scale;
+            const _Float16 h = (_Float16)v;
+            hi[j] = h;
+            lo[j] = (_Float16)(v - (float)h);
+        }
+        uint4* dst = frag + ((((size_t)l * NDB + db) * 2 + s) * 64 + lane) * 2;
+        dst[0] = __builtin_bit_cast(uint4, hi);
+        dst[1] = __builtin_bit_cast(uint4, lo);
+    }
+}
+
+// 16-lane sum (every lane of each 16-lane row gets its row's total)
+__device__ __forceinline__ float row16_sum(float v)
+{
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad [1,0,3,2]
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad [2,3,0,1]
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));  // row_mirror
+    return v;
+}
+
+// F tile of pixel row pb for one 16-dim block: the split product, small terms first
+#define LSR_DEC_MFMA6(acc, pb)                                                                  \
+    do {                                                                                        \
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(Wl[pb][0], c0h, acc, 0, 0, 0);             \
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(Wh[pb][0], c0l, acc, 0, 0, 0);             \
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(Wl[pb][1], c1h, acc, 0, 0, 0);             \
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(Wh[pb][1], c1l, acc, 0, 0, 0);             \
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(Wh[pb][0], c0h, acc, 0, 0, 0);             \
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(Wh[pb][1], c1h, acc, 0, 0, 0);             \
+    } while (0)
+
+template <bool NORM, bool VEC>
+__global__ void __launch_bounds__(64, LSR_DEC_WAVES) k_quick_decode_h(const float* __restrict__ wmap, int L, int Df,
+                                                                      int W, int H, const uint4* __restrict__ frag,
+                                                                      const float* __restrict__ scales,
+                                                                      const uint4* __restrict__ gfrag,
+                                                                      const float* __restrict__ gscales,
+                                                                      float* __restrict__ out, float eps)
+{
+    const int lane = threadIdx.x, lg = lane >> 4, li = lane & 15;
+    // one wave = 64 consecutive pixels of one image row, in two halves of two 16-pixel
+    // blocks (PB) whose A fragments (hi + lo, 32 VGPRs) stay in registers across every
+    // dim block; each dim's 64-B output pieces of a half are adjacent (whole lines)
+    constexpr int PB = LSR_DEC_PB;
+    const int nbx = (W + 63) / 64;
+    const int bx0 = (int)(blockIdx.x % nbx) * 64, y = (int)(blockIdx.x / nbx);
+    const size_t HW = (size_t)W * H;
+    const int NDB = Df / 16;
+    for (int l = 0; l < L; l++) {
+        const float sc = scales[l];
+        const uint4* fl = frag + (size_t)l * NDB * 256;   // per dim block: 2 K-steps x 64 lanes x (hi, lo)
+        for (int half = 0; half < 4 / PB; half++) {
+            const int bx = bx0 + 16 * PB * half;
+            if (bx >= W) break;
+            // A = W^T: lane (li, lg) holds W[32 s + 8 lg + j][x = bx + 16 pb + li]
+            h8 Wh[PB][2], Wl[PB][2];
+#pragma unroll
+            for (int pb = 0; pb < PB; pb++) {
+                const int xa = bx + 16 * pb + li;
+                const size_t pa = (size_t)y * W + min(xa, W - 1);
+#pragma unroll
+                for (int s = 0; s < 2; s++)
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        const float w = wmap[(size_t)(l * 64 + 32 * s + 8 * lg + j) * HW + pa];
+                        const float v = xa < W ? w : 0.f;
+                        const _Float16 h = (_Float16)v;
+                        Wh[pb][s][j] = h;
+                        Wl[pb][s][j] = (_Float16)(v - (float)h);
+                    }
+            }
+            float mul[PB][4];
+#pragma unroll
+            for (int pb = 0; pb < PB; pb++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) mul[pb][r] = sc;
+            if constexpr (NORM) {
+                // |F_p|^2 = sum_m W[m][p] (G W)[m][p]; lane (m = 16 mb + li, lg) gets (G W)[m] at x = 4 lg + r
+                float sq[PB][4];
+#pragma unroll
+                for (int pb = 0; pb < PB; pb++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) sq[pb][r] = 0.f;
+                const uint4* gl = gfrag + (size_t)l * 4 * 256;
+#pragma unroll 1
+                for (int mb = 0; mb < 4; mb++) {
+                    const uint4* f = gl + (size_t)mb * 256 + lane * 2;
+                    const h8 c0h = __builtin_bit_cast(h8, f[0]), c0l = __builtin_bit_cast(h8, f[1]);
+                    const h8 c1h = __builtin_bit_cast(h8, f[128]), c1l = __builtin_bit_cast(h8, f[129]);
+                    const float* wm = wmap + (size_t)(l * 64 + mb * 16 + li) * HW + (size_t)y * W;
+#pragma unroll
+                    for (int pb = 0; pb < PB; pb++) {
+                        f32x4q acc = {0.f, 0.f, 0.f, 0.f};
+                        LSR_DEC_MFMA6(acc, pb);
+                        const int xo = bx + 16 * pb + 4 * lg;
+                        float wv[4] = {0.f, 0.f, 0.f, 0.f};
+                        if (VEC && xo + 3 < W) {
+                            const float4 v = *reinterpret_cast<const float4*>(wm + xo);
+                            wv[0] = v.x; wv[1] = v.y; wv[2] = v.z; wv[3] = v.w;
+                        } else {
+#pragma unroll
+                            for (int r = 0; r < 4; r++)
+                                if (xo + r < W) wv[r] = wm[xo + r];
+                        }
+#pragma unroll
+                        for (int r = 0; r < 4; r++) sq[pb][r] = fmaf(wv[r], acc[r], sq[pb][r]);
+                    }
+                }
+                const float gs = gscales[l];
+#pragma unroll
+                for (int pb = 0; pb < PB; pb++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++)
+                        mul[pb][r] = sc / (sqrtf(fmaxf(row16_sum(sq[pb][r]) * gs, 0.f)) + eps);
+            }
+            // the next dim block's fragments are loaded while this one computes
+            const uint4* fp = fl + lane * 2;
+            uint4 n0h = fp[0], n0l = fp[1], n1h = fp[128], n1l = fp[129];
+#pragma unroll 1
+            for (int db = 0; db < NDB; db++) {
+                const h8 c0h = __builtin_bit_cast(h8, n0h), c0l = __builtin_bit_cast(h8, n0l);
+                const h8 c1h = __builtin_bit_cast(h8, n1h), c1l = __builtin_bit_cast(h8, n1l);
+                if (db + 1 < NDB) {
+                    const uint4* f = fp + (size_t)(db + 1) * 256;
+                    n0h = f[0]; n0l = f[1]; n1h = f[128]; n1l = f[129];
+                }
+                float* od = out + (size_t)(l * Df + db * 16 + li) * HW + (size_t)y * W;
+#pragma unroll
+                for (int pb = 0; pb < PB; pb++) {
+                    f32x4q acc = {0.f, 0.f, 0.f, 0.f};
+#ifdef LSR_PROBE_DEC_NOMFMA   // timing probe only (wrong results): stores without the matrix work
+                    acc = f32x4q{(float)db, (float)pb, (float)lane, 1.f};
+#else
+                    LSR_DEC_MFMA6(acc, pb);
+#endif
+                    const int xo = bx + 16 * pb + 4 * lg;
+                    float* o = od + xo;
+#ifdef LSR_PROBE_DEC_NOSTORE   // timing probe only: matrix work without the stores
+                    if (acc[0] != 1234.5f) continue;
+#endif
+                    if (VEC && xo + 3 < W) {
+                        *reinterpret_cast<float4*>(o) = make_float4(acc[0] * mul[pb][0], acc[1] * mul[pb][1],
+                                                                    acc[2] * mul[pb][2], acc[3] * mul[pb][3]);
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 4; r++)
+                            if (xo + r < W) o[r] = acc[r] * mul[pb][r];
+                    }
+                }
+            }
+        }
+    }
+}
+
+size_t quick_decode_workspace_bytes(int L, int K, int Df, int normalize)
+{
+#ifdef LSR_DECODE_F32
+    return normalize ? sizeof(float) * (size_t)L * K * K : 0;
+#else
+    // codebook fragments (L * Df/16 * 2 * 64 * 32 B) + per-level scales; with normalisation the
+    // Gram matrices (L * 64 * 64 f32), their fragments (L * 4 * 2 * 64 * 32 B) and scales
+    return (size_t)L * Df * 256 + 256 + (normalize ? (size_t)L * K * K * 4 + (size_t)L * 64 * 256 + 256 : 0);
+#endif
+}
+
 hipError_t launch_quick_decode(const float* wmap, const float* cb, int L, int K, int Df, int H, int W, int normalize,
-                               float eps, float* G, float* out, hipStream_t st)
+                               float eps, void* ws, float* out, hipStream_t st)
 {
     if (L == 0 || H == 0 || W == 0) return hipSuccess;
+#ifdef LSR_DECODE_F32
+    const unsigned nb = (unsigned)(((W + 15) / 16) * ((H + 3) / 4));
+    float* G = (float*)ws;
     if (normalize) {
         dim3 g((unsigned)((K * K + 255) / 256), (unsigned)L);
         k_codebook_gram<<<g, 256, 0, st>>>(cb, K, Df, G);
     }
-    const unsigned nb = (unsigned)(((W + 15) / 16) * ((H + 3) / 4));
     k_quick_decode<64><<<nb, 64, 0, st>>>(wmap, L, Df, W, H, cb, G, out, eps, normalize);
+#else
+    const unsigned nb = (unsigned)(((W + 63) / 64) * H);
+    uint8_t* p = (uint8_t*)ws;
+    uint4* frag = (uint4*)p;
+    float* scales = (float*)(p + (size_t)L * Df * 256);
+    k_codebook_frag<<<L, 256, 0, st>>>(cb, K, Df, frag, scales);
+    const bool vec = (W % 4) == 0;
+    if (normalize) {
+        float* G = (float*)(p + (size_t)L * Df * 256 + 256);
+        uint4* gfrag = (uint4*)((uint8_t*)G + (size_t)L * K * K * 4);
+        float* gscales = (float*)((uint8_t*)gfrag + (size_t)L * 64 * 256);
+        dim3 g((unsigned)((K * K + 255) / 256), (unsigned)L);
+        k_codebook_gram<<<g, 256, 0, st>>>(cb, K, Df, G);
+        k_codebook_frag<<<L, 256, 0, st>>>(G, K, K, gfrag, gscales);
+        if (vec)
+            k_quick_decode_h<true, true><<<nb, 64, 0, st>>>(wmap, L, Df, W, H, frag, scales, gfrag, gscales, out, eps);
+        else
+            k_quick_decode_h<true, false><<<nb, 64, 0, st>>>(wmap, L, Df, W, H, frag, scales, gfrag, gscales, out, eps);
+    } else {
+        if (vec)
+            k_quick_decode_h<false, true><<<nb, 64, 0, st>>>(wmap, L, Df, W, H, frag, scales, nullptr, nullptr, out, eps);
+        else
+            k_quick_decode_h<false, false><<<nb, 64, 0, st>>>(wmap, L, Df, W, H, frag, scales, nullptr, nullptr, out,
+                                                               eps);
+    }
+#endif
     return hipGetLastError();
 }
 

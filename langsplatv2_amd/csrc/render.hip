@@ -1029,15 +1029,30 @@ struct BwdFrags {
     float momB[16];       // moment (l&15) of block pixel 4t + (l>>4)
 };
 
+#ifndef LSR_BWD_BRFREE
+#define LSR_BWD_BRFREE 1   // bwd: loads issued unconditionally at clamped (valid) addresses, results selected:
+                           // no exec-skip branches around loads, so the compiler's vmcnt waits stay exact
+                           // (a conditional load makes every later wait a vmcnt(0), defeating the prefetches)
+#endif
 template <int NL>
 __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int bx, int by)
 {
     const Cam& cm = b.f.cam;
     const int qx = bx + (q & 7), qy = by + (q >> 3);
+#if LSR_BWD_BRFREE
+    const bool ok = qx < cm.W && qy < cm.H && c < 3 + b.f.D;
+    const size_t HW = (size_t)cm.H * cm.W;
+    const size_t pix = (size_t)min(qy, cm.H - 1) * cm.W + min(qx, cm.W - 1);
+    const float* src = c < 3 ? b.dout_color + (size_t)c * HW : b.dout_lang + (size_t)min(c - 3, max(b.f.D - 1, 0)) * HW;
+    if (c >= 3 && b.f.D == 0) src = b.dout_color;
+    const float v = src[pix];
+    return ok ? v : 0.f;
+#else
     if (qx >= cm.W || qy >= cm.H || c >= 3 + b.f.D) return 0.f;
     const size_t HW = (size_t)cm.H * cm.W;
     const size_t pix = (size_t)qy * cm.W + qx;
     return c < 3 ? b.dout_color[c * HW + pix] : b.dout_lang[(size_t)(c - 3) * HW + pix];
+#endif
 }
 
 #define LSR_DOT_STRIDE 68   // sDot row stride: conflict-free fragment stores
@@ -1118,9 +1133,17 @@ __device__ __forceinline__ int stage_candidates_geo_rec(WaveStageG& st, int carr
 template <int NL>
 __device__ __forceinline__ float feature_at(const RenderArgs& a, uint32_t gid, int c)
 {
+#if LSR_BWD_BRFREE
+    const bool ok = c < 3 + a.D;
+    const float* src = c < 3 ? a.rgb + 3 * (size_t)gid + c
+                             : (ok ? a.lang + (size_t)gid * a.D + (c - 3) : a.rgb + 3 * (size_t)gid);
+    const float v = *src;
+    return ok ? v : 0.f;
+#else
     if (c < 3) return a.rgb[3 * (size_t)gid + c];
     if (c - 3 < a.D) return a.lang[(size_t)gid * a.D + (c - 3)];
     return 0.f;
+#endif
 }
 
 #ifdef LSR_EXP_NOMF   // timing experiment only (wrong results): no matrix-core work
@@ -1133,6 +1156,24 @@ __device__ __forceinline__ float feature_at(const RenderArgs& a, uint32_t gid, i
 // requiring grad).  Then dL/dlang[j][c] = sum_p aT[j][p] dL/dout[c][p] is all
 // that is left: no dot products, no dL/dalpha recurrence, no moments, and the
 // rows go straight into the (N, D) output (b.grad_acc, b.VP = D).
+// Phase timing of the backward (diagnostic builds only, -DLSR_BWD_STAMPS):
+// per wave, s_memtime deltas summed per phase, added once per wave into
+// g_bwd_stamps (read by lsr_dbg_bwd_stamps).  Each stamp waits for the wave's
+// outstanding LDS operations (the counter read shares lgkmcnt), so phase
+// boundaries are slightly sharper than in the product build.
+#ifdef LSR_BWD_STAMPS
+__device__ unsigned long long g_bwd_stamps[16];
+#define BWD_STAMP_DECL unsigned long long st_acc[10] = {}; unsigned long long st_t = __builtin_amdgcn_s_memtime();
+#define BWD_STAMP(i) do { const unsigned long long _t = __builtin_amdgcn_s_memtime(); st_acc[i] += _t - st_t; st_t = _t; } while (0)
+#define BWD_COUNT(i) do { st_acc[i] += 1; } while (0)
+#define BWD_STAMP_FLUSH() do { if (threadIdx.x == 0) for (int _i = 0; _i < 10; _i++) atomicAdd(&g_bwd_stamps[_i + (threadIdx.x & 64)], st_acc[_i]); } while (0)
+#else
+#define BWD_STAMP_DECL
+#define BWD_STAMP(i) do {} while (0)
+#define BWD_COUNT(i) do {} while (0)
+#define BWD_STAMP_FLUSH() do {} while (0)
+#endif
+
 // SP (with LO): the language input is the quick path's sparse (weights,
 // codes) rows; the per-channel gradient rows are gathered at each Gaussian's
 // codes into dL/dweights (b.qw_acc, (P, K)) instead of being added densely.
@@ -1202,6 +1243,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     const int last = inside ? (int)a.n_contrib[pix] : 0;
     const int wmax = wave_max_i(last);
     if (wmax == 0) return;
+    BWD_STAMP_DECL
     // entries past a group's end are read unconditionally (immediate-offset
     // loads, no index clamps): keep them finite
     for (int e = lane; e < 80; e += 64) {
@@ -1215,13 +1257,23 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #pragma unroll
         for (int t = 0; t < KS; t++)
 #pragma unroll
-            for (int pb = 0; pb < 4; pb++) dotB[t][pb] = gd_at<NL>(b, 4 * t + lg, pb * 16 + li, pm.bx, pm.by);
+            for (int pb = 0; pb < 4; pb++)
+#ifdef LSR_PROBE_NOPRO   // timing probe only (wrong results): no prologue dL/dout loads
+                dotB[t][pb] = (float)(t * 4 + pb + lane);
+#else
+                dotB[t][pb] = gd_at<NL>(b, 4 * t + lg, pb * 16 + li, pm.bx, pm.by);
+#endif
     }
 #if LSR_BWD_VMOM
 #pragma unroll
     for (int nb = 0; nb < NBC; nb++)
 #pragma unroll
-        for (int t = 0; t < 16; t++) chB[nb][t] = gd_at<NL>(b, 3 + nb * 16 + li, 4 * t + lg, pm.bx, pm.by);
+        for (int t = 0; t < 16; t++)
+#ifdef LSR_PROBE_NOPRO
+            chB[nb][t] = (float)(t + lane);
+#else
+            chB[nb][t] = gd_at<NL>(b, 3 + nb * 16 + li, 4 * t + lg, pm.bx, pm.by);
+#endif
     if constexpr (!LO)
         sDrgb[lane] = make_float4(gd_at<NL>(b, 0, lane, pm.bx, pm.by), gd_at<NL>(b, 1, lane, pm.bx, pm.by),
                                   gd_at<NL>(b, 2, lane, pm.bx, pm.by), 0.f);
@@ -1255,41 +1307,61 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     // ahead, so staging never waits on a dependent gather (9 more VGPRs: off
     // for the widest language set, where they would spill)
     constexpr bool SPF = LSR_BWD_SPLAT_PF && NL <= 32;
-    uint32_t gid1 = (wmax - 1 - lane >= 0) ? a.point_list[rs + wmax - 1 - lane] : 0u;
+#if LSR_BWD_BRFREE
+    // tile-list position clamped to the range (wmax >= 1: position 0 exists), result selected
+    auto pl_at = [&](int q) -> uint32_t { const uint32_t v = a.point_list[rs + max(q, 0)]; return q >= 0 ? v : 0u; };
+#else
+    auto pl_at = [&](int q) -> uint32_t { return q >= 0 ? a.point_list[rs + q] : 0u; };
+#endif
+    uint32_t gid1 = pl_at(wmax - 1 - lane);
     uint32_t gid2 = 0u;
     float4 A1 = make_float4(0.f, 0.f, 0.f, 0.f), B1 = A1;
     if constexpr (SPF) {
-        gid2 = (wmax - 65 - lane >= 0) ? a.point_list[rs + wmax - 65 - lane] : 0u;
+        gid2 = pl_at(wmax - 65 - lane);
+#if LSR_BWD_BRFREE
+        A1 = a.splatA[gid1];   // gid 0 for positions past the range: a valid record, never staged
+        B1 = a.splatB[gid1];
+#else
         if (wmax - 1 - lane >= 0) {
             A1 = a.splatA[gid1];
             B1 = a.splatB[gid1];
         }
+#endif
     }
+    BWD_STAMP(0);
     for (int c0 = 0; c0 < wmax; c0 += 64) {
         const int p = wmax - 1 - (c0 + lane);
         const bool valid = p >= 0;
         int n;
+        BWD_COUNT(8);
         if constexpr (SPF) {
             const uint32_t gid = gid1;
             const float4 Ac = A1, Bc = B1;
             gid1 = gid2;
+#if LSR_BWD_BRFREE
+            A1 = a.splatA[gid1];
+            B1 = a.splatB[gid1];
+#else
             A1 = make_float4(0.f, 0.f, 0.f, 0.f);
             B1 = A1;
             if (p - 64 >= 0) {
                 A1 = a.splatA[gid1];
                 B1 = a.splatB[gid1];
             }
-            gid2 = (p - 128 >= 0) ? a.point_list[rs + p - 128] : 0u;
+#endif
+            gid2 = pl_at(p - 128);
             n = carry + stage_candidates_geo_rec(st, carry, valid, gid, p, pm.bx, pm.by, Ac, Bc);
         } else {
             const uint32_t gid = gid1;
-            gid1 = (p - 64 >= 0) ? a.point_list[rs + p - 64] : 0u;
+            gid1 = pl_at(p - 64);
             n = carry + stage_candidates_geo(st, carry, valid, gid, p, pm.bx, pm.by, a.splatA, a.splatB);
         }
         const int nfull = (c0 + 64 >= wmax) ? n : (n & ~15);
+        BWD_STAMP(1);
 
         for (int g0 = 0; g0 < nfull; g0 += 16) {
             const int kn = min(16, nfull - g0);
+            BWD_COUNT(9);
             // A fragments of the dot product: feature 4t+lg of candidate g0+li,
             // gathered now, consumed after phase 1
 #if LSR_BWD_AF_PF
@@ -1299,7 +1371,11 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 const uint32_t gi = st.gid[g0 + (li < kn ? li : 0)];
 #pragma unroll
                 for (int t = 0; t < KS; t++)
+#ifdef LSR_PROBE_NOFEAT   // timing probe only (wrong results): no feature gather
+                    af[t] = __uint_as_float(gi) * 1e-30f;
+#else
                     af[t] = feature_at<NL>(a, gi, 4 * t + lg);
+#endif
             }
             // phase 1: G of the 16 candidates (0 where the pair does not
             // contribute), independent across candidates; straight-line code
@@ -1332,6 +1408,20 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                     }
                 }
             }
+            BWD_STAMP(2);
+#ifdef LSR_PROBE_ADDVALU   // timing probe only: LSR_PROBE_ADDVALU extra independent VALU ops per group
+            {
+                float z0 = __uint_as_float(lane), z1 = z0 + 1.f, z2 = z0 + 2.f, z3 = z0 + 3.f;
+#pragma unroll
+                for (int i = 0; i < LSR_PROBE_ADDVALU / 4; i++) {
+                    asm volatile("v_fmac_f32 %0, %1, %1" : "+v"(z0) : "v"(z1));
+                    asm volatile("v_fmac_f32 %0, %1, %1" : "+v"(z1) : "v"(z2));
+                    asm volatile("v_fmac_f32 %0, %1, %1" : "+v"(z2) : "v"(z3));
+                    asm volatile("v_fmac_f32 %0, %1, %1" : "+v"(z3) : "v"(z0));
+                }
+                if (z0 == 1234.5f) sAT[lane] = z3;
+            }
+#endif
             // dot[k][p] of the group's candidates on MFMA: (16 x C) . (C x 64)
             if constexpr (!LO) {
                 f32x4 acc[4];
@@ -1358,6 +1448,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             }
 #endif
             wave_lds_fence();
+            BWD_STAMP(3);
             // phase 2: the serial back-to-front recurrence per pixel.  S is the
             // colour accumulated behind the current instance (the upstream
             // "accum_rec" once the last contributor is folded in):
@@ -1401,6 +1492,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 }
             }
             wave_lds_fence();
+            BWD_STAMP(4);
 #if LSR_BWD_VMOM
             // phase 3: language gradients on MFMA; RGB gradients and the six
             // pixel moments sum_p u {1, lx, ly, lx^2, lx ly, ly^2} on the VALU.
@@ -1554,6 +1646,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             }
 #endif
             wave_lds_fence();
+            BWD_STAMP(5);
             if constexpr (SP) {
                 // (slot, code) pairs: dL/dw[gid][m] += row[slot][idx[gid][m]]
                 const int K = a.K;
@@ -1588,6 +1681,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 }
             }
             wave_lds_fence();
+            BWD_STAMP(6);
         }
         // carry the partial group to the front of the stage
         carry = n - nfull;
@@ -1597,7 +1691,9 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             st.gid[lane] = st.gid[nfull + lane];
         }
         wave_lds_fence();
+        BWD_STAMP(7);
     }
+    BWD_STAMP_FLUSH();
 }
 
 
@@ -2212,6 +2308,18 @@ hipError_t launch_render_bwd_lang_sparse(const RenderBwdArgs& b, hipStream_t st)
     }
     return hipGetLastError();
 }
+
+#ifdef LSR_BWD_STAMPS
+}  // namespace lsr
+extern "C" int lsr_dbg_bwd_stamps(unsigned long long* out)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lsr::g_bwd_stamps), sizeof(unsigned long long) * 16) != hipSuccess)
+        return 3;
+    unsigned long long z[16] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(lsr::g_bwd_stamps), z, sizeof(z)) == hipSuccess ? 0 : 3;
+}
+namespace lsr {
+#endif
 
 bool bwd_lang_direct(int D)
 {
