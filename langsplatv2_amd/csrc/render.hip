@@ -1072,12 +1072,26 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
 #ifndef LSR_GRP_STRIDE
 #define LSR_GRP_STRIDE 66   // dot/u and aT tiles: conflict-free A-fragment reads (li*66 mod 32 = 2 li)
 #endif
+#ifndef LSR_BWD_RSCAT
+#define LSR_BWD_RSCAT 1     // bwd: phase-3 sums reduced two values per permlane swap, parked in LDS
+#endif
+#define LSR_MOM9_STRIDE 12  // reduced moment + colour sums per candidate (16-B aligned rows)
+static_assert(!LSR_BWD_RSCAT || LSR_BWD_ALIAS, "the reduced sums are parked in the aliased aT tile");
 #define LSR_LOG2E 1.4426950408889634f
 #ifdef LSR_MF_NO_ATOMIC   // timing experiment only: keeps the work, drops the atomics
 #define LSR_MF_ATOMIC(ptr, v) do { if ((v) == 1234.5678f) atomicAdd((ptr), (v)); } while (0)
 #else
 #define LSR_MF_ATOMIC(ptr, v) atomicAdd((ptr), (v))
 #endif
+
+// Lane mask of |v| < bound, straight from the compare (the compiler otherwise
+// round-trips a ballot's operand through a VGPR: two extra VALU per use).
+__device__ __forceinline__ uint64_t lanes_abs_lt(float v, float bound)
+{
+    uint64_t m;
+    asm("v_cmp_gt_f32_e64 %0, %1, |%2|" : "=s"(m) : "s"(bound), "v"(v));
+    return m;
+}
 
 // Per-wave LDS staging of one chunk's candidate geometry (no feature rows).
 // 80 entries: up to 15 candidates carried over from the previous chunk + 64.
@@ -1213,7 +1227,8 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     // 12 instead of 10 resident waves per CU at D = 16.
     constexpr int DUG = (16 * GS > 16 * GRS) ? 16 * GS : 16 * GRS;
     __shared__ float sDU[DUG];        // dot[k][p] -> u[k][p] -> the group's gradient rows
-    __shared__ float sAT[16 * GS];    // G[k][p] (phase 1) -> aT[k][p] (phase 2) -> moments
+    __shared__ __attribute__((aligned(16))) float sAT[16 * GS];   // G[k][p] (phase 1) -> aT[k][p] (phase 2) -> moments
+    static_assert(16 * LSR_MOM9_STRIDE <= 16 * GS, "moment rows must fit the aT tile");
     float* const sGr = sDU;
     float* const sMom = sAT;
 #else
@@ -1378,20 +1393,26 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #endif
             }
             // phase 1: G of the 16 candidates (0 where the pair does not
-            // contribute), independent across candidates; straight-line code
-            uint32_t near_any = 0u;
+            // contribute), independent across candidates; straight-line code.
+            // The forward's exponent cut (power < B.z) needs no test here: below
+            // it alpha < e^-0.02 / 255, far outside the fast exp's error band, so
+            // the alpha test rejects those pairs.  Lanes in the band are collected
+            // as a lane mask (scalar ORs), not per-lane flags.
+            uint64_t near_m = 0u;
+            const int kn_u = __builtin_amdgcn_readfirstlane(kn);   // uniform: scalar compares below
 #pragma unroll LSR_P1_UNROLL
             for (int k = 0; k < 16; k++) {
                 const float4 A = st.A[g0 + k];
                 const float4 B = st.B[g0 + k];
                 const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
-                const bool cj = (k < kn) & (__float_as_int(B.w) < last) & !(power > 0.0f) & !(power < B.z);
-                const float G = __builtin_amdgcn_exp2f(power * LSR_LOG2E);
+                const bool cj = (k < kn_u) && (__float_as_int(B.w) < last) && !(power > 0.0f);
+                // G = 0 for a non-candidate pair: alpha - 1/255 is then far below the band
+                const float G = cj ? __builtin_amdgcn_exp2f(power * LSR_LOG2E) : 0.f;
                 const float d = fminf(0.99f, B.y * G) - (1.0f / 255.0f);
-                near_any |= (uint32_t)(cj & (fabsf(d) < 2e-8f));
-                sAT[k * GS + lane] = (cj & (d >= 0.f)) ? G : 0.f;
+                near_m |= lanes_abs_lt(d, 2e-8f);
+                sAT[k * GS + lane] = d >= 0.f ? G : 0.f;
             }
-            if (wave_any(near_any != 0u)) {
+            if (near_m != 0u) {
                 // the 1/255 decision must be the forward's: lanes inside the fast
                 // exp's error band re-evaluate with the forward's exp (rare)
                 for (int k = 0; k < kn; k++) {
@@ -1539,12 +1560,41 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                     M5 = fmaf(ly * ly, R0, M5);
                 }
             }
+#if LSR_BWD_RSCAT
+            // The nine partial sums over the four lane groups, reduced two at a
+            // time: a permlane swap exchanges half of one value for half of
+            // another, so swap + add halves two values' lane groups at once
+            // (8 swaps + 8 adds instead of 18 xor-exchanges).  Row lg then holds
+            // value slot s0(lg) of Y0 and 4 + s0(lg) of Y1 (slots: M0..M5, C0..C2);
+            // the rows park them in the moment area (sAT is free once the loop
+            // above has read it: a wave's LDS operations complete in order).
+            {
+                auto red32 = [](float x, float y) {
+                    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+                    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+                };
+                auto red16 = [](float x, float y) {
+                    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+                    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+                };
+                const float Y0 = red16(red32(M0, M1), red32(M2, M3));   // rows: M0 M2 M1 M3
+                const float Y1 = red16(red32(M4, M5), red32(C0, C1));   // rows: M4 C0 M5 C1
+                const float X4 = red32(C2, C2);
+                const float Y2 = red16(X4, X4);                         // row 0: C2
+                const int s0 = ((lg & 1) << 1) | (lg >> 1);
+                float* const mr = sMom + li * LSR_MOM9_STRIDE;
+                mr[s0] = Y0;
+                mr[4 + s0] = Y1;
+                if (lg == 0) mr[8] = Y2;
+            }
+#else
             M0 += xor_f32<16>(M0); M1 += xor_f32<16>(M1); M2 += xor_f32<16>(M2);
             M3 += xor_f32<16>(M3); M4 += xor_f32<16>(M4); M5 += xor_f32<16>(M5);
             C0 += xor_f32<16>(C0); C1 += xor_f32<16>(C1); C2 += xor_f32<16>(C2);
             M0 += xor_f32<32>(M0); M1 += xor_f32<32>(M1); M2 += xor_f32<32>(M2);
             M3 += xor_f32<32>(M3); M4 += xor_f32<32>(M4); M5 += xor_f32<32>(M5);
             C0 += xor_f32<32>(C0); C1 += xor_f32<32>(C1); C2 += xor_f32<32>(C2);
+#endif
             }
             // Gradient rows of the group staged in LDS (row layout of lsr_device.h:
             // [0..5] geometry, [6..8] colour, [12..) language), then added with
@@ -1558,11 +1608,24 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                     for (int r = 0; r < 4; r++) sGr[(4 * lg + r) * GRS + GCOL0 + chn] = ch[nb][r];
                 }
             }
+#if LSR_BWD_RSCAT
+            if constexpr (!LO) wave_lds_fence();
+#endif
             if (!LO && lane < kn) {   // lane = candidate li (lg = 0)
                 const int j = g0 + lane;
                 const float4 A = st.A[j];
                 const float4 B = st.B[j];
+#if LSR_BWD_RSCAT
+                const float* const mr = sMom + lane * LSR_MOM9_STRIDE;
+                const float4 m03 = *reinterpret_cast<const float4*>(mr);
+                const float4 m47 = *reinterpret_cast<const float4*>(mr + 4);
+                const float S0 = m03.x, S1 = m03.y, S2 = m03.z, S3 = m03.w, S4 = m47.x, S5 = m47.y;
+                C0 = m47.z;
+                C1 = m47.w;
+                C2 = mr[8];
+#else
                 const float S0 = M0, S1 = M1, S2 = M2, S3 = M3, S4 = M4, S5 = M5;
+#endif
                 const float X = A.x - cx, Y = A.y - cy;
                 const float Sdx = fmaf(X, S0, -S1), Sdy = fmaf(Y, S0, -S2);
                 const float Sdxx = fmaf(X, fmaf(X, S0, -2.f * S1), S3);
