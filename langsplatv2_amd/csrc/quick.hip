@@ -351,14 +351,220 @@ __global__ void __launch_bounds__(64, LSR_DEC_WAVES) k_quick_decode_h(const floa
     }
 }
 
+// ---------------------------------------------------------------------------
+// Level-resident decode (default for Df <= 512).  k_quick_decode_h reloads each
+// 16-dim block's codebook fragments from global memory inside its store loop,
+// and a load issued while stores are pending waits for those stores too (one
+// vmcnt counter for both): every dim block paid the write latency of the one
+// before (2.38 ms at 1 Mpix = 2.6 TB/s, while the MFMA work alone takes 0.73 ms
+// and the same store pattern alone sustains 5 TB/s, profiles/r02_decode_store_pattern.txt).
+// Here a persistent workgroup of 8 waves owns one level: its codebook fragments
+// (Df/16 x 4 KB) and the norm factor's fragments (4 x 4 KB) live in LDS for the
+// whole kernel, so the dim loop reads only LDS and the only global loads are a
+// tile's weights, prefetched one tile ahead.
+//
+// The L2 norm needs |F_p|^2 = w_p^T G w_p (G = CB CB^T) before any dim of pixel
+// p is written.  With the Cholesky factor G = L L^T (f64, k_codebook_chol) it
+// is |L^T w_p|^2: a 64-column product on the same A fragments (1/8 of the
+// decode's matrix work), squared and summed along the output rows, with no
+// second read of the weights.
+// G[l][i][j] = sum_d CB[l][i][d] CB[l][j][d]: one wave per (row i, level), lanes along d.
+__global__ void __launch_bounds__(64) k_codebook_gram_w(const float* __restrict__ cb, int K, int Df,
+                                                        float* __restrict__ G)
+{
+    const int i = blockIdx.x, l = blockIdx.y, lane = threadIdx.x;
+    const float* ci = cb + ((size_t)l * K + i) * Df;
+    for (int j = 0; j < K; j++) {
+        const float* cj = cb + ((size_t)l * K + j) * Df;
+        float v = 0.f;
+        for (int d = lane; d < Df; d += 64) v = fmaf(ci[d], cj[d], v);
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+        if (lane == 0) G[((size_t)l * K + i) * K + j] = v;
+    }
+}
+
+// Lower-triangular L with L L^T = G (per level, K <= 64, f64 in LDS).  A pivot
+// at or below 1e-12 of the largest diagonal entry (rank-deficient codebook)
+// leaves its column zero.  Output row-major (K x K) f32, zeros above the diagonal.
+__global__ void __launch_bounds__(64) k_codebook_chol(const float* __restrict__ G, int K, float* __restrict__ Lout)
+{
+    __shared__ double A[64][65];
+    const int l = blockIdx.x, t = threadIdx.x;
+    const float* g = G + (size_t)l * K * K;
+    for (int e = t; e < K * K; e += 64) A[e / K][e % K] = (double)g[e];
+    __syncthreads();
+    double mx = 0.0;
+    for (int j = 0; j < K; j++) mx = fmax(mx, A[j][j]);
+    const double tol = 1e-12 * mx;
+    for (int j = 0; j < K; j++) {
+        const double d = A[j][j];
+        const double piv = d > tol ? sqrt(d) : 0.0;
+        __syncthreads();
+        if (t == j) A[j][j] = piv;
+        if (t > j && t < K) A[t][j] = piv > 0.0 ? A[t][j] / piv : 0.0;
+        __syncthreads();
+        if (t > j && t < K)
+            for (int k = j + 1; k <= t; k++) A[t][k] -= A[t][j] * A[k][j];
+    }
+    __syncthreads();
+    float* o = Lout + (size_t)l * K * K;
+    for (int e = t; e < K * K; e += 64) {
+        const int r = e / K, c = e % K;
+        o[e] = c <= r ? (float)A[r][c] : 0.f;
+    }
+}
+
+#ifndef LSR_DEC2_WAVES
+#define LSR_DEC2_WAVES 8     // waves per level-resident workgroup (one workgroup per CU: LDS)
+#endif
+#ifndef LSR_DEC2_PF
+#define LSR_DEC2_PF 1        // next tile's weights loaded one tile ahead (64 VGPRs)
+#endif
+#ifndef LSR_DEC2_NT
+#define LSR_DEC2_NT 0        // non-temporal output stores
+#endif
+#define LSR_DEC2_MAXDB 32    // Df <= 512: fragments + norm factor fit in 144 KB of LDS
+
+template <bool NORM, bool VEC>
+__global__ void __launch_bounds__(64 * LSR_DEC2_WAVES, 1)
+    k_quick_decode_l(const float* __restrict__ wmap, int Df, int W, int H, const uint4* __restrict__ frag,
+                     const float* __restrict__ scales, const uint4* __restrict__ nfrag,
+                     const float* __restrict__ nscales, float* __restrict__ out, float eps, int nwg)
+{
+    extern __shared__ uint4 sfr[];   // [db][s][lane][hi, lo] codebook, then 4 blocks of the norm factor
+    const int l = (int)blockIdx.x / nwg, wi = (int)blockIdx.x % nwg;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, lg = lane >> 4, li = lane & 15;
+    const int NDB = Df / 16;
+    {
+        const uint4* src = frag + (size_t)l * NDB * 256;
+        for (int i = threadIdx.x; i < NDB * 256; i += 64 * LSR_DEC2_WAVES) sfr[i] = src[i];
+        if constexpr (NORM) {
+            const uint4* ns = nfrag + (size_t)l * 4 * 256;
+            for (int i = threadIdx.x; i < 4 * 256; i += 64 * LSR_DEC2_WAVES) sfr[NDB * 256 + i] = ns[i];
+        }
+    }
+    __syncthreads();
+    const float sc = scales[l];
+    const float ns2 = NORM ? nscales[l] * nscales[l] : 0.f;
+    const size_t HW = (size_t)W * H;
+    const int nbx = (W + 63) / 64;
+    const int ntile = nbx * H;
+    const int stride = nwg * LSR_DEC2_WAVES;
+    // raw weights of a 64-pixel tile: lane (li, lg) holds W[64 l + 32 s + 8 lg + j][x = bx + 16 pb + li]
+    float raw[4][2][8];
+    auto load = [&](int tt) {
+        const bool ok = tt < ntile;
+        const int tq = ok ? tt : 0;
+        const int bx = (tq % nbx) * 64, y = tq / nbx;
+#pragma unroll
+        for (int pb = 0; pb < 4; pb++) {
+            const int xa = bx + 16 * pb + li;
+            const size_t pa = (size_t)y * W + min(xa, W - 1);
+            const bool in = ok && xa < W;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; s2++)
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const float v = wmap[(size_t)(l * 64 + 32 * s2 + 8 * lg + j) * HW + pa];
+                    raw[pb][s2][j] = in ? v : 0.f;
+                }
+        }
+    };
+    int t = wi * LSR_DEC2_WAVES + w;
+#if LSR_DEC2_PF
+    load(t);
+#endif
+    for (; t < ntile; t += stride) {
+#if !LSR_DEC2_PF
+        load(t);
+#endif
+        const int bx = (t % nbx) * 64, y = t / nbx;
+        h8 Wh[4][2], Wl[4][2];
+#pragma unroll
+        for (int pb = 0; pb < 4; pb++)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; s2++)
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const float v = raw[pb][s2][j];
+                    const _Float16 h = (_Float16)v;
+                    Wh[pb][s2][j] = h;
+                    Wl[pb][s2][j] = (_Float16)(v - (float)h);
+                }
+#if LSR_DEC2_PF
+        load(t + stride);   // next tile's weights in flight during this tile's products and stores
+#endif
+        float mul[4][4];
+#pragma unroll
+        for (int pb = 0; pb < 4; pb++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) mul[pb][r] = sc;
+        if constexpr (NORM) {
+            // Y^T = W^T L: lane (k = 16 mb + li, lg) gets Y[k] of pixels 4 lg + r; |F_p|^2 = sum_k Y[k]^2
+            float sq[4][4];
+#pragma unroll
+            for (int pb = 0; pb < 4; pb++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) sq[pb][r] = 0.f;
+#pragma unroll 1
+            for (int mb = 0; mb < 4; mb++) {
+                const uint4* f = sfr + (size_t)(NDB + mb) * 256 + lane * 2;
+                const h8 c0h = __builtin_bit_cast(h8, f[0]), c0l = __builtin_bit_cast(h8, f[1]);
+                const h8 c1h = __builtin_bit_cast(h8, f[128]), c1l = __builtin_bit_cast(h8, f[129]);
+#pragma unroll
+                for (int pb = 0; pb < 4; pb++) {
+                    f32x4q acc = {0.f, 0.f, 0.f, 0.f};
+                    LSR_DEC_MFMA6(acc, pb);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) sq[pb][r] = fmaf(acc[r], acc[r], sq[pb][r]);
+                }
+            }
+#pragma unroll
+            for (int pb = 0; pb < 4; pb++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) mul[pb][r] = sc / (sqrtf(fmaxf(row16_sum(sq[pb][r]) * ns2, 0.f)) + eps);
+        }
+        float* const orow = out + (size_t)(l * Df + li) * HW + (size_t)y * W;
+#pragma unroll 1
+        for (int db = 0; db < NDB; db++) {
+            const uint4* f = sfr + (size_t)db * 256 + lane * 2;
+            const h8 c0h = __builtin_bit_cast(h8, f[0]), c0l = __builtin_bit_cast(h8, f[1]);
+            const h8 c1h = __builtin_bit_cast(h8, f[128]), c1l = __builtin_bit_cast(h8, f[129]);
+            float* const od = orow + (size_t)db * 16 * HW;
+#pragma unroll
+            for (int pb = 0; pb < 4; pb++) {
+                f32x4q acc = {0.f, 0.f, 0.f, 0.f};
+                LSR_DEC_MFMA6(acc, pb);
+                const int xo = bx + 16 * pb + 4 * lg;
+                float* o = od + xo;
+                if (VEC && xo + 3 < W) {
+#if LSR_DEC2_NT
+                    f32x4q v = {acc[0] * mul[pb][0], acc[1] * mul[pb][1], acc[2] * mul[pb][2], acc[3] * mul[pb][3]};
+                    __builtin_nontemporal_store(v, reinterpret_cast<f32x4q*>(o));
+#else
+                    *reinterpret_cast<float4*>(o) = make_float4(acc[0] * mul[pb][0], acc[1] * mul[pb][1],
+                                                                acc[2] * mul[pb][2], acc[3] * mul[pb][3]);
+#endif
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; r++)
+                        if (xo + r < W) o[r] = acc[r] * mul[pb][r];
+                }
+            }
+        }
+    }
+}
+
 size_t quick_decode_workspace_bytes(int L, int K, int Df, int normalize)
 {
 #ifdef LSR_DECODE_F32
     return normalize ? sizeof(float) * (size_t)L * K * K : 0;
 #else
     // codebook fragments (L * Df/16 * 2 * 64 * 32 B) + per-level scales; with normalisation the
-    // Gram matrices (L * 64 * 64 f32), their fragments (L * 4 * 2 * 64 * 32 B) and scales
-    return (size_t)L * Df * 256 + 256 + (normalize ? (size_t)L * K * K * 4 + (size_t)L * 64 * 256 + 256 : 0);
+    // Gram matrices and their Cholesky factors (2 * L * 64 * 64 f32), the factor's (or, for
+    // Df > 512, the Gram matrices') fragments (L * 4 * 2 * 64 * 32 B) and scales
+    return (size_t)L * Df * 256 + 256 + (normalize ? 2 * (size_t)L * K * K * 4 + (size_t)L * 64 * 256 + 256 : 0);
 #endif
 }
 
@@ -375,23 +581,52 @@ hipError_t launch_quick_decode(const float* wmap, const float* cb, int L, int K,
     }
     k_quick_decode<64><<<nb, 64, 0, st>>>(wmap, L, Df, W, H, cb, G, out, eps, normalize);
 #else
-    const unsigned nb = (unsigned)(((W + 63) / 64) * H);
     uint8_t* p = (uint8_t*)ws;
     uint4* frag = (uint4*)p;
     float* scales = (float*)(p + (size_t)L * Df * 256);
     k_codebook_frag<<<L, 256, 0, st>>>(cb, K, Df, frag, scales);
     const bool vec = (W % 4) == 0;
+    float* G = (float*)(p + (size_t)L * Df * 256 + 256);
+    float* Lf = G + (size_t)L * K * K;
+    uint4* nfrag = (uint4*)(Lf + (size_t)L * K * K);
+    float* nscales = (float*)((uint8_t*)nfrag + (size_t)L * 64 * 256);
+    const int NDB = Df / 16;
+#ifndef LSR_DECODE_H
+    if (NDB <= LSR_DEC2_MAXDB) {
+        // level-resident: one workgroup per CU, the CUs split evenly over the levels
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        const int nwg = ncu / L > 0 ? ncu / L : 1;
+        const size_t lds = (size_t)(NDB + (normalize ? 4 : 0)) * 256 * sizeof(uint4);
+        if (normalize) {
+            k_codebook_gram_w<<<dim3((unsigned)K, (unsigned)L), 64, 0, st>>>(cb, K, Df, G);
+            k_codebook_chol<<<L, 64, 0, st>>>(G, K, Lf);
+            k_codebook_frag<<<L, 256, 0, st>>>(Lf, K, K, nfrag, nscales);
+        }
+        auto run = [&](auto kern) {
+            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            kern<<<(unsigned)(nwg * L), 64 * LSR_DEC2_WAVES, lds, st>>>(wmap, Df, W, H, frag, scales, nfrag, nscales,
+                                                                      out, eps, nwg);
+        };
+        if (normalize) {
+            if (vec) run(k_quick_decode_l<true, true>);
+            else run(k_quick_decode_l<true, false>);
+        } else {
+            if (vec) run(k_quick_decode_l<false, true>);
+            else run(k_quick_decode_l<false, false>);
+        }
+        return hipGetLastError();
+    }
+#endif
+    const unsigned nb = (unsigned)(((W + 63) / 64) * H);
     if (normalize) {
-        float* G = (float*)(p + (size_t)L * Df * 256 + 256);
-        uint4* gfrag = (uint4*)((uint8_t*)G + (size_t)L * K * K * 4);
-        float* gscales = (float*)((uint8_t*)gfrag + (size_t)L * 64 * 256);
         dim3 g((unsigned)((K * K + 255) / 256), (unsigned)L);
         k_codebook_gram<<<g, 256, 0, st>>>(cb, K, Df, G);
-        k_codebook_frag<<<L, 256, 0, st>>>(G, K, K, gfrag, gscales);
+        k_codebook_frag<<<L, 256, 0, st>>>(G, K, K, nfrag, nscales);
         if (vec)
-            k_quick_decode_h<true, true><<<nb, 64, 0, st>>>(wmap, L, Df, W, H, frag, scales, gfrag, gscales, out, eps);
+            k_quick_decode_h<true, true><<<nb, 64, 0, st>>>(wmap, L, Df, W, H, frag, scales, nfrag, nscales, out, eps);
         else
-            k_quick_decode_h<true, false><<<nb, 64, 0, st>>>(wmap, L, Df, W, H, frag, scales, gfrag, gscales, out, eps);
+            k_quick_decode_h<true, false><<<nb, 64, 0, st>>>(wmap, L, Df, W, H, frag, scales, nfrag, nscales, out, eps);
     } else {
         if (vec)
             k_quick_decode_h<false, true><<<nb, 64, 0, st>>>(wmap, L, Df, W, H, frag, scales, nullptr, nullptr, out, eps);
