@@ -55,6 +55,9 @@
 #ifndef LSR_QUICK_QB
 #define LSR_QUICK_QB 4      // quick path: 64-channel slabs
 #endif
+#ifndef LSR_QUICK_V
+#define LSR_QUICK_V 1       // quick path: per-pixel accumulators in VGPRs, sparse (weight, code) updates
+#endif
 #ifndef LSR_FWD_MF_WIDE
 #define LSR_FWD_MF_WIDE 1   // D = 64: MFMA-accumulated forward
 #endif
@@ -647,6 +650,226 @@ __global__ void __launch_bounds__(64) k_render_fwd_quick(RenderArgs a)
     }
 }
 
+// Quick path, sparse accumulation in registers (default for Dq <= 192, K <= 12).
+// The dense-slab kernels above scatter each group's (weight, code) pairs into a
+// 16 x Dq tile and accumulate it on MFMA: 16x the arithmetic the 12 non-zero
+// codes need, plus barriers between the blend wave and the slab waves.  Here
+// one wave per 8x8 block keeps each pixel's Dq accumulators in VGPRs (NP
+// vectors of 32) and, per contributing candidate, adds only its K pairs:
+// the code is wave-uniform, so acc[code] is a register indexed by M0 (movrel)
+// and each pair costs one FMA plus two register moves.  Same per-pixel
+// recurrence, same fmaf(w, alpha T, acc) in candidate order as the oracle:
+// bit-exact.  Staged per candidate in LDS: the splat record, rgb, the K
+// weights and the codes as bytes (0xFF = outside [0, Dq)).
+typedef float lsr_f32x32 __attribute__((ext_vector_type(32)));
+struct WaveStageV {
+    float4 A[64];
+    float4 B[64];          // .w = 1-based tile-list position (int bits)
+    float4 C[64];          // rgb
+    float4 Wt[64][3];      // weights 0..11
+    uint4 Q[64];           // codes 0..11 as bytes
+};
+
+// The Dq <= 192 accumulators live in v64..v255, outside the compiler's
+// allocation (amdgpu_num_vgpr(63): compiled code uses v0..v62; an asm clobber
+// of v255 makes the kernel descriptor allocate all 256).  A candidate's K <= 12
+// updates run in one asm block in VGPR index mode with SRC2 and DST indexed
+// from v63: code q is stored as index q + 1, so v_fma_f32 v63, w, aT, v63
+// updates v[64 + q] in one VALU instruction, and an invalid code (index 0)
+// lands in the junk register v63.  M0 (the index) is saved and restored.
+// (s_set_gpr_idx_idx reads only bits [7:0], so byte k of a code word is
+// selected by a shift.)
+#define LSR_QV_STEP0(word, wv)                                                          \
+    "s_set_gpr_idx_idx %[" #word "]\n\t"                                                \
+    "s_nop 0\n\t"                                                                       \
+    "v_fma_f32 v63, %[" #wv "], %[aT], v63\n\t"
+#define LSR_QV_STEP(word, sh, wv)                                                       \
+    "s_lshr_b32 %[ix], %[" #word "], " #sh "\n\t"                                         \
+    "s_set_gpr_idx_idx %[ix]\n\t"                                                       \
+    "s_nop 0\n\t"                                                                       \
+    "v_fma_f32 v63, %[" #wv "], %[aT], v63\n\t"
+// one candidate's K <= 12 pairs (codes in three words q0..q2, weights w0..w11)
+#define LSR_QV_UPDATE(aT_, Q_, W0_, W1_, W2_)                                                                   \
+    do {                                                                                                        \
+        const uint32_t qw0 = __builtin_amdgcn_readfirstlane((Q_).x), qw1 = __builtin_amdgcn_readfirstlane((Q_).y), \
+                       qw2 = __builtin_amdgcn_readfirstlane((Q_).z);                                            \
+        uint32_t ix, sv;                                                                                        \
+        asm volatile("s_mov_b32 %[sv], m0\n\t"                                                                  \
+                     "s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)\n\t"                                                \
+                     LSR_QV_STEP0(q0, w0) LSR_QV_STEP(q0, 8, w1) LSR_QV_STEP(q0, 16, w2) LSR_QV_STEP(q0, 24, w3)  \
+                     LSR_QV_STEP0(q1, w4) LSR_QV_STEP(q1, 8, w5) LSR_QV_STEP(q1, 16, w6) LSR_QV_STEP(q1, 24, w7)  \
+                     LSR_QV_STEP0(q2, w8) LSR_QV_STEP(q2, 8, w9) LSR_QV_STEP(q2, 16, w10) LSR_QV_STEP(q2, 24, w11) \
+                     "s_set_gpr_idx_off\n\t"                                                                    \
+                     "s_mov_b32 m0, %[sv]"                                                                      \
+                     : [ix] "=&s"(ix), [sv] "=&s"(sv)                                                           \
+                     : [q0] "s"(qw0), [q1] "s"(qw1), [q2] "s"(qw2), [aT] "v"(aT_), [w0] "v"((W0_).x),           \
+                       [w1] "v"((W0_).y), [w2] "v"((W0_).z), [w3] "v"((W0_).w), [w4] "v"((W1_).x),              \
+                       [w5] "v"((W1_).y), [w6] "v"((W1_).z), [w7] "v"((W1_).w), [w8] "v"((W2_).x),              \
+                       [w9] "v"((W2_).y), [w10] "v"((W2_).z), [w11] "v"((W2_).w)                                \
+                     : "scc");                                                                                  \
+    } while (0)
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"   // the v255 clobber is the point: it sizes the allocation
+template <int NP>
+__global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_render_fwd_quick_v(RenderArgs a)
+{
+    static_assert(NP >= 1 && NP <= 6, "up to 192 quick channels");
+    __shared__ WaveStageV st;
+    const Cam& c = a.cam;
+    const WaveTile wt;
+    const int lane = threadIdx.x;
+    const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
+    const bool inside = pm.px < c.W && pm.py < c.H;
+    const float pfx = (float)pm.px, pfy = (float)pm.py;
+    const uint32_t rs = a.tile_start[wt.tile], re = a.tile_start[wt.tile + 1];
+    const int K = a.K, Dq = a.Dq;
+
+    {   // zero v63 (junk) .. v255 (accumulators)
+        uint32_t i, sv;
+        asm volatile(
+            "s_mov_b32 %[sv], m0\n\t"
+            "s_mov_b32 %[i], 0\n\t"
+            "s_set_gpr_idx_on 0, gpr_idx(DST)\n\t"
+            "1:\n\t"
+            "s_set_gpr_idx_idx %[i]\n\t"
+            "s_nop 0\n\t"
+            "v_mov_b32 v63, 0\n\t"
+            "s_add_u32 %[i], %[i], 1\n\t"
+            "s_cmp_lt_u32 %[i], 193\n\t"
+            "s_cbranch_scc1 1b\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "s_mov_b32 m0, %[sv]"
+            : [i] "=&s"(i), [sv] "=&s"(sv)
+            :
+            : "scc", "v63", "v255", "memory");
+    }
+    float T = 1.0f, cr = 0.f, cg = 0.f, cbl = 0.f;
+    uint32_t last = 0;
+    bool done = !inside;
+    uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
+    for (uint32_t base = rs; base < re; base += 64) {
+        if (wave_ballot(!done) == 0) break;
+        const uint32_t idx = base + lane;
+        const bool valid = idx < re;
+        const uint32_t gid = next_gid;
+        next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;
+        float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+        if (valid) {
+            A = a.splatA[gid];
+            B = a.splatB[gid];
+        }
+        const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), pm.bx, pm.by) &&
+                        block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, pm.bx, pm.by);
+        const uint64_t m = wave_ballot(ok);
+        if (ok) {
+            const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            st.A[r] = A;
+            st.B[r] = make_float4(B.x, B.y, B.z, __int_as_float((int)(idx - rs) + 1));
+            st.C[r] = make_float4(a.rgb[3 * (size_t)gid], a.rgb[3 * (size_t)gid + 1], a.rgb[3 * (size_t)gid + 2], 0.f);
+            float wv[12];
+            uint32_t qv[3] = {0u, 0u, 0u};   // register index q + 1 per code; 0 = the junk register
+#pragma unroll
+            for (int k = 0; k < 12; k++) {
+                wv[k] = 0.f;
+                if (k < K) {
+                    const size_t off = (size_t)gid * K + k;
+                    wv[k] = a.qw[off];
+                    const int q = quick_index(a.qi, a.qidx_dtype, off);
+                    const uint32_t qb = (q >= 0 && q < Dq) ? (uint32_t)(q + 1) : 0u;
+                    qv[k >> 2] |= qb << (8 * (k & 3));
+                }
+            }
+            st.Wt[r][0] = make_float4(wv[0], wv[1], wv[2], wv[3]);
+            st.Wt[r][1] = make_float4(wv[4], wv[5], wv[6], wv[7]);
+            st.Wt[r][2] = make_float4(wv[8], wv[9], wv[10], wv[11]);
+            st.Q[r] = make_uint4(qv[0], qv[1], qv[2], 0u);
+        }
+        wave_lds_fence();
+        const int n = __popcll(m);
+        // two candidates per step: their exponents on packed f32 (expf_det2,
+        // bitwise = expf_det), then the per-pixel recurrence in order
+        for (int j0 = 0; j0 < n; j0 += 2) {
+            if (wave_ballot(!done) == 0) break;
+            const bool two = j0 + 1 < n;
+            const int j1 = two ? j0 + 1 : j0;
+            const float4 A0 = st.A[j0], B0 = st.B[j0];
+            const float4 A1 = st.A[j1], B1 = st.B[j1];
+            const float p0 = splat_power(A0.z, A0.w, B0.x, A0.x - pfx, A0.y - pfy);
+            const float p1 = splat_power(A1.z, A1.w, B1.x, A1.x - pfx, A1.y - pfy);
+            bool ok0 = !done && !(p0 > 0.0f || p0 < B0.z);
+            bool ok1 = two && !done && !(p1 > 0.0f || p1 < B1.z);
+            if (!wave_any(ok0 || ok1)) continue;
+            const f32x2 EX = expf_det2(f32x2{p0, p1});
+            const float al0 = fminf(0.99f, B0.y * EX.x);
+            const float al1 = fminf(0.99f, B1.y * EX.y);
+            ok0 = ok0 && !(al0 < 1.0f / 255.0f);
+            ok1 = ok1 && !(al1 < 1.0f / 255.0f);
+            float aT0, aT1;
+            {
+                const float test_T = T * (1.0f - al0);
+                const bool term = ok0 && (test_T < 0.0001f);
+                done = done || term;
+                ok0 = ok0 && !term;
+                ok1 = ok1 && !term;
+                aT0 = ok0 ? al0 * T : 0.f;
+                if (ok0) {
+                    const float4 C0 = st.C[j0];
+                    cr = fmaf(C0.x, aT0, cr);
+                    cg = fmaf(C0.y, aT0, cg);
+                    cbl = fmaf(C0.z, aT0, cbl);
+                    T = test_T;
+                    last = (uint32_t)__float_as_int(B0.w);
+                }
+            }
+            {
+                const float test_T = T * (1.0f - al1);
+                const bool term = ok1 && (test_T < 0.0001f);
+                done = done || term;
+                ok1 = ok1 && !term;
+                aT1 = ok1 ? al1 * T : 0.f;
+                if (ok1) {
+                    const float4 C1 = st.C[j1];
+                    cr = fmaf(C1.x, aT1, cr);
+                    cg = fmaf(C1.y, aT1, cg);
+                    cbl = fmaf(C1.z, aT1, cbl);
+                    T = test_T;
+                    last = (uint32_t)__float_as_int(B1.w);
+                }
+            }
+            if (wave_any(ok0)) LSR_QV_UPDATE(aT0, st.Q[j0], st.Wt[j0][0], st.Wt[j0][1], st.Wt[j0][2]);
+            if (wave_any(ok1)) LSR_QV_UPDATE(aT1, st.Q[j1], st.Wt[j1][0], st.Wt[j1][1], st.Wt[j1][2]);
+        }
+        wave_lds_fence();
+    }
+    const size_t HW = (size_t)c.H * c.W;
+    if (inside) {
+        const size_t pix = (size_t)pm.py * c.W + pm.px;
+        a.final_T[pix] = T;
+        a.n_contrib[pix] = last;
+        a.out_color[pix] = fmaf(T, c.bg[0], cr);
+        a.out_color[HW + pix] = fmaf(T, c.bg[1], cg);
+        a.out_color[2 * HW + pix] = fmaf(T, c.bg[2], cbl);
+        float* const o = a.out_lang + pix;
+        for (int q = 0; q < Dq; q++) {
+            float v;
+            uint32_t sv;
+            asm volatile(
+                "s_mov_b32 %[sv], m0\n\t"
+                "s_set_gpr_idx_on %[q], gpr_idx(SRC0)\n\t"
+                "s_nop 0\n\t"
+                "v_mov_b32 %[v], v64\n\t"
+                "s_set_gpr_idx_off\n\t"
+                "s_mov_b32 m0, %[sv]"
+                : [v] "=v"(v), [sv] "=&s"(sv)
+                : [q] "s"(q)
+                : "memory");
+            o[(size_t)q * HW] = v;
+        }
+    }
+}
+#pragma clang diagnostic pop
+
 int lang_set_for(int D)
 {
     if (D <= 0) return 0;
@@ -672,6 +895,19 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
     const int T = a.cam.gx * a.cam.gy;
     if (T == 0) return hipSuccess;
     if (a.qw) {
+#if LSR_QUICK_V
+        if (a.K <= 12 && a.Dq <= 192) {
+            switch ((a.Dq + 31) / 32) {
+                case 1: k_render_fwd_quick_v<1><<<T * 4, 64, 0, st>>>(a); break;
+                case 2: k_render_fwd_quick_v<2><<<T * 4, 64, 0, st>>>(a); break;
+                case 3: k_render_fwd_quick_v<3><<<T * 4, 64, 0, st>>>(a); break;
+                case 4: k_render_fwd_quick_v<4><<<T * 4, 64, 0, st>>>(a); break;
+                case 5: k_render_fwd_quick_v<5><<<T * 4, 64, 0, st>>>(a); break;
+                default: k_render_fwd_quick_v<6><<<T * 4, 64, 0, st>>>(a); break;
+            }
+            return hipGetLastError();
+        }
+#endif
 #if LSR_QUICK_MF
         if (a.K <= LSR_QUICK_KMAX) {
             // one workgroup of Dq/64 waves per 8x8 block (64-channel slabs)
