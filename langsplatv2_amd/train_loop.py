@@ -1,0 +1,225 @@
+"""RGB-phase training iteration of the reference, over the view-sharded
+exchange (BASELINE.json cfg4's loop shape).
+
+What it restates (reference file:line):
+  * Gaussian parameters and activations: scene/gaussian_model.py:28-32
+    (exp scaling, sigmoid opacity, normalised rotation), :153-157 (features =
+    cat(f_dc, f_rest)), :180-182 (oneupSHdegree), the Adam groups and learning
+    rates of training_setup :234-255 (eps 1e-15);
+  * render(): gaussian_renderer/__init__.py:19-129, RGB mode: the screen-space
+    points are `zeros_like(xyz, requires_grad=True) + 0` with retain_grad,
+    the (1,) placeholder for the language input, SH evaluated by the rasterizer;
+  * the loss (1 - lambda_dssim) L1 + lambda_dssim (1 - SSIM): train.py:166-168,
+    utils/loss_utils.py:18-75;
+  * per-view bookkeeping: max_radii2D over the visibility filter and
+    add_densification_stats (train.py:245-251, scene/gaussian_model.py:506-508);
+  * the SH-degree ramp every 1000 iterations (train.py:135-136) and the
+    optimizer step every `accum_iter` iterations (train.py:261-263).
+
+Data parallelism: each of R ranks renders one view per step, the exchange
+(dp.ViewShardedExchange) all-reduces the gradients and the densification
+increments and MAX-reduces the radii, then every rank steps its replica — the
+same update as `--accum_iter R` on one GPU with the R views in one
+accumulation window (only the gradient summation order differs).  One step
+advances the iteration counter by R; the SH ramp is applied at step
+granularity (all views of a window use the degree active at its first
+iteration, so the replicas stay identical).  densify_and_prune itself (clone /
+split / prune, scene/gaussian_model.py:422-505) is outside the rasterizer path
+and not restated; its inputs (max_radii2D, xyz_gradient_accum, denom) are.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import dp
+from .optim import FusedAdam
+from .rasterizer import GaussianRasterizationSettings, GaussianRasterizer
+
+PARAM_NAMES = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")
+
+
+def inverse_sigmoid(x: torch.Tensor) -> torch.Tensor:
+    return torch.log(x / (1 - x))
+
+
+class GaussianState:
+    """The reference GaussianModel's tensors for the RGB phase (no language)."""
+
+    def __init__(self, means3D, shs, opacities, scales, rotations, max_sh_degree: int = 3):
+        dev = means3D.device
+        self._xyz = means3D.detach().clone().contiguous().requires_grad_(True)
+        self._features_dc = shs[:, :1].detach().clone().contiguous().requires_grad_(True)
+        self._features_rest = shs[:, 1:].detach().clone().contiguous().requires_grad_(True)
+        self._opacity = inverse_sigmoid(opacities.detach().clamp(1e-6, 1 - 1e-6)).contiguous().requires_grad_(True)
+        self._scaling = torch.log(scales.detach()).contiguous().requires_grad_(True)
+        self._rotation = rotations.detach().clone().contiguous().requires_grad_(True)
+        self.max_sh_degree = max_sh_degree
+        self.active_sh_degree = 0
+        n = means3D.shape[0]
+        self.max_radii2D = torch.zeros(n, device=dev)
+        self.xyz_gradient_accum = torch.zeros(n, 1, device=dev)
+        self.denom = torch.zeros(n, 1, device=dev)
+
+    def params(self) -> list[torch.Tensor]:
+        return [self._xyz, self._features_dc, self._features_rest, self._opacity, self._scaling, self._rotation]
+
+    @property
+    def get_xyz(self):
+        return self._xyz
+
+    @property
+    def get_features(self):
+        return torch.cat((self._features_dc, self._features_rest), dim=1)
+
+    @property
+    def get_opacity(self):
+        return torch.sigmoid(self._opacity)
+
+    @property
+    def get_scaling(self):
+        return torch.exp(self._scaling)
+
+    @property
+    def get_rotation(self):
+        return F.normalize(self._rotation)
+
+    def oneup_sh_degree(self):
+        if self.active_sh_degree < self.max_sh_degree:
+            self.active_sh_degree += 1
+
+    def optimizer(self, spatial_lr_scale: float = 1.0, fused: bool = True):
+        """training_setup's groups (scene/gaussian_model.py:234-255, OptimizationParams defaults)."""
+        groups = [
+            {"params": [self._xyz], "lr": 0.00016 * spatial_lr_scale, "name": "xyz"},
+            {"params": [self._features_dc], "lr": 0.0025, "name": "f_dc"},
+            {"params": [self._features_rest], "lr": 0.0025 / 20.0, "name": "f_rest"},
+            {"params": [self._opacity], "lr": 0.05, "name": "opacity"},
+            {"params": [self._scaling], "lr": 0.005, "name": "scaling"},
+            {"params": [self._rotation], "lr": 0.001, "name": "rotation"},
+        ]
+        return FusedAdam(groups, lr=0.0, eps=1e-15) if fused else torch.optim.Adam(groups, lr=0.0, eps=1e-15)
+
+
+def render_rgb(cam: dict, gs: GaussianState, bg: torch.Tensor, scaling_modifier: float = 1.0) -> dict:
+    """gaussian_renderer/__init__.py:19-129 for include_feature = False."""
+    screenspace_points = torch.zeros_like(gs.get_xyz, dtype=gs.get_xyz.dtype, requires_grad=True) + 0
+    screenspace_points.retain_grad()
+    dev = gs.get_xyz.device
+    rs = GaussianRasterizationSettings(
+        image_height=int(cam["H"]), image_width=int(cam["W"]), tanfovx=cam["tanfovx"], tanfovy=cam["tanfovy"],
+        bg=bg, scale_modifier=scaling_modifier, viewmatrix=cam["viewmatrix"].to(dev),
+        projmatrix=cam["projmatrix"].to(dev), sh_degree=gs.active_sh_degree, campos=cam["campos"].to(dev),
+        prefiltered=False, debug=False, include_feature=False)
+    rasterizer = GaussianRasterizer(raster_settings=rs)
+    placeholder = torch.zeros((1,), dtype=gs.get_opacity.dtype, device=dev)
+    image, _lang, radii = rasterizer(means3D=gs.get_xyz, means2D=screenspace_points, shs=gs.get_features,
+                                     colors_precomp=None, language_feature_precomp=placeholder,
+                                     opacities=gs.get_opacity, scales=gs.get_scaling, rotations=gs.get_rotation,
+                                     cov3D_precomp=None)
+    return {"render": image, "viewspace_points": screenspace_points, "visibility_filter": radii > 0, "radii": radii}
+
+
+def l1_loss(out: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
+    return torch.abs(out - gt).mean()
+
+
+def _gauss_window(window_size: int, sigma: float, channel: int, like: torch.Tensor) -> torch.Tensor:
+    g = torch.tensor([math.exp(-(x - window_size // 2) ** 2 / float(2 * sigma ** 2)) for x in range(window_size)])
+    g = g / g.sum()
+    w2 = (g[:, None] @ g[None, :]).float()
+    return w2.expand(channel, 1, window_size, window_size).contiguous().to(like.device, like.dtype)
+
+
+def ssim(img1: torch.Tensor, img2: torch.Tensor, window_size: int = 11) -> torch.Tensor:
+    """utils/loss_utils.py:38-75 (11x11 Gaussian window, sigma 1.5, mean SSIM)."""
+    c = img1.size(-3)
+    w = _gauss_window(window_size, 1.5, c, img1)
+    pad = window_size // 2
+    mu1 = F.conv2d(img1, w, padding=pad, groups=c)
+    mu2 = F.conv2d(img2, w, padding=pad, groups=c)
+    mu1_sq, mu2_sq, mu12 = mu1.pow(2), mu2.pow(2), mu1 * mu2
+    s1 = F.conv2d(img1 * img1, w, padding=pad, groups=c) - mu1_sq
+    s2 = F.conv2d(img2 * img2, w, padding=pad, groups=c) - mu2_sq
+    s12 = F.conv2d(img1 * img2, w, padding=pad, groups=c) - mu12
+    C1, C2 = 0.01 ** 2, 0.03 ** 2
+    return (((2 * mu12 + C1) * (2 * s12 + C2)) / ((mu1_sq + mu2_sq + C1) * (s1 + s2 + C2))).mean()
+
+
+def view_loss(image: torch.Tensor, gt: torch.Tensor, lambda_dssim: float) -> torch.Tensor:
+    return (1.0 - lambda_dssim) * l1_loss(image, gt) + lambda_dssim * (1.0 - ssim(image, gt))
+
+
+def sh_ramp(gs: GaussianState, iteration: int, window: int, interval: int = 1000):
+    """train.py:135-136 (oneupSHdegree when iteration % 1000 == 0) for the window
+    of iterations iteration+1 .. iteration+window, applied before its first view."""
+    for it in range(iteration + 1, iteration + window + 1):
+        if it % interval == 0:
+            gs.oneup_sh_degree()
+
+
+@torch.no_grad()
+def apply_view_stats(gs: GaussianState, radii: torch.Tensor, stats: torch.Tensor):
+    """max_radii2D over the visibility filter and add_densification_stats with the
+    (reduced) per-view increments [||dL/d means2D[:, :2]||, visible]."""
+    vis = radii > 0
+    gs.max_radii2D[vis] = torch.max(gs.max_radii2D[vis], radii[vis].to(gs.max_radii2D.dtype))
+    gs.xyz_gradient_accum += stats[:, :1]
+    gs.denom += stats[:, 1:2]
+
+
+class RGBTrainer:
+    """One optimizer step per call: this rank renders `view`, the exchange sums
+    the R ranks' gradients and statistics, every rank steps its replica."""
+
+    def __init__(self, gs: GaussianState, bg: torch.Tensor, lambda_dssim: float = 0.2, group=None, fused_adam=True,
+                 sh_interval: int = 1000):
+        self.gs = gs
+        self.sh_interval = sh_interval
+        self.bg = bg
+        self.lambda_dssim = lambda_dssim
+        self.opt = gs.optimizer(fused=fused_adam)
+        self.exchange = dp.ViewShardedExchange(gs.params(), with_stats=True, group=group, names=list(PARAM_NAMES))
+        self.world = self.exchange.world
+        self.iteration = 0
+
+    def step(self, cam: dict, gt: torch.Tensor) -> float:
+        sh_ramp(self.gs, self.iteration, self.world, self.sh_interval)
+        pkg = render_rgb(cam, self.gs, self.bg)
+        loss = view_loss(pkg["render"], gt, self.lambda_dssim)
+        loss.backward()
+        params = self.gs.params()
+        grads, stats, max_radii = self.exchange.exchange([p.grad for p in params],
+                                                         pkg["viewspace_points"].grad, pkg["radii"])
+        apply_view_stats(self.gs, max_radii, stats)
+        for p, g in zip(params, grads):
+            p.grad = g
+        self.opt.step()
+        self.opt.zero_grad(set_to_none=True)
+        self.iteration += self.world
+        return float(loss.detach())
+
+
+def accumulate_views(gs: GaussianState, opt, cams: list, gts: list, bg: torch.Tensor, lambda_dssim: float = 0.2,
+                     iteration: int = 0, sh_interval: int = 1000):
+    """The single-GPU reference of one DP step: `len(cams)` iterations with
+    accum_iter = len(cams) (train.py:245-263): per view, backward into .grad
+    (autograd accumulates), max_radii2D / densification stats; one optimizer
+    step at the end of the window."""
+    sh_ramp(gs, iteration, len(cams), sh_interval)
+    losses = []
+    for cam, gt in zip(cams, gts):
+        pkg = render_rgb(cam, gs, bg)
+        loss = view_loss(pkg["render"], gt, lambda_dssim)
+        loss.backward()
+        apply_view_stats(gs, pkg["radii"], dp.densify_increment(pkg["viewspace_points"].grad, pkg["radii"]))
+        losses.append(float(loss.detach()))
+    opt.step()
+    opt.zero_grad(set_to_none=True)
+    return losses
+
+
+__all__ = ["GaussianState", "render_rgb", "sh_ramp", "l1_loss", "ssim", "view_loss", "apply_view_stats", "RGBTrainer",
+           "accumulate_views", "PARAM_NAMES"]
