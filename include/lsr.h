@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 4
+#define LSR_ABI_VERSION 5
 
 enum {
     LSR_OK = 0,
@@ -175,6 +175,17 @@ int lsr_mark_visible(int P, const float* means3D, const float* viewmatrix,
  * device pointers.  K must be 64 and Df a multiple of 16. */
 int lsr_quick_decode(const float* weight_map, const float* codebooks, int L, int K, int Df, int H, int W,
                      int normalize, float eps, float* out, lsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+
+/* The same decode in two steps for many frames with fixed codebooks (the
+ * eval loops of eval_lerf.py decode every view with one model's codebooks):
+ * lsr_quick_decode_prepare writes the codebook-only part (fragments, norm
+ * factor) into a caller-owned device buffer of lsr_quick_decode_plan_bytes
+ * bytes (0 = unsupported shape); lsr_quick_decode_run decodes a frame with it.
+ * The plan is valid until the codebooks change. */
+size_t lsr_quick_decode_plan_bytes(int L, int K, int Df, int normalize);
+int lsr_quick_decode_prepare(const float* codebooks, int L, int K, int Df, int normalize, void* plan, void* stream);
+int lsr_quick_decode_run(const float* weight_map, const void* plan, int L, int K, int Df, int H, int W, int normalize,
+                         float eps, float* out, void* stream);
 
 /* Fused top-k soft codes (replaces softmax_to_topk_soft_code,
  * utils/vq_utils.py:9-24; get_weights_and_indices, :26-40; the per-level

@@ -107,7 +107,8 @@ class BwdOut(ctypes.Structure):
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
 
-EXPORTS = ("lsr_forward", "lsr_backward", "lsr_mark_visible", "lsr_quick_decode", "lsr_topk_code_forward",
+EXPORTS = ("lsr_forward", "lsr_backward", "lsr_mark_visible", "lsr_quick_decode", "lsr_quick_decode_plan_bytes",
+           "lsr_quick_decode_prepare", "lsr_quick_decode_run", "lsr_topk_code_forward",
            "lsr_topk_code_backward", "lsr_topk_code_backward_sparse", "lsr_knn_dist2", "lsr_lang_loss_forward", "lsr_lang_loss_backward", "lsr_adam_step", "lsr_strerror",
            "lsr_abi_version", "lsr_max_lang_dim", "lsr_profile_enable", "lsr_profile_stages", "lsr_profile_reset",
            "lsr_profile_query")
@@ -138,6 +139,13 @@ def load(path: str | None = None):
     lib.lsr_quick_decode.argtypes = [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_float, _vp, ALLOC_FN, _vp, _vp]
     lib.lsr_quick_decode.restype = ctypes.c_int
+    lib.lsr_quick_decode_plan_bytes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.lsr_quick_decode_plan_bytes.restype = ctypes.c_size_t
+    lib.lsr_quick_decode_prepare.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]
+    lib.lsr_quick_decode_prepare.restype = ctypes.c_int
+    lib.lsr_quick_decode_run.argtypes = [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_float, _vp, _vp]
+    lib.lsr_quick_decode_run.restype = ctypes.c_int
     lib.lsr_topk_code_forward.argtypes = [_vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp,
                                           _vp, ctypes.c_int, ctypes.c_int, _vp]
     lib.lsr_topk_code_forward.restype = ctypes.c_int

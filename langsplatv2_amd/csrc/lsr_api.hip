@@ -277,6 +277,36 @@ int lsr_quick_decode(const float* weight_map, const float* codebooks, int L, int
     return LSR_OK;
 }
 
+size_t lsr_quick_decode_plan_bytes(int L, int K, int Df, int normalize)
+{
+    if (L < 0 || K != 64 || Df <= 0 || (Df % 16) != 0) return 0;
+    return lsr::quick_decode_workspace_bytes(L, K, Df, normalize);
+}
+
+int lsr_quick_decode_prepare(const float* codebooks, int L, int K, int Df, int normalize, void* plan, void* stream)
+{
+    if (L < 0 || Df <= 0 || (Df % 16) != 0) return LSR_EINVAL;
+    if (K != 64) return LSR_EUNSUPPORTED;
+    if (L == 0) return LSR_OK;
+    if (!codebooks || !plan) return LSR_EINVAL;
+    if (lsr::launch_quick_decode_prepare(codebooks, L, K, Df, normalize, plan, (hipStream_t)stream) != hipSuccess)
+        return LSR_EHIP;
+    return LSR_OK;
+}
+
+int lsr_quick_decode_run(const float* weight_map, const void* plan, int L, int K, int Df, int H, int W, int normalize,
+                         float eps, float* out, void* stream)
+{
+    if (L < 0 || H < 0 || W < 0 || Df <= 0 || (Df % 16) != 0) return LSR_EINVAL;
+    if (K != 64) return LSR_EUNSUPPORTED;
+    if (L == 0 || H == 0 || W == 0) return LSR_OK;
+    if (!weight_map || !plan || !out) return LSR_EINVAL;
+    if (lsr::launch_quick_decode_run(weight_map, nullptr, L, K, Df, H, W, normalize, eps, plan, out,
+                                     (hipStream_t)stream) != hipSuccess)
+        return LSR_EHIP;
+    return LSR_OK;
+}
+
 static int lang_loss_args(const float* wm, const float* cb, int K, int Df, int H, int W, const int32_t* seg,
                           const float* feat, int S)
 {

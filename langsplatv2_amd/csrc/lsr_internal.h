@@ -104,6 +104,9 @@ size_t knn_workspace_bytes(int64_t N, size_t sort_temp);
 hipError_t knn_sort_temp_bytes(int64_t N, size_t* bytes);
 hipError_t launch_knn_dist2(const float* points, int64_t N, float* out, uint8_t* ws, size_t sort_temp, hipStream_t st);
 size_t quick_decode_workspace_bytes(int L, int K, int Df, int normalize);
+hipError_t launch_quick_decode_prepare(const float* cb, int L, int K, int Df, int normalize, void* ws, hipStream_t st);
+hipError_t launch_quick_decode_run(const float* wmap, const float* cb, int L, int K, int Df, int H, int W,
+                                   int normalize, float eps, const void* ws, float* out, hipStream_t st);
 hipError_t launch_quick_decode(const float* wmap, const float* cb, int L, int K, int Df, int H, int W, int normalize,
                                float eps, void* ws, float* out, hipStream_t st);
 

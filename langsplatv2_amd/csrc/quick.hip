@@ -368,48 +368,70 @@ __global__ void __launch_bounds__(64, LSR_DEC_WAVES) k_quick_decode_h(const floa
 // is |L^T w_p|^2: a 64-column product on the same A fragments (1/8 of the
 // decode's matrix work), squared and summed along the output rows, with no
 // second read of the weights.
-// G[l][i][j] = sum_d CB[l][i][d] CB[l][j][d]: one wave per (row i, level), lanes along d.
-__global__ void __launch_bounds__(64) k_codebook_gram_w(const float* __restrict__ cb, int K, int Df,
-                                                        float* __restrict__ G)
+// G[l][i][j] = sum_d CB[l][i][d] CB[l][j][d]: one 256-thread workgroup per
+// (16 x 16 output tile, level), one output per thread, the two 16-row slices
+// staged through LDS 128 dims at a time.
+__global__ void __launch_bounds__(256) k_codebook_gram_t(const float* __restrict__ cb, int K, int Df,
+                                                         float* __restrict__ G)
 {
-    const int i = blockIdx.x, l = blockIdx.y, lane = threadIdx.x;
-    const float* ci = cb + ((size_t)l * K + i) * Df;
-    for (int j = 0; j < K; j++) {
-        const float* cj = cb + ((size_t)l * K + j) * Df;
-        float v = 0.f;
-        for (int d = lane; d < Df; d += 64) v = fmaf(ci[d], cj[d], v);
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-        if (lane == 0) G[((size_t)l * K + i) * K + j] = v;
+    __shared__ float sa[16][129], sb[16][129];
+    const int nt = K / 16;
+    const int ti = (int)blockIdx.x / nt, tj = (int)blockIdx.x % nt, l = blockIdx.y;
+    const int r = threadIdx.x >> 4, c = threadIdx.x & 15;
+    const float* base = cb + (size_t)l * K * Df;
+    float v = 0.f;
+    for (int d0 = 0; d0 < Df; d0 += 128) {
+        __syncthreads();
+        for (int e = threadIdx.x; e < 16 * 128; e += 256) {
+            const int rr = e >> 7, dd = e & 127;
+            const bool ok = d0 + dd < Df;
+            sa[rr][dd] = ok ? base[(size_t)(16 * ti + rr) * Df + d0 + dd] : 0.f;
+            sb[rr][dd] = ok ? base[(size_t)(16 * tj + rr) * Df + d0 + dd] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll 8
+        for (int dd = 0; dd < 128; dd++) v = fmaf(sa[r][dd], sb[c][dd], v);
     }
+    G[((size_t)l * K + 16 * ti + r) * K + 16 * tj + c] = v;
 }
 
-// Lower-triangular L with L L^T = G (per level, K <= 64, f64 in LDS).  A pivot
-// at or below 1e-12 of the largest diagonal entry (rank-deficient codebook)
-// leaves its column zero.  Output row-major (K x K) f32, zeros above the diagonal.
-__global__ void __launch_bounds__(64) k_codebook_chol(const float* __restrict__ G, int K, float* __restrict__ Lout)
+// Lower-triangular L with L L^T = G (per level, K <= 64, f64 in LDS), right-
+// looking: per column j the pivot, the column scale, then the trailing lower
+// triangle updated by all 256 threads.  A pivot at or below 1e-12 of the
+// largest diagonal entry (rank-deficient codebook) leaves its column zero.
+// Output row-major (K x K) f32, zeros above the diagonal.
+__global__ void __launch_bounds__(256) k_codebook_chol(const float* __restrict__ G, int K, float* __restrict__ Lout)
 {
     __shared__ double A[64][65];
+    __shared__ double s_tol;
     const int l = blockIdx.x, t = threadIdx.x;
     const float* g = G + (size_t)l * K * K;
-    for (int e = t; e < K * K; e += 64) A[e / K][e % K] = (double)g[e];
+    for (int e = t; e < K * K; e += 256) A[e / K][e % K] = (double)g[e];
     __syncthreads();
-    double mx = 0.0;
-    for (int j = 0; j < K; j++) mx = fmax(mx, A[j][j]);
-    const double tol = 1e-12 * mx;
+    if (t == 0) {
+        double mx = 0.0;
+        for (int j = 0; j < K; j++) mx = fmax(mx, A[j][j]);
+        s_tol = 1e-12 * mx;
+    }
+    __syncthreads();
+    const double tol = s_tol;
     for (int j = 0; j < K; j++) {
         const double d = A[j][j];
         const double piv = d > tol ? sqrt(d) : 0.0;
-        __syncthreads();
+        __syncthreads();   // every thread has read the pivot
         if (t == j) A[j][j] = piv;
         if (t > j && t < K) A[t][j] = piv > 0.0 ? A[t][j] / piv : 0.0;
         __syncthreads();
-        if (t > j && t < K)
-            for (int k = j + 1; k <= t; k++) A[t][k] -= A[t][j] * A[k][j];
+        // trailing lower triangle: rows i > j, columns j < k <= i
+        const int m = K - 1 - j;
+        for (int e = t; e < m * m; e += 256) {
+            const int i = j + 1 + e / m, k = j + 1 + e % m;
+            if (k <= i) A[i][k] -= A[i][j] * A[k][j];
+        }
+        __syncthreads();
     }
-    __syncthreads();
     float* o = Lout + (size_t)l * K * K;
-    for (int e = t; e < K * K; e += 64) {
+    for (int e = t; e < K * K; e += 256) {
         const int r = e / K, c = e % K;
         o[e] = c <= r ? (float)A[r][c] : 0.f;
     }
@@ -568,41 +590,69 @@ size_t quick_decode_workspace_bytes(int L, int K, int Df, int normalize)
 #endif
 }
 
-hipError_t launch_quick_decode(const float* wmap, const float* cb, int L, int K, int Df, int H, int W, int normalize,
-                               float eps, void* ws, float* out, hipStream_t st)
+// The plan (= the workspace): codebook fragments + scales, and with
+// normalisation the Gram matrices, their Cholesky factors and the factors'
+// fragments + scales (for Df > 512 the Gram matrices' fragments instead).
+// It depends on the codebooks only, so a caller decoding many frames with the
+// same codebooks prepares it once (lsr_quick_decode_prepare).
+hipError_t launch_quick_decode_prepare(const float* cb, int L, int K, int Df, int normalize, void* ws, hipStream_t st)
 {
-    if (L == 0 || H == 0 || W == 0) return hipSuccess;
+    if (L == 0) return hipSuccess;
 #ifdef LSR_DECODE_F32
-    const unsigned nb = (unsigned)(((W + 15) / 16) * ((H + 3) / 4));
-    float* G = (float*)ws;
     if (normalize) {
         dim3 g((unsigned)((K * K + 255) / 256), (unsigned)L);
-        k_codebook_gram<<<g, 256, 0, st>>>(cb, K, Df, G);
+        k_codebook_gram<<<g, 256, 0, st>>>(cb, K, Df, (float*)ws);
     }
-    k_quick_decode<64><<<nb, 64, 0, st>>>(wmap, L, Df, W, H, cb, G, out, eps, normalize);
 #else
     uint8_t* p = (uint8_t*)ws;
     uint4* frag = (uint4*)p;
     float* scales = (float*)(p + (size_t)L * Df * 256);
     k_codebook_frag<<<L, 256, 0, st>>>(cb, K, Df, frag, scales);
+    if (normalize) {
+        float* G = (float*)(p + (size_t)L * Df * 256 + 256);
+        float* Lf = G + (size_t)L * K * K;
+        uint4* nfrag = (uint4*)(Lf + (size_t)L * K * K);
+        float* nscales = (float*)((uint8_t*)nfrag + (size_t)L * 64 * 256);
+        k_codebook_gram_t<<<dim3((unsigned)((K / 16) * (K / 16)), (unsigned)L), 256, 0, st>>>(cb, K, Df, G);
+#ifndef LSR_DECODE_H
+        if (Df / 16 <= LSR_DEC2_MAXDB) {
+            k_codebook_chol<<<L, 256, 0, st>>>(G, K, Lf);
+            k_codebook_frag<<<L, 256, 0, st>>>(Lf, K, K, nfrag, nscales);
+        } else
+#endif
+            k_codebook_frag<<<L, 256, 0, st>>>(G, K, K, nfrag, nscales);
+    }
+#endif
+    return hipGetLastError();
+}
+
+hipError_t launch_quick_decode_run(const float* wmap, const float* cb, int L, int K, int Df, int H, int W,
+                                   int normalize, float eps, const void* ws, float* out, hipStream_t st)
+{
+    if (L == 0 || H == 0 || W == 0) return hipSuccess;
+#ifdef LSR_DECODE_F32
+    const unsigned nb = (unsigned)(((W + 15) / 16) * ((H + 3) / 4));
+    k_quick_decode<64><<<nb, 64, 0, st>>>(wmap, L, Df, W, H, cb, (const float*)ws, out, eps, normalize);
+#else
+    const uint8_t* p = (const uint8_t*)ws;
+    const uint4* frag = (const uint4*)p;
+    const float* scales = (const float*)(p + (size_t)L * Df * 256);
+    const float* G = (const float*)(p + (size_t)L * Df * 256 + 256);
+    const float* Lf = G + (size_t)L * K * K;
+    const uint4* nfrag = (const uint4*)(Lf + (size_t)L * K * K);
+    const float* nscales = (const float*)((const uint8_t*)nfrag + (size_t)L * 64 * 256);
     const bool vec = (W % 4) == 0;
-    float* G = (float*)(p + (size_t)L * Df * 256 + 256);
-    float* Lf = G + (size_t)L * K * K;
-    uint4* nfrag = (uint4*)(Lf + (size_t)L * K * K);
-    float* nscales = (float*)((uint8_t*)nfrag + (size_t)L * 64 * 256);
     const int NDB = Df / 16;
 #ifndef LSR_DECODE_H
     if (NDB <= LSR_DEC2_MAXDB) {
         // level-resident: one workgroup per CU, the CUs split evenly over the levels
-        int dev = 0, ncu = 256;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        static int ncu = [] {
+            int dev = 0, n = 256;
+            if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+            return n > 0 ? n : 256;
+        }();
         const int nwg = ncu / L > 0 ? ncu / L : 1;
         const size_t lds = (size_t)(NDB + (normalize ? 4 : 0)) * 256 * sizeof(uint4);
-        if (normalize) {
-            k_codebook_gram_w<<<dim3((unsigned)K, (unsigned)L), 64, 0, st>>>(cb, K, Df, G);
-            k_codebook_chol<<<L, 64, 0, st>>>(G, K, Lf);
-            k_codebook_frag<<<L, 256, 0, st>>>(Lf, K, K, nfrag, nscales);
-        }
         auto run = [&](auto kern) {
             (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             kern<<<(unsigned)(nwg * L), 64 * LSR_DEC2_WAVES, lds, st>>>(wmap, Df, W, H, frag, scales, nfrag, nscales,
@@ -620,9 +670,6 @@ hipError_t launch_quick_decode(const float* wmap, const float* cb, int L, int K,
 #endif
     const unsigned nb = (unsigned)(((W + 63) / 64) * H);
     if (normalize) {
-        dim3 g((unsigned)((K * K + 255) / 256), (unsigned)L);
-        k_codebook_gram<<<g, 256, 0, st>>>(cb, K, Df, G);
-        k_codebook_frag<<<L, 256, 0, st>>>(G, K, K, nfrag, nscales);
         if (vec)
             k_quick_decode_h<true, true><<<nb, 64, 0, st>>>(wmap, L, Df, W, H, frag, scales, nfrag, nscales, out, eps);
         else
@@ -636,6 +683,15 @@ hipError_t launch_quick_decode(const float* wmap, const float* cb, int L, int K,
     }
 #endif
     return hipGetLastError();
+}
+
+hipError_t launch_quick_decode(const float* wmap, const float* cb, int L, int K, int Df, int H, int W, int normalize,
+                               float eps, void* ws, float* out, hipStream_t st)
+{
+    if (L == 0 || H == 0 || W == 0) return hipSuccess;
+    const hipError_t e = launch_quick_decode_prepare(cb, L, K, Df, normalize, ws, st);
+    if (e != hipSuccess) return e;
+    return launch_quick_decode_run(wmap, cb, L, K, Df, H, W, normalize, eps, ws, out, st);
 }
 
 }  // namespace lsr

@@ -10,16 +10,20 @@ render() (eval_lerf.py:210-220, backend_renderer.py:16-36):
 and, for the dense training/eval map, compute_final_feature_map
 (scene/gaussian_model.py:545-550): codebooks.view(-1, Df).T @ W.
 
-`decode_language_features` does both in one HIP kernel (csrc/quick.hip:
-exact-f32 MFMA, per-pixel norms from the codebook Gram matrix, each output
-written once).  There is no CPU path.
+`decode_language_features` does both in one HIP kernel per frame
+(csrc/quick.hip: split-f16 MFMA with f32 accumulation, per-pixel norms from
+the Cholesky factor of the codebook Gram matrix, each output written once);
+the codebook-only preparation is cached per codebook tensor (`decode_plan`).
+There is no CPU path.
 """
 from __future__ import annotations
+
+from collections import OrderedDict
 
 import torch
 
 from . import _lib
-from .rasterizer import _Alloc, _stream
+from .rasterizer import _stream
 
 
 def decode_language_features(weight_map: torch.Tensor, codebooks: torch.Tensor, normalize: bool = True,
@@ -39,12 +43,42 @@ def decode_language_features(weight_map: torch.Tensor, codebooks: torch.Tensor, 
     wm = weight_map.contiguous().float()
     cb = codebooks.contiguous().float()
     out = torch.empty((L, Df, H, W), dtype=torch.float32, device=weight_map.device)
-    alloc = _Alloc(weight_map.device)
     lib = _lib.load()
-    rc = lib.lsr_quick_decode(wm.data_ptr(), cb.data_ptr(), L, K, Df, H, W, int(bool(normalize)), float(eps),
-                              out.data_ptr(), alloc.fn, None, _stream(weight_map.device))
-    _lib.check(rc, "lsr_quick_decode")
+    plan = decode_plan(cb, normalize)
+    rc = lib.lsr_quick_decode_run(wm.data_ptr(), plan.data_ptr(), L, K, Df, H, W, int(bool(normalize)), float(eps),
+                                  out.data_ptr(), _stream(weight_map.device))
+    _lib.check(rc, "lsr_quick_decode_run")
     return out
+
+
+_PLANS: "OrderedDict[tuple, tuple]" = OrderedDict()
+_PLAN_CACHE_SIZE = 4
+
+
+def decode_plan(codebooks: torch.Tensor, normalize: bool = True) -> torch.Tensor:
+    """The codebook-only part of the decode (MFMA fragments, Cholesky factor of
+    the Gram matrix for the norm), prepared once per codebook tensor and reused
+    for every frame (lsr_quick_decode_prepare).  Cached by the tensor's storage,
+    shape and version counter, so an in-place update of the codebooks (an
+    optimizer step) prepares a new plan."""
+    cb = codebooks.contiguous().float()
+    L, K, Df = cb.shape
+    key = (cb.data_ptr(), cb.device, tuple(cb.shape), cb._version, bool(normalize))
+    hit = _PLANS.get(key)
+    if hit is not None:
+        _PLANS.move_to_end(key)
+        return hit[1]
+    lib = _lib.load()
+    nbytes = int(lib.lsr_quick_decode_plan_bytes(L, K, Df, int(bool(normalize))))
+    if nbytes == 0:
+        raise ValueError("decode_plan: unsupported codebook shape")
+    plan = torch.empty(nbytes, dtype=torch.uint8, device=cb.device)
+    _lib.check(lib.lsr_quick_decode_prepare(cb.data_ptr(), L, K, Df, int(bool(normalize)), plan.data_ptr(),
+                                            _stream(cb.device)), "lsr_quick_decode_prepare")
+    _PLANS[key] = (cb, plan)   # the reference keeps the storage (and its data_ptr) alive
+    while len(_PLANS) > _PLAN_CACHE_SIZE:
+        _PLANS.popitem(last=False)
+    return plan
 
 
 def compute_final_feature_map(weight_map: torch.Tensor, codebooks: torch.Tensor) -> torch.Tensor:

@@ -87,3 +87,33 @@ def test_final_feature_map_any_level_count(gpu, shape):
     scale = np.abs(ref).max()
     assert got.shape == (Df, 24, 40)
     np.testing.assert_allclose(got.cpu().numpy() / scale, ref / scale, atol=DEC_ATOL, rtol=0)
+
+
+@pytest.mark.gpu
+def test_plan_reuse_one_shot_and_invalidation(gpu):
+    """lsr_quick_decode_prepare/_run (the per-codebook plan, cached by decode_plan)
+    give the one-shot lsr_quick_decode's bits; an in-place codebook update (the
+    tensor's version counter moves) prepares a new plan; a rank-deficient
+    codebook (duplicated codes: a singular Gram matrix) still normalises."""
+    import ctypes
+    from langsplatv2_amd import _lib
+    from langsplatv2_amd.rasterizer import _Alloc, _stream
+    g = np.random.default_rng(3)
+    L, K, Df, H, W = 3, 64, 512, 40, 52
+    wmap = torch.from_numpy((g.random((L * K, H, W)) * (g.random((L * K, H, W)) < 0.2)).astype(np.float32)).to(gpu)
+    cb = torch.from_numpy(g.standard_normal((L, K, Df)).astype(np.float32)).to(gpu)
+    a = quick.decode_language_features(wmap, cb)
+    b = quick.decode_language_features(wmap, cb)          # cached plan
+    one = torch.empty_like(a)
+    alloc = _Alloc(gpu)
+    lib = _lib.load()
+    _lib.check(lib.lsr_quick_decode(wmap.data_ptr(), cb.data_ptr(), L, K, Df, H, W, 1, ctypes.c_float(1e-10),
+                                    one.data_ptr(), alloc.fn, None, _stream(gpu)), "lsr_quick_decode")
+    assert torch.equal(a, b) and torch.equal(a, one)
+    cb.mul_(-0.5)                                          # in place: version counter moves
+    c = quick.decode_language_features(wmap, cb)
+    np.testing.assert_allclose(c.cpu().numpy(), ref_decode(wmap.cpu().numpy(), cb.cpu().numpy()), atol=DEC_ATOL)
+    cb2 = cb.clone()
+    cb2[:, 32:] = cb2[:, :32]                              # rank 32 per level
+    d = quick.decode_language_features(wmap, cb2)
+    np.testing.assert_allclose(d.cpu().numpy(), ref_decode(wmap.cpu().numpy(), cb2.cpu().numpy()), atol=DEC_ATOL)
