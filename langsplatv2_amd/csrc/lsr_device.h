@@ -298,10 +298,15 @@ __device__ __forceinline__ uint32_t cut_extent(float cut, float a, float c, floa
 
 // Does the Gaussian (center x,y; packed extents) possibly touch the 8x8 pixel
 // block whose top-left pixel is (bx, by)?
-__device__ __forceinline__ bool block_overlap(float x, float y, uint32_t ext, int bx, int by)
+// rect_overlap: the same for a (EX+1) x (EY+1) pixel rectangle.
+__device__ __forceinline__ bool rect_overlap(float x, float y, uint32_t ext, int bx, int by, int EX, int EY)
 {
     const float hx = (float)(ext & 0xffffu), hy = (float)(ext >> 16);
-    return (x + hx >= (float)bx) && (x - hx <= (float)(bx + 7)) && (y + hy >= (float)by) && (y - hy <= (float)(by + 7));
+    return (x + hx >= (float)bx) && (x - hx <= (float)(bx + EX)) && (y + hy >= (float)by) && (y - hy <= (float)(by + EY));
+}
+__device__ __forceinline__ bool block_overlap(float x, float y, uint32_t ext, int bx, int by)
+{
+    return rect_overlap(x, y, ext, bx, by, 7, 7);
 }
 
 // Exact (conservative) test: does the cut ellipse {d : Q(d) <= -2 cut},
@@ -313,13 +318,14 @@ __device__ __forceinline__ bool block_overlap(float x, float y, uint32_t ext, in
 // every pair the blend would accept survives (results stay bit-identical);
 // the bounding-box test (block_overlap) keeps far more false candidates for
 // thin, rotated splats.
-__device__ __forceinline__ bool block_overlap_exact(float x, float y, float ca, float cb, float cc, float cut,
-                                                    int bx, int by)
+// rect_overlap_exact: the same test for the (EX+1) x (EY+1) rectangle at (bx, by).
+__device__ __forceinline__ bool rect_overlap_exact(float x, float y, float ca, float cb, float cc, float cut,
+                                                   int bx, int by, float EX, float EY)
 {
     if (!(ca > 0.f) || !(cc > 0.f) || !(cut > -3.0e38f)) return true;   // degenerate / no cut: keep
     const float thr = fmaf(-2.f * cut, 1.001f, 1e-3f);
-    const float u1 = x - (float)bx, u0 = u1 - 7.f;   // dx over the block's columns
-    const float v1 = y - (float)by, v0 = v1 - 7.f;   // dy over its rows
+    const float u1 = x - (float)bx, u0 = u1 - EX;   // dx over the rectangle's columns
+    const float v1 = y - (float)by, v0 = v1 - EY;   // dy over its rows
     if (u0 <= 0.f && u1 >= 0.f && v0 <= 0.f && v1 >= 0.f) return true;
     const float ica = 1.f / ca, icc = 1.f / cc;
     auto q = [&](float u, float v) { return fmaf(ca * u, u, fmaf(2.f * cb * u, v, cc * v * v)); };
@@ -329,6 +335,11 @@ __device__ __forceinline__ bool block_overlap_exact(float x, float y, float ca, 
     const float ub = fminf(fmaxf(-cb * v1 * ica, u0), u1);
     const float qmin = fminf(fminf(q(u0, va), q(u1, vb)), fminf(q(ua, v0), q(ub, v1)));
     return !(qmin > thr);
+}
+__device__ __forceinline__ bool block_overlap_exact(float x, float y, float ca, float cb, float cc, float cut,
+                                                    int bx, int by)
+{
+    return rect_overlap_exact(x, y, ca, cb, cc, cut, bx, by, 7.f, 7.f);
 }
 
 // ------------------------------------------------------------- layouts --

@@ -74,6 +74,9 @@
 #define LSR_FWD_PKEXP 1     // fwd (VALU blend): the pair's two deterministic exps on packed f32 (the
                             // MFMA forwards keep the scalar exp: packed pairs there measured 5 % slower)
 #endif
+#ifndef LSR_FWD_2PX
+#define LSR_FWD_2PX 0       // fwd (VALU blend, D <= 32): two pixels per lane, one wave per 16x8 half tile (measured slower: cfg3 0.356 -> 0.361, cfg5 1.94 -> 2.09 ms)
+#endif
 #ifndef LSR_EXACT_CULL
 #define LSR_EXACT_CULL 1
 #endif
@@ -252,12 +255,31 @@ __device__ __forceinline__ uint64_t sub_mask(const float4* sA, const float4* sB,
 // Work-item mapping for the wave-independent render kernels: one 64-thread
 // workgroup (one wave) per 8x8 block; the four blocks of a tile get
 // consecutive indices inside one XCD's range (xcd_remap), so they share an L2.
+//
+// Inside its range an XCD walks the tiles in band order (band_tile): bands of
+// LSR_BAND tile rows, column by column inside a band.  A Gaussian's tiles are
+// then visited close together in time, so the lines its blocks read (records,
+// feature rows) and the backward's gradient lines its atomics update are
+// still in that XCD's L2 (row-major order revisits them a whole tile row
+// later, after ~6 MB of other lines have passed through the 4 MB L2).
+#ifndef LSR_BAND
+#define LSR_BAND 4          // tile rows per band; 0 = row-major tile order (cfg3 sum 1.487 -> 1.479 ms, cfg5 fwd 1.93 -> 1.88)
+#endif
+__device__ __forceinline__ int band_tile(int t, int gx, int gy)
+{
+    if (LSR_BAND <= 0) return t;
+    const int per = gx * LSR_BAND;
+    const int b = t / per, r = t - b * per;
+    const int rows = min(LSR_BAND, gy - b * LSR_BAND);
+    const int col = r / rows;
+    return (b * LSR_BAND + (r - col * rows)) * gx + col;
+}
 struct WaveTile {
     int tile, sub;
-    __device__ WaveTile()
+    __device__ WaveTile(const Cam& c)
     {
         const int o = xcd_remap(blockIdx.x, gridDim.x);
-        tile = o >> 2;
+        tile = band_tile(o >> 2, c.gx, c.gy);
         sub = o & 3;
     }
 };
@@ -405,7 +427,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
 #endif
 
     const Cam& c = a.cam;
-    const WaveTile wt;
+    const WaveTile wt(c);
     const int lane = threadIdx.x;
     const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
     const bool inside = pm.px < c.W && pm.py < c.H;
@@ -553,6 +575,211 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
     }
 }
 
+// Two pixels per lane (the VALU-blend forward's default): one wave per 16x8
+// half tile, two per tile; lane l owns column l & 15 of rows (l >> 4) and
+// (l >> 4) + 4.  Every broadcast LDS read of a staged candidate (geometry pair,
+// feature row, position) now serves two pixels, which halves the LDS
+// instructions per pixel of the blend; the two pixels share dx (same column),
+// so ca.dx and cb.dx are computed once; the two pixels' recurrences are
+// independent chains.  Per pixel the operation sequence is exactly
+// k_render_fwd's (bit-identical).  Stores: each instruction writes four 64-B
+// row segments.
+template <int NL>
+__global__ void __launch_bounds__(64) k_render_fwd2(RenderArgs a)
+{
+    constexpr int C = 3 + NL;
+    constexpr int F4 = (C + 3) / 4;  // float4 per feature row
+    constexpr bool SF = fwd_sfeat<NL>();
+    __shared__ WaveStageP<F4, SF> st;
+
+    const Cam& c = a.cam;
+    const int o = xcd_remap(blockIdx.x, gridDim.x);
+    const int tile = band_tile(o >> 1, c.gx, c.gy);
+    const int lane = threadIdx.x;
+    const int bx = (tile % c.gx) * LSR_TILE, by = (tile / c.gx) * LSR_TILE + (o & 1) * 8;
+    const int px = bx + (lane & 15), pyA = by + (lane >> 4), pyB = pyA + 4;
+    const bool inA = px < c.W && pyA < c.H, inB = px < c.W && pyB < c.H;
+    const float pfx = (float)px, pfyA = (float)pyA, pfyB = (float)pyB;
+    const uint32_t rs = a.tile_start[tile], re = a.tile_start[tile + 1];
+    const int D = a.D;
+
+    float TA = 1.0f, TB = 1.0f;
+    float accA[F4 * 4], accB[F4 * 4];
+#pragma unroll
+    for (int k = 0; k < F4 * 4; k++) accA[k] = accB[k] = 0.f;
+    uint32_t lastA = 0, lastB = 0;
+    bool doneA = !inA, doneB = !inB;
+
+    uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
+    for (uint32_t base = rs; base < re; base += 64) {
+        if (wave_ballot(!(doneA && doneB)) == 0) break;
+        const uint32_t idx = base + lane;
+        const bool valid = idx < re;
+        const uint32_t gid = next_gid;
+        next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;   // prefetch the next chunk's ids
+        int n;
+        {
+            float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+            if (valid) {
+                A = a.splatA[gid];
+                B = a.splatB[gid];
+            }
+            const bool ok = valid && rect_overlap(A.x, A.y, __float_as_uint(B.w), bx, by, 15, 7) &&
+                            rect_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, bx, by, 15.f, 7.f);
+            const uint64_t m = wave_ballot(ok);
+            n = __popcll(m);
+            if (ok) {
+                const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                float* sb = reinterpret_cast<float*>(&st) + (r & 1);
+                const int e = (r >> 1) * 2;
+                sb[0 * 64 + e] = A.x;
+                sb[1 * 64 + e] = A.y;
+                sb[2 * 64 + e] = A.z;
+                sb[3 * 64 + e] = A.w;
+                sb[4 * 64 + e] = B.x;
+                sb[5 * 64 + e] = B.y;
+                sb[6 * 64 + e] = B.z;
+                st.pos[r] = (int)(idx - rs) + 1;
+                if constexpr (SF)
+                    st.gid[r] = gid;
+                else
+                    stage_features<NL, F4>(&st.F[r * F4], a.rgb, a.lang, D, gid);
+            }
+            wave_lds_fence();
+        }
+        for (int j0 = 0; j0 < n; j0 += 2) {
+            if (wave_ballot(!(doneA && doneB)) == 0) break;
+            const bool two = j0 + 1 < n;
+            const int j1 = two ? j0 + 1 : j0;
+            const int e = j0 >> 1;
+            float fr0[F4 * 4], fr1[F4 * 4];
+            if constexpr (SF) {
+                feature_row_uniform<NL, F4>(fr0, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j0]));
+                feature_row_uniform<NL, F4>(fr1, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j1]));
+            }
+            // both candidates' exponents at both pixels (splat_power's sequence;
+            // a missing second candidate reads a stale slot: its ok flags mask it)
+            const f32x2 dx = st.X[e] - f32x2{pfx, pfx};
+            const f32x2 cadx = st.CA[e] * dx, cbdx = st.CB[e] * dx, CC = st.CC[e];
+            const f32x2 dyA = st.Y[e] - f32x2{pfyA, pfyA}, dyB = st.Y[e] - f32x2{pfyB, pfyB};
+            const f32x2 PA = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f},
+                                                       __builtin_elementwise_fma(cadx, dx, (CC * dyA) * dyA),
+                                                       -(cbdx * dyA));
+            const f32x2 PB = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f},
+                                                       __builtin_elementwise_fma(cadx, dx, (CC * dyB) * dyB),
+                                                       -(cbdx * dyB));
+            const f32x2 CUT = st.CUT[e], OP = st.OP[e];
+            bool okA0 = !doneA && !(PA.x > 0.0f || PA.x < CUT.x);
+            bool okA1 = two && !doneA && !(PA.y > 0.0f || PA.y < CUT.y);
+            bool okB0 = !doneB && !(PB.x > 0.0f || PB.x < CUT.x);
+            bool okB1 = two && !doneB && !(PB.y > 0.0f || PB.y < CUT.y);
+            const f32x2 EXA = expf_det2(PA), EXB = expf_det2(PB);
+            const float alA0 = fminf(0.99f, OP.x * EXA.x), alA1 = fminf(0.99f, OP.y * EXA.y);
+            const float alB0 = fminf(0.99f, OP.x * EXB.x), alB1 = fminf(0.99f, OP.y * EXB.y);
+            okA0 = okA0 && !(alA0 < 1.0f / 255.0f);
+            okA1 = okA1 && !(alA1 < 1.0f / 255.0f);
+            okB0 = okB0 && !(alB0 < 1.0f / 255.0f);
+            okB1 = okB1 && !(alB1 < 1.0f / 255.0f);
+            const uint32_t pos0 = (uint32_t)st.pos[j0], pos1 = (uint32_t)st.pos[j1];
+            // candidate j0 at both pixels
+            float aTA, aTB;
+            {
+                const float tA = TA * (1.0f - alA0), tB = TB * (1.0f - alB0);
+                const bool termA = okA0 && (tA < 0.0001f), termB = okB0 && (tB < 0.0001f);
+                doneA = doneA || termA;
+                doneB = doneB || termB;
+                okA0 = okA0 && !termA;
+                okA1 = okA1 && !termA;
+                okB0 = okB0 && !termB;
+                okB1 = okB1 && !termB;
+                aTA = okA0 ? alA0 * TA : 0.f;
+                aTB = okB0 ? alB0 * TB : 0.f;
+                TA = okA0 ? tA : TA;
+                TB = okB0 ? tB : TB;
+                lastA = okA0 ? pos0 : lastA;
+                lastB = okB0 ? pos0 : lastB;
+            }
+            if constexpr (SF) {
+#pragma unroll
+                for (int k = 0; k < F4 * 4; k++) {
+                    accA[k] = fmaf(fr0[k], aTA, accA[k]);
+                    accB[k] = fmaf(fr0[k], aTB, accB[k]);
+                }
+            } else {
+#pragma unroll
+                for (int f = 0; f < F4; f++) {
+                    const float4 v = st.F[j0 * F4 + f];
+                    accA[4 * f + 0] = fmaf(v.x, aTA, accA[4 * f + 0]);
+                    accA[4 * f + 1] = fmaf(v.y, aTA, accA[4 * f + 1]);
+                    accA[4 * f + 2] = fmaf(v.z, aTA, accA[4 * f + 2]);
+                    accA[4 * f + 3] = fmaf(v.w, aTA, accA[4 * f + 3]);
+                    accB[4 * f + 0] = fmaf(v.x, aTB, accB[4 * f + 0]);
+                    accB[4 * f + 1] = fmaf(v.y, aTB, accB[4 * f + 1]);
+                    accB[4 * f + 2] = fmaf(v.z, aTB, accB[4 * f + 2]);
+                    accB[4 * f + 3] = fmaf(v.w, aTB, accB[4 * f + 3]);
+                }
+            }
+            // candidate j1
+            {
+                const float tA = TA * (1.0f - alA1), tB = TB * (1.0f - alB1);
+                const bool termA = okA1 && (tA < 0.0001f), termB = okB1 && (tB < 0.0001f);
+                doneA = doneA || termA;
+                doneB = doneB || termB;
+                okA1 = okA1 && !termA;
+                okB1 = okB1 && !termB;
+                aTA = okA1 ? alA1 * TA : 0.f;
+                aTB = okB1 ? alB1 * TB : 0.f;
+                TA = okA1 ? tA : TA;
+                TB = okB1 ? tB : TB;
+                lastA = okA1 ? pos1 : lastA;
+                lastB = okB1 ? pos1 : lastB;
+            }
+            if constexpr (SF) {
+#pragma unroll
+                for (int k = 0; k < F4 * 4; k++) {
+                    accA[k] = fmaf(fr1[k], aTA, accA[k]);
+                    accB[k] = fmaf(fr1[k], aTB, accB[k]);
+                }
+            } else {
+#pragma unroll
+                for (int f = 0; f < F4; f++) {
+                    const float4 v = st.F[j1 * F4 + f];
+                    accA[4 * f + 0] = fmaf(v.x, aTA, accA[4 * f + 0]);
+                    accA[4 * f + 1] = fmaf(v.y, aTA, accA[4 * f + 1]);
+                    accA[4 * f + 2] = fmaf(v.z, aTA, accA[4 * f + 2]);
+                    accA[4 * f + 3] = fmaf(v.w, aTA, accA[4 * f + 3]);
+                    accB[4 * f + 0] = fmaf(v.x, aTB, accB[4 * f + 0]);
+                    accB[4 * f + 1] = fmaf(v.y, aTB, accB[4 * f + 1]);
+                    accB[4 * f + 2] = fmaf(v.z, aTB, accB[4 * f + 2]);
+                    accB[4 * f + 3] = fmaf(v.w, aTB, accB[4 * f + 3]);
+                }
+            }
+        }
+        wave_lds_fence();
+    }
+    const size_t HW = (size_t)c.H * c.W;
+    if (inA) {
+        const size_t pix = (size_t)pyA * c.W + px;
+        a.final_T[pix] = TA;
+        a.n_contrib[pix] = lastA;
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) a.out_color[ch * HW + pix] = fmaf(TA, c.bg[ch], accA[ch]);
+#pragma unroll
+        for (int k = 0; k < NL; k++)
+            if (k < D) a.out_lang[k * HW + pix] = accA[3 + k];
+    }
+    if (inB) {
+        const size_t pix = (size_t)pyB * c.W + px;
+        a.final_T[pix] = TB;
+        a.n_contrib[pix] = lastB;
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) a.out_color[ch * HW + pix] = fmaf(TB, c.bg[ch], accB[ch]);
+#pragma unroll
+        for (int k = 0; k < NL; k++)
+            if (k < D) a.out_lang[k * HW + pix] = accB[3 + k];
+    }
+}
+
 // Sparse "quick" language path: Dq output channels, K (weight, index) pairs
 // per Gaussian.  One wave per 8x8 pixel block; per-pixel accumulators in LDS
 // laid out [channel][lane] (conflict-free: the channel index is wave-uniform
@@ -569,7 +796,7 @@ __global__ void __launch_bounds__(64) k_render_fwd_quick(RenderArgs a)
     int* sI = (int*)(sW + 64 * K);                                // 64 * K
 
     const Cam& c = a.cam;
-    const int tile = xcd_remap(blockIdx.x >> 2, gridDim.x >> 2);
+    const int tile = band_tile(xcd_remap(blockIdx.x >> 2, gridDim.x >> 2), c.gx, c.gy);
     const int t = threadIdx.x;
     const PixMap pm(c, tile, t + ((blockIdx.x & 3) << 6));
     const bool inside = pm.px < c.W && pm.py < c.H;
@@ -717,7 +944,7 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
     static_assert(NP >= 1 && NP <= 6, "up to 192 quick channels");
     __shared__ WaveStageV st;
     const Cam& c = a.cam;
-    const WaveTile wt;
+    const WaveTile wt(c);
     const int lane = threadIdx.x;
     const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
     const bool inside = pm.px < c.W && pm.py < c.H;
@@ -930,6 +1157,11 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
         case 4: k_render_fwd_mf<4><<<4 * T, 64, 0, st>>>(a); break;
         case 8: k_render_fwd_mf<8><<<4 * T, 64, 0, st>>>(a); break;
         case 16: k_render_fwd_mf<16><<<4 * T, 64, 0, st>>>(a); break;
+#elif LSR_FWD_2PX
+        case 0: k_render_fwd2<0><<<2 * T, 64, 0, st>>>(a); break;
+        case 4: k_render_fwd2<4><<<2 * T, 64, 0, st>>>(a); break;
+        case 8: k_render_fwd2<8><<<2 * T, 64, 0, st>>>(a); break;
+        case 16: k_render_fwd2<16><<<2 * T, 64, 0, st>>>(a); break;
 #else
         case 0: k_render_fwd<0><<<4 * T, 64, 0, st>>>(a); break;
         case 4: k_render_fwd<4><<<4 * T, 64, 0, st>>>(a); break;
@@ -938,7 +1170,11 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
 #endif
 #if LSR_FWD_MF_WIDE
         // measured (cfg3 geometry): D = 32 legacy 0.78 vs MFMA 0.81 ms; D = 64 legacy 1.38 vs MFMA 1.13 ms
+#if LSR_FWD_2PX
+        case 32: k_render_fwd2<32><<<2 * T, 64, 0, st>>>(a); break;
+#else
         case 32: k_render_fwd<32><<<4 * T, 64, 0, st>>>(a); break;
+#endif
         case 64: k_render_fwd_mf<64><<<4 * T, 64, 0, st>>>(a); break;
 #else
         case 32: k_render_fwd<32><<<4 * T, 64, 0, st>>>(a); break;
@@ -1070,7 +1306,7 @@ __global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs b)
 
     const RenderArgs& a = b.f;
     const Cam& c = a.cam;
-    const WaveTile wt;
+    const WaveTile wt(c);
     const int lane = threadIdx.x;
     const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
     const bool inside = pm.px < c.W && pm.py < c.H;
@@ -1311,6 +1547,9 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
 #ifndef LSR_BWD_RSCAT
 #define LSR_BWD_RSCAT 1     // bwd: phase-3 sums reduced two values per permlane swap, parked in LDS
 #endif
+#ifndef LSR_BWD_ATOM_BATCH
+#define LSR_BWD_ATOM_BATCH 1   // bwd: the group's atomic values and ids read from LDS before any atomic issues
+#endif
 #define LSR_MOM9_STRIDE 12  // reduced moment + colour sums per candidate (16-B aligned rows)
 static_assert(!LSR_BWD_RSCAT || LSR_BWD_ALIAS, "the reduced sums are parked in the aliased aT tile");
 #define LSR_LOG2E 1.4426950408889634f
@@ -1476,7 +1715,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 
     const RenderArgs& a = b.f;
     const Cam& c = a.cam;
-    const WaveTile wt;
+    const WaveTile wt(c);
     const int lane = threadIdx.x;
     const int lg = lane >> 4, li = lane & 15;
     const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
@@ -1960,24 +2199,55 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                         }
                     }
                 }
-            } else
+            } else {
+#if LSR_BWD_ATOM_BATCH
+                // every value and id the group's atomics need is read from LDS
+                // first (one wait), then the atomics issue back to back
+                uint32_t gq[4];
+                float vq[GRL][4];
 #pragma unroll
-            for (int h = 0; h < GRL; h++) {
-                const int f = 16 * h + li;
-                const bool fcol = LO ? (f < D)
-                                  : LD ? (h == 0 ? (f < 9) : (f - 16 < D))
-                                       : ((f < 9) | ((f >= LSR_GROW_LANG) & (f < LSR_GROW_LANG + D)));
+                for (int q = 0; q < 4; q++) gq[q] = st.gid[g0 + 4 * q + lg];
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int slot = 4 * q + lg;
-                    const float v = sGr[slot * GRS + f];
-                    if (fcol & (slot < kn) & (v != 0.f)) {
-                        if (LD && h > 0)
-                            LSR_MF_ATOMIC(b.lang_acc + (size_t)st.gid[g0 + slot] * D + (f - 16), v);
-                        else
-                            LSR_MF_ATOMIC(b.grad_acc + (size_t)st.gid[g0 + slot] * VP + f, v);
+                for (int h = 0; h < GRL; h++)
+#pragma unroll
+                    for (int q = 0; q < 4; q++) vq[h][q] = sGr[(4 * q + lg) * GRS + 16 * h + li];
+#pragma unroll
+                for (int h = 0; h < GRL; h++) {
+                    const int f = 16 * h + li;
+                    const bool fcol = LO ? (f < D)
+                                      : LD ? (h == 0 ? (f < 9) : (f - 16 < D))
+                                           : ((f < 9) | ((f >= LSR_GROW_LANG) & (f < LSR_GROW_LANG + D)));
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const float v = vq[h][q];
+                        if (fcol & (4 * q + lg < kn) & (v != 0.f)) {
+                            if (LD && h > 0)
+                                LSR_MF_ATOMIC(b.lang_acc + (size_t)gq[q] * D + (f - 16), v);
+                            else
+                                LSR_MF_ATOMIC(b.grad_acc + (size_t)gq[q] * VP + f, v);
+                        }
                     }
                 }
+#else
+#pragma unroll
+                for (int h = 0; h < GRL; h++) {
+                    const int f = 16 * h + li;
+                    const bool fcol = LO ? (f < D)
+                                      : LD ? (h == 0 ? (f < 9) : (f - 16 < D))
+                                           : ((f < 9) | ((f >= LSR_GROW_LANG) & (f < LSR_GROW_LANG + D)));
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const int slot = 4 * q + lg;
+                        const float v = sGr[slot * GRS + f];
+                        if (fcol & (slot < kn) & (v != 0.f)) {
+                            if (LD && h > 0)
+                                LSR_MF_ATOMIC(b.lang_acc + (size_t)st.gid[g0 + slot] * D + (f - 16), v);
+                            else
+                                LSR_MF_ATOMIC(b.grad_acc + (size_t)st.gid[g0 + slot] * VP + f, v);
+                        }
+                    }
+                }
+#endif
             }
             wave_lds_fence();
             BWD_STAMP(6);
@@ -2049,7 +2319,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_fwd_mf(RenderArgs a
     __shared__ float sT[64];
 
     const Cam& c = a.cam;
-    const WaveTile wt;
+    const WaveTile wt(c);
     const int lane = threadIdx.x;
     const int lg = lane >> 4, li = lane & 15;
     const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
@@ -2207,7 +2477,7 @@ __global__ void __launch_bounds__(64) k_render_fwd_quick_mf(RenderArgs a)
     __shared__ float sT[64];
 
     const Cam& c = a.cam;
-    const WaveTile wt;
+    const WaveTile wt(c);
     const int lane = threadIdx.x;
     const int lg = lane >> 4, li = lane & 15;
     const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
@@ -2399,7 +2669,7 @@ __global__ void __launch_bounds__(64 * NS) k_render_fwd_quick_wg(RenderArgs a)
     __shared__ int sN[2];
 
     const Cam& c = a.cam;
-    const WaveTile wt;
+    const WaveTile wt(c);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int lg = lane >> 4, li = lane & 15;
     const int q0 = w * DQ;
