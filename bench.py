@@ -88,6 +88,9 @@ def algorithmic_bytes(g, rs, D, S):
     staged_f = torch.minimum(cnt, ((tmax + 1 + 255) // 256) * 256).sum().item()
     staged_b = torch.minimum(cnt, ((tmax + 255) // 256) * 256).sum().item()
     vis = int((radii > 0).sum().item())
+    # the reference's instance count for the same frame (its 3-sigma rect lists, A.2);
+    # this build's binning drops the instances whose cut ellipse misses the tile
+    M_ref = int(dec["tiles_touched"].to(torch.int64)[radii > 0].sum().item())
     P = W * H
     T = gx * gy
     C = 3 + D
@@ -102,8 +105,8 @@ def algorithmic_bytes(g, rs, D, S):
         "render_bwd": M * (28 + 4 * C) + T * 8 + P * (4 * C + 8) + N * (24 + 4 * C),
         "preprocess_bwd": N * (12 + 12 + 16 + 4 * S + 4 + 24 + 12 + 8 + 12 + 3) + N * (12 + 12 + 16 + 4 * S + 12),
     }
-    return b, dict(num_rendered=M, visible=vis, staged_fwd=staged_f, staged_bwd=staged_b,
-                   mean_n_contrib=float(nc.float().mean().item()))
+    return b, dict(num_rendered=M, num_rendered_reference=M_ref, visible=vis, staged_fwd=staged_f,
+                   staged_bwd=staged_b, mean_n_contrib=float(nc.float().mean().item()))
 
 
 def pmc_traffic(stage):
@@ -423,6 +426,10 @@ def main() -> int:
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": int(bytes_[dom]),
+                # context: the same §8d formula with the reference's M (its full rect lists) for
+                # this frame, i.e. the bytes the reference's algorithm implies for the same output
+                "algorithmic_bytes_reference_M": int(bytes_[dom] + (info["num_rendered_reference"] - info["num_rendered"])
+                                                     * (28 + 4 * (3 + D))) if dom in ("render_fwd", "render_bwd") else None,
                 "bytes_formula": "SURVEY.md §8d (bench.py:algorithmic_bytes)",
                 "ms_per_launch": round(dom_ms, 4),
                 "launches_timed": dom_calls,

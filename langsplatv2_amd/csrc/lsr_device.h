@@ -273,10 +273,13 @@ __device__ __forceinline__ float splat_power(float ca, float cb, float cc, float
 // Conservative exponent cut: for power < cut, opacity*exp(power) < 1/255 is
 // certain, so the pair is skipped without evaluating exp.  Never changes a
 // result (the margin 0.02 dwarfs exp/log rounding); only saves work.
+// The logarithm is taken in double and rounded once, so the value is the
+// oracle's (lso_power_cut) bit for bit: the binning's tile cull (tile_keep)
+// decides with it, and both sides must emit the same instance lists.
 __device__ __forceinline__ float power_cut(float o)
 {
     if (!(o * 255.0f > 1.0f)) return (o == o) ? -0.02f : -INFINITY;
-    return -__logf(255.0f * o) - 0.02f;
+    return (float)(-log((double)(255.0f * o))) - 0.02f;
 }
 
 // Conservative half-extents (pixels) of the region where power >= cut, i.e.
@@ -318,14 +321,57 @@ __device__ __forceinline__ bool block_overlap(float x, float y, uint32_t ext, in
 // every pair the blend would accept survives (results stay bit-identical);
 // the bounding-box test (block_overlap) keeps far more false candidates for
 // thin, rotated splats.
-// rect_overlap_exact: the same test for the (EX+1) x (EY+1) rectangle at (bx, by).
+// The test with its per-Gaussian part (threshold, reciprocals) prepared once,
+// for loops that test one Gaussian against many rectangles (the binning's
+// tile cull); rect_overlap_exact below is the same sequence of operations.
+struct CutEllipse {
+    float x, y, ca, cb, cc, thr, ica, icc;
+    bool all;   // degenerate / no cut: every rectangle is kept
+    __device__ __forceinline__ CutEllipse() {}
+    // packed form for LDS staging: {x, y, ca, cb}, {cc, thr, ica, icc}; `all`
+    // travels as thr = +inf (then every path of meets() returns true)
+    __device__ __forceinline__ void pack(float4& p0, float4& p1) const
+    {
+        p0 = make_float4(x, y, ca, cb);
+        p1 = make_float4(cc, all ? INFINITY : thr, ica, icc);
+    }
+    __device__ __forceinline__ CutEllipse(const float4& p0, const float4& p1)
+        : x(p0.x), y(p0.y), ca(p0.z), cb(p0.w), cc(p1.x), thr(p1.y), ica(p1.z), icc(p1.w), all(p1.y == INFINITY) {}
+    __device__ __forceinline__ CutEllipse(float x_, float y_, float ca_, float cb_, float cc_, float cut)
+        : x(x_), y(y_), ca(ca_), cb(cb_), cc(cc_)
+    {
+        all = !(ca > 0.f) || !(cc > 0.f) || !(cut > -3.0e38f);
+        thr = fmaf(-2.f * cut, 1.001f, 1e-3f);
+        ica = 1.f / ca;
+        icc = 1.f / cc;
+    }
+    // does the ellipse meet the (EX+1) x (EY+1) rectangle at (bx, by)?
+    __device__ __forceinline__ bool meets(int bx, int by, float EX, float EY) const
+    {
+        if (all) return true;
+        const float u1 = x - (float)bx, u0 = u1 - EX;   // dx over the rectangle's columns
+        const float v1 = y - (float)by, v0 = v1 - EY;   // dy over its rows
+        if (u0 <= 0.f && u1 >= 0.f && v0 <= 0.f && v1 >= 0.f) return true;
+        auto q = [&](float u, float v) { return fmaf(ca * u, u, fmaf(2.f * cb * u, v, cc * v * v)); };
+        const float va = fminf(fmaxf(-cb * u0 * icc, v0), v1);
+        const float vb = fminf(fmaxf(-cb * u1 * icc, v0), v1);
+        const float ua = fminf(fmaxf(-cb * v0 * ica, u0), u1);
+        const float ub = fminf(fmaxf(-cb * v1 * ica, u0), u1);
+        const float qmin = fminf(fminf(q(u0, va), q(u1, vb)), fminf(q(ua, v0), q(ub, v1)));
+        return !(qmin > thr);
+    }
+};
+
+// rect_overlap_exact: the same test for the (EX+1) x (EY+1) rectangle at
+// (bx, by), in one piece (the reciprocals only past the early exits: the
+// render's staging mostly exits early).
 __device__ __forceinline__ bool rect_overlap_exact(float x, float y, float ca, float cb, float cc, float cut,
                                                    int bx, int by, float EX, float EY)
 {
     if (!(ca > 0.f) || !(cc > 0.f) || !(cut > -3.0e38f)) return true;   // degenerate / no cut: keep
     const float thr = fmaf(-2.f * cut, 1.001f, 1e-3f);
-    const float u1 = x - (float)bx, u0 = u1 - EX;   // dx over the rectangle's columns
-    const float v1 = y - (float)by, v0 = v1 - EY;   // dy over its rows
+    const float u1 = x - (float)bx, u0 = u1 - EX;
+    const float v1 = y - (float)by, v0 = v1 - EY;
     if (u0 <= 0.f && u1 >= 0.f && v0 <= 0.f && v1 >= 0.f) return true;
     const float ica = 1.f / ca, icc = 1.f / cc;
     auto q = [&](float u, float v) { return fmaf(ca * u, u, fmaf(2.f * cb * u, v, cc * v * v)); };
@@ -340,6 +386,28 @@ __device__ __forceinline__ bool block_overlap_exact(float x, float y, float ca, 
                                                     int bx, int by)
 {
     return rect_overlap_exact(x, y, ca, cb, cc, cut, bx, by, 7.f, 7.f);
+}
+// Binning's tile cull: can Gaussian (splat records A, B) contribute to any
+// pixel of tile (tx, ty)?  The exact cut-ellipse test on the whole 16x16 tile
+// (no clipping at the image border).  A rejected instance has alpha < 1/255 at
+// every pixel of its tile, so dropping it from the tile's list changes no
+// output; the reference's 3-sigma rect (A.2) emits 43 % more instances at cfg3
+// (tools/bin_cull_census.py).
+#ifndef LSR_TILE_CULL
+#define LSR_TILE_CULL 1     // 0: the reference's full rect lists (A/B timing only; the oracle's cull=False)
+#endif
+__device__ __forceinline__ CutEllipse tile_cull_prep(const float4& A, const float4& B)
+{
+    return CutEllipse(A.x, A.y, A.z, A.w, B.x, B.z);
+}
+__device__ __forceinline__ bool tile_keep(const CutEllipse& e, int tx, int ty)
+{
+    if (!LSR_TILE_CULL) return true;
+    return e.meets(tx * LSR_TILE, ty * LSR_TILE, 15.f, 15.f);
+}
+__device__ __forceinline__ bool tile_keep(const float4& A, const float4& B, int tx, int ty)
+{
+    return tile_keep(tile_cull_prep(A, B), tx, ty);
 }
 
 // ------------------------------------------------------------- layouts --

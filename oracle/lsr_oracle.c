@@ -318,6 +318,60 @@ int64_t lso_num_rendered(int N, const uint32_t* t)
     return m;
 }
 
+/* Conservative cut of the pair exponent: opacity * exp(power) < 1/255 for
+ * every power below it (lsr_device.h power_cut, the log taken in double and
+ * rounded once on both sides). */
+float lso_power_cut(float o)
+{
+    if (!(o * 255.0f > 1.0f)) return (o == o) ? -0.02f : -INFINITY;
+    return (float)(-log((double)(255.0f * o))) - 0.02f;
+}
+
+/* Does the cut ellipse {d : Q(d) <= -2 cut} of the Gaussian at (x, y) with
+ * conic (ca, cb, cc) meet the 16x16 tile (tx, ty)?  Q is convex: its minimum
+ * over the tile is 0 with the centre inside, else on an edge at a clamped
+ * stationary point; relative + absolute margin.  Operation for operation
+ * lsr_device.h rect_overlap_exact with a 15 x 15 extent. */
+int lso_tile_keep(float x, float y, float ca, float cb, float cc, float cut, int tx, int ty)
+{
+    if (!(ca > 0.f) || !(cc > 0.f) || !(cut > -3.0e38f)) return 1;
+    const float thr = fmaf(-2.f * cut, 1.001f, 1e-3f);
+    const float u1 = x - (float)(tx * TILE), u0 = u1 - 15.f;
+    const float v1 = y - (float)(ty * TILE), v0 = v1 - 15.f;
+    if (u0 <= 0.f && u1 >= 0.f && v0 <= 0.f && v1 >= 0.f) return 1;
+    const float ica = 1.f / ca, icc = 1.f / cc;
+#define LSO_Q(u, v) fmaf(ca * (u), (u), fmaf(2.f * cb * (u), (v), cc * (v) * (v)))
+    const float va = fminf(fmaxf(-cb * u0 * icc, v0), v1);
+    const float vb = fminf(fmaxf(-cb * u1 * icc, v0), v1);
+    const float ua = fminf(fmaxf(-cb * v0 * ica, u0), u1);
+    const float ub = fminf(fmaxf(-cb * v1 * ica, u0), u1);
+    const float qmin = fminf(fminf(LSO_Q(u0, va), LSO_Q(u1, vb)), fminf(LSO_Q(ua, v0), LSO_Q(ub, v1)));
+#undef LSO_Q
+    return !(qmin > thr);
+}
+
+static inline int keep_instance(const lso_geom* g, int i, float cut, int tx, int ty)
+{
+    const float* co = g->conic_opacity + 4 * i;
+    return lso_tile_keep(g->xy[2 * i], g->xy[2 * i + 1], co[0], co[1], co[2], cut, tx, ty);
+}
+
+int64_t lso_num_rendered_ex(const lso_settings* s, int N, const lso_geom* g, int cull)
+{
+    if (!cull) return lso_num_rendered(N, g->tiles_touched);
+    const int gx = (s->W + TILE - 1) / TILE, gy = (s->H + TILE - 1) / TILE;
+    int64_t m = 0;
+    for (int i = 0; i < N; i++) {
+        if (g->radii[i] <= 0) continue;
+        int r0[2], r1[2];
+        get_rect(g->xy[2 * i], g->xy[2 * i + 1], g->radii[i], gx, gy, r0, r1);
+        const float cut = lso_power_cut(g->conic_opacity[4 * i + 3]);
+        for (int y = r0[1]; y < r1[1]; y++)
+            for (int x = r0[0]; x < r1[0]; x++) m += keep_instance(g, i, cut, x, y);
+    }
+    return m;
+}
+
 static int cmp_u64(const void* a, const void* b)
 {
     uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
@@ -326,9 +380,15 @@ static int cmp_u64(const void* a, const void* b)
 
 void lso_binning(const lso_settings* s, int N, const lso_geom* g, uint32_t* point_list, uint32_t* ranges)
 {
+    lso_binning_ex(s, N, g, point_list, ranges, 0);
+}
+
+void lso_binning_ex(const lso_settings* s, int N, const lso_geom* g, uint32_t* point_list, uint32_t* ranges,
+                    int cull)
+{
     const int gx = (s->W + TILE - 1) / TILE, gy = (s->H + TILE - 1) / TILE;
     const int T = gx * gy;
-    int64_t M = lso_num_rendered(N, g->tiles_touched);
+    int64_t M = lso_num_rendered_ex(s, N, g, cull);
     /* Counting sort by tile, then per-tile sort by (depth bits, id): the
      * order of a stable sort on (tile<<32 | depth bits) with duplicates
      * emitted in Gaussian order (Appendix A.2). */
@@ -337,8 +397,10 @@ void lso_binning(const lso_settings* s, int N, const lso_geom* g, uint32_t* poin
         if (g->radii[i] <= 0) continue;
         int r0[2], r1[2];
         get_rect(g->xy[2 * i], g->xy[2 * i + 1], g->radii[i], gx, gy, r0, r1);
+        const float cut = lso_power_cut(g->conic_opacity[4 * i + 3]);
         for (int y = r0[1]; y < r1[1]; y++)
-            for (int x = r0[0]; x < r1[0]; x++) cnt[y * gx + x + 1]++;
+            for (int x = r0[0]; x < r1[0]; x++)
+                if (!cull || keep_instance(g, i, cut, x, y)) cnt[y * gx + x + 1]++;
     }
     for (int t = 0; t < T; t++) cnt[t + 1] += cnt[t];
     uint64_t* keys = (uint64_t*)malloc((size_t)(M > 0 ? M : 1) * sizeof(uint64_t));
@@ -350,8 +412,10 @@ void lso_binning(const lso_settings* s, int N, const lso_geom* g, uint32_t* poin
         get_rect(g->xy[2 * i], g->xy[2 * i + 1], g->radii[i], gx, gy, r0, r1);
         uint32_t db;
         memcpy(&db, &g->depth[i], 4);
+        const float cut = lso_power_cut(g->conic_opacity[4 * i + 3]);
         for (int y = r0[1]; y < r1[1]; y++)
             for (int x = r0[0]; x < r1[0]; x++) {
+                if (cull && !keep_instance(g, i, cut, x, y)) continue;
                 int t = y * gx + x;
                 keys[cur[t]++] = ((uint64_t)db << 32) | (uint32_t)i;
             }

@@ -86,6 +86,18 @@ int64_t lso_num_rendered(int N, const uint32_t* tiles_touched);
 void lso_binning(const lso_settings* s, int N, const lso_geom* g,
                  uint32_t* point_list, uint32_t* ranges);
 
+/* The same with the product's tile cull (cull != 0): an instance (Gaussian,
+ * tile) of the rect is kept only if the Gaussian's cut ellipse meets the
+ * 16x16 tile (lso_tile_keep, the restatement of lsr_device.h tile_keep).
+ * Dropped instances have alpha < 1/255 at every pixel of their tile, so the
+ * rendered outputs equal lso_binning's; the lists shrink.  cull = 0 is
+ * lso_num_rendered / lso_binning. */
+int64_t lso_num_rendered_ex(const lso_settings* s, int N, const lso_geom* g, int cull);
+void lso_binning_ex(const lso_settings* s, int N, const lso_geom* g,
+                    uint32_t* point_list, uint32_t* ranges, int cull);
+float lso_power_cut(float opacity);
+int lso_tile_keep(float x, float y, float ca, float cb, float cc, float cut, int tx, int ty);
+
 /* A.3 render forward.  out_color 3*H*W; out_lang Dout*H*W (Dout = D dense
  * or quick_dim); final_T, n_contrib H*W.  Tiles are processed in parallel
  * with OpenMP when nthreads > 1 (results do not depend on nthreads). */

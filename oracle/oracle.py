@@ -60,6 +60,12 @@ def load():
         lib = ctypes.CDLL(_SO)
         lib.lso_num_rendered.restype = ctypes.c_int64
         lib.lso_num_rendered.argtypes = [ctypes.c_int, _vp]
+        lib.lso_num_rendered_ex.restype = ctypes.c_int64
+        lib.lso_num_rendered_ex.argtypes = [_vp, ctypes.c_int, _vp, ctypes.c_int]
+        lib.lso_binning_ex.restype = None
+        lib.lso_binning_ex.argtypes = [_vp, ctypes.c_int, _vp, _vp, _vp, ctypes.c_int]
+        lib.lso_power_cut.restype = ctypes.c_float
+        lib.lso_power_cut.argtypes = [ctypes.c_float]
         lib.lso_expf.restype = ctypes.c_float
         lib.lso_expf.argtypes = [ctypes.c_float]
         _lib = lib
@@ -122,9 +128,12 @@ class Problem:
         return s, i
 
 
-def forward(pb: Problem, nthreads: int = 1, tiles=None) -> dict:
+def forward(pb: Problem, nthreads: int = 1, tiles=None, cull: bool = True) -> dict:
     """Full oracle forward; returns geometry, binning and image outputs.
-    `tiles`: optional subset of tile ids to render (others left zero)."""
+    `tiles`: optional subset of tile ids to render (others left zero).
+    `cull`: the product's tile cull in the binning (lso_binning_ex); False
+    gives the reference's instance lists (A.2) — the rendered outputs are the
+    same either way (tests/test_oracle.py::test_tile_cull_changes_no_output)."""
     lib = load()
     N = pb.N
     g = dict(depth=np.zeros(N, np.float32), radii=np.zeros(N, np.int32), xy=np.zeros((N, 2), np.float32),
@@ -135,11 +144,11 @@ def forward(pb: Problem, nthreads: int = 1, tiles=None) -> dict:
                                      "tiles_touched")])
     s, i = pb._structs()
     lib.lso_preprocess(ctypes.byref(s), ctypes.byref(i), ctypes.byref(geom))
-    M = int(lib.lso_num_rendered(N, _p(g["tiles_touched"])))
+    M = int(lib.lso_num_rendered_ex(ctypes.byref(s), N, ctypes.byref(geom), int(bool(cull))))
     T = pb.gx * pb.gy
     point_list = np.zeros(max(M, 1), np.uint32)
     ranges = np.zeros((T, 2), np.uint32)
-    lib.lso_binning(ctypes.byref(s), N, ctypes.byref(geom), _p(point_list), _p(ranges))
+    lib.lso_binning_ex(ctypes.byref(s), N, ctypes.byref(geom), _p(point_list), _p(ranges), int(bool(cull)))
     Dout = pb.quick_dim if pb.quick else pb.D
     H, W = pb.H, pb.W
     color = np.zeros((3, H, W), np.float32)

@@ -166,13 +166,14 @@ def test_cfg5_binning_and_image_properties(gpu):
     N, W, H = t["means3D"].shape[0], rs.image_width, rs.image_height
     dec = layout.decode(bufs, N, W, H, M)
     tt = dec["tiles_touched"].to(torch.int64)
-    assert M == int(tt[radii > 0].sum()) and M > 0
+    assert 0 < M <= int(tt[radii > 0].sum())
     ts = dec["tile_start"].to(torch.int64)
     assert int(ts[0]) == 0 and int(ts[-1]) == M and bool((ts[1:] >= ts[:-1]).all())
     pl = dec["point_list"].to(torch.int64)
-    # every visible Gaussian appears exactly tiles_touched times
+    # every visible Gaussian appears at most tiles_touched times (the tile
+    # cull keeps the rect tiles its cut ellipse meets), invisible ones never
     counts = torch.bincount(pl, minlength=N)
-    assert torch.equal(counts, torch.where(radii > 0, tt, torch.zeros_like(tt)))
+    assert bool((counts <= torch.where(radii > 0, tt, torch.zeros_like(tt))).all())
     # strict (depth bits, id) order inside each tile
     key = (dec["depth"].contiguous().view(torch.int32).to(torch.int64)[pl] << 32) | pl
     tile_of = torch.repeat_interleave(torch.arange(ts.numel() - 1, device=gpu), ts[1:] - ts[:-1])

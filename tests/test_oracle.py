@@ -269,19 +269,26 @@ def test_expf_accuracy(oracle_lib):
     assert oracle_lib.expf(0.0) == 1.0
 
 
-def test_binning_properties(oracle_lib):
+@pytest.mark.parametrize("cull", [False, True])
+def test_binning_properties(oracle_lib, cull):
     from oracle import oracle as O
     case = make_case(400, 96, 80, seed=11, sh_degree=0)
-    fwd = O.forward(oracle_problem(case))
+    fwd = O.forward(oracle_problem(case), cull=cull)
     rng = fwd["ranges"]
     pl = fwd["point_list"]
     tt = fwd["tiles_touched"]
-    assert fwd["num_rendered"] == int(tt.sum()) == len(pl)
+    assert fwd["num_rendered"] == len(pl)
     # ranges tile the point list contiguously in tile order
     nz = rng[rng[:, 1] > rng[:, 0]]
     assert np.all(nz[1:, 0] == nz[:-1, 1]) and nz[0, 0] == 0 and nz[-1, 1] == len(pl)
-    # every Gaussian appears exactly tiles_touched times
-    np.testing.assert_array_equal(np.bincount(pl, minlength=len(tt)), tt)
+    counts = np.bincount(pl, minlength=len(tt))
+    if cull:
+        # the tile cull keeps a subset of each Gaussian's rect tiles
+        assert np.all(counts <= tt) and len(pl) < int(tt.sum())
+    else:
+        # the reference's lists: every Gaussian exactly tiles_touched times
+        assert fwd["num_rendered"] == int(tt.sum())
+        np.testing.assert_array_equal(counts, tt)
     # within a tile: (depth, id) ascending
     d = fwd["depth"]
     for s, e in rng:
@@ -312,3 +319,36 @@ def test_tile_subset_render_matches_full(oracle_lib):
         sl = (slice(ty * 16, ty * 16 + 16), slice(tx * 16, tx * 16 + 16))
         np.testing.assert_array_equal(sub["color"][(slice(None),) + sl], full["color"][(slice(None),) + sl])
         np.testing.assert_array_equal(sub["n_contrib"][sl], full["n_contrib"][sl])
+
+
+TILE_CULL_CASES = {
+    "rgb": dict(N=3000, W=96, H=80, seed=21, sh_degree=None),
+    "sh3_lang16_bg": dict(N=4000, W=112, H=72, seed=22, sh_degree=3, lang_dim=16, bg=(0.2, 0.4, 0.6)),
+    "yaw_cov_precomp": dict(N=3000, W=80, H=64, seed=23, sh_degree=1, yaw=25.0, cov_precomp=True),
+    "quick": dict(N=2000, W=64, H=48, seed=24, sh_degree=3, quick_k=4),
+}
+
+
+@pytest.mark.parametrize("name", sorted(TILE_CULL_CASES))
+def test_tile_cull_changes_no_output(oracle_lib, name):
+    """The product's binning drops the (Gaussian, tile) instances whose cut
+    ellipse misses the tile (tile_keep).  Against the reference's full lists
+    (A.2) the culled lists render the same images, final_T and visibility
+    bit for bit, and the backward gives the same gradients: a dropped pair
+    has alpha < 1/255 at every pixel of its tile, so it never contributes."""
+    from oracle import oracle as O
+    case = make_case(**TILE_CULL_CASES[name])
+    pb = oracle_problem(case)
+    full = O.forward(pb, nthreads=4, cull=False)
+    cut = O.forward(pb, nthreads=4, cull=True)
+    assert 0 < cut["num_rendered"] < full["num_rendered"]
+    for k in ("color", "lang", "final_T", "radii"):
+        np.testing.assert_array_equal(cut[k], full[k], err_msg=k)
+    rng = np.random.default_rng(5)
+    dC = rng.standard_normal(full["color"].shape).astype(np.float32)
+    dL = rng.standard_normal(full["lang"].shape).astype(np.float32) if full["lang"].shape[0] else None
+    gf = O.backward(pb, full, dC, dL)
+    gc = O.backward(pb, cut, dC, dL)
+    for k, v in gf.items():
+        if isinstance(v, np.ndarray) and v.dtype.kind == "f":
+            np.testing.assert_array_equal(gc[k], v, err_msg=k)
