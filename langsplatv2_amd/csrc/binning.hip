@@ -266,7 +266,9 @@ hipError_t launch_scatter(const Cam& c, int P, const uint8_t* geom, const int32_
 // re-walks the chunk and places every instance at tile_start + block base +
 // LDS-atomic rank.  No global atomics; the in-bucket order is arbitrary and
 // fixed by the per-tile sort.
-#define BIN_BLOCK 256
+#ifndef BIN_BLOCK
+#define BIN_BLOCK 512   // 8 waves per (chunk, band) block: bin_count 0.097 -> 0.077 ms at cfg3 with the tile cull (A/B)
+#endif
 
 // Screen bands: blockIdx.y = band of `rows` tile rows, so a block's LDS
 // histogram covers rows * gx tiles (<= LSR_BAND_LDS bytes) and several blocks
