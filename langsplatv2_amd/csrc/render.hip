@@ -1734,65 +1734,12 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     const int wmax = wave_max_i(last);
     if (wmax == 0) return;
     BWD_STAMP_DECL
-    // entries past a group's end are read unconditionally (immediate-offset
-    // loads, no index clamps): keep them finite
-    for (int e = lane; e < 80; e += 64) {
-        st.A[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-        st.B[e] = make_float4(0.f, 0.f, 0.f, __int_as_float(0x7fffffff));
-        st.gid[e] = 0u;
-    }
-
-    float dotB[KS][4], chB[NBA][16];
-    if constexpr (!LO) {
-#pragma unroll
-        for (int t = 0; t < KS; t++)
-#pragma unroll
-            for (int pb = 0; pb < 4; pb++)
-#ifdef LSR_PROBE_NOPRO   // timing probe only (wrong results): no prologue dL/dout loads
-                dotB[t][pb] = (float)(t * 4 + pb + lane);
-#else
-                dotB[t][pb] = gd_at<NL>(b, 4 * t + lg, pb * 16 + li, pm.bx, pm.by);
-#endif
-    }
-#if LSR_BWD_VMOM
-#pragma unroll
-    for (int nb = 0; nb < NBC; nb++)
-#pragma unroll
-        for (int t = 0; t < 16; t++)
-#ifdef LSR_PROBE_NOPRO
-            chB[nb][t] = (float)(t + lane);
-#else
-            chB[nb][t] = gd_at<NL>(b, 3 + nb * 16 + li, 4 * t + lg, pm.bx, pm.by);
-#endif
-    if constexpr (!LO)
-        sDrgb[lane] = make_float4(gd_at<NL>(b, 0, lane, pm.bx, pm.by), gd_at<NL>(b, 1, lane, pm.bx, pm.by),
-                                  gd_at<NL>(b, 2, lane, pm.bx, pm.by), 0.f);
-    // block-centred x of the pixels this lane's fragments cover: columns lg
-    // (even K-steps) and 4 + lg (odd K-steps)
-    const float lxe = (float)lg - 3.5f, lxo = (float)lg + 0.5f;
-    const float lxe2 = lxe * lxe, lxo2 = lxo * lxo;
-#else
-#pragma unroll
-    for (int nb = 0; nb < NBC; nb++)
-#pragma unroll
-        for (int t = 0; t < 16; t++) chB[nb][t] = gd_at<NL>(b, nb * 16 + li, 4 * t + lg, pm.bx, pm.by);
-#endif
-    const float bg0 = c.bg[0], bg1 = c.bg[1], bg2 = c.bg[2];
-    const float bg_dot = (inside && !LO)
-                             ? bg0 * b.dout_color[pix] + bg1 * b.dout_color[HW + pix] + bg2 * b.dout_color[2 * HW + pix]
-                             : 0.f;   // 0 with a black background: the term below is then exact 0
-
-    const bool has_bg = (bg0 != 0.f) || (bg1 != 0.f) || (bg2 != 0.f);   // uniform
-    float T = T_final;
-    float S = 0.f;
-
-    // positions [0, wmax) back to front, 64 per chunk; candidates are processed
-    // in groups of 16, a partial group carried into the next chunk
-    int carry = 0;
-    float af[KS];
-#if LSR_BWD_AF_PF
-    bool af_ready = false;
-#endif
+    // Prologue order: the loads the first chunk's staging depends on (ids,
+    // then records) are issued before the block's dL/dout fragments, so
+    // waiting for them (vector-memory operations complete in issue order)
+    // never waits for the 40 fragment loads; the lane's own RGB dL/dout is
+    // loaded first among those, reaches LDS (sDrgb) just before the chunk
+    // loop, and gives the background term without reloading it.
     // SPF: chunk c's ids are loaded two chunks ahead and its records one chunk
     // ahead, so staging never waits on a dependent gather (9 more VGPRs: off
     // for the widest language set, where they would spill)
@@ -1818,6 +1765,71 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
         }
 #endif
     }
+    // entries past a group's end are read unconditionally (immediate-offset
+    // loads, no index clamps): keep them finite
+    for (int e = lane; e < 80; e += 64) {
+        st.A[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+        st.B[e] = make_float4(0.f, 0.f, 0.f, __int_as_float(0x7fffffff));
+        st.gid[e] = 0u;
+    }
+
+    float dr0 = 0.f, dr1 = 0.f, dr2 = 0.f;   // the lane's own pixel's RGB dL/dout (0 outside the image)
+    if constexpr (!LO) {
+        dr0 = gd_at<NL>(b, 0, lane, pm.bx, pm.by);
+        dr1 = gd_at<NL>(b, 1, lane, pm.bx, pm.by);
+        dr2 = gd_at<NL>(b, 2, lane, pm.bx, pm.by);
+    }
+    float dotB[KS][4], chB[NBA][16];
+    if constexpr (!LO) {
+#pragma unroll
+        for (int t = 0; t < KS; t++)
+#pragma unroll
+            for (int pb = 0; pb < 4; pb++)
+#ifdef LSR_PROBE_NOPRO   // timing probe only (wrong results): no prologue dL/dout loads
+                dotB[t][pb] = (float)(t * 4 + pb + lane);
+#else
+                dotB[t][pb] = gd_at<NL>(b, 4 * t + lg, pb * 16 + li, pm.bx, pm.by);
+#endif
+    }
+#if LSR_BWD_VMOM
+#pragma unroll
+    for (int nb = 0; nb < NBC; nb++)
+#pragma unroll
+        for (int t = 0; t < 16; t++)
+#ifdef LSR_PROBE_NOPRO
+            chB[nb][t] = (float)(t + lane);
+#else
+            chB[nb][t] = gd_at<NL>(b, 3 + nb * 16 + li, 4 * t + lg, pm.bx, pm.by);
+#endif
+    // block-centred x of the pixels this lane's fragments cover: columns lg
+    // (even K-steps) and 4 + lg (odd K-steps)
+    const float lxe = (float)lg - 3.5f, lxo = (float)lg + 0.5f;
+    const float lxe2 = lxe * lxe, lxo2 = lxo * lxo;
+#else
+#pragma unroll
+    for (int nb = 0; nb < NBC; nb++)
+#pragma unroll
+        for (int t = 0; t < 16; t++) chB[nb][t] = gd_at<NL>(b, nb * 16 + li, 4 * t + lg, pm.bx, pm.by);
+#endif
+    const float bg0 = c.bg[0], bg1 = c.bg[1], bg2 = c.bg[2];
+    // dr* are the lane's own pixel's values (0 outside): 0 with a black
+    // background, and the term below is then exact 0
+    const float bg_dot = LO ? 0.f : bg0 * dr0 + bg1 * dr1 + bg2 * dr2;
+
+    const bool has_bg = (bg0 != 0.f) || (bg1 != 0.f) || (bg2 != 0.f);   // uniform
+    float T = T_final;
+    float S = 0.f;
+
+    // positions [0, wmax) back to front, 64 per chunk; candidates are processed
+    // in groups of 16, a partial group carried into the next chunk
+    int carry = 0;
+    float af[KS];
+#if LSR_BWD_AF_PF
+    bool af_ready = false;
+#endif
+#if LSR_BWD_VMOM
+    if constexpr (!LO) sDrgb[lane] = make_float4(dr0, dr1, dr2, 0.f);
+#endif
     BWD_STAMP(0);
     for (int c0 = 0; c0 < wmax; c0 += 64) {
         const int p = wmax - 1 - (c0 + lane);
