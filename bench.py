@@ -330,7 +330,8 @@ def main() -> int:
             grads = torch.autograd.grad([color, lang], inputs, [dcolor, dlang])
         if timed_exchange:
             xev[0].record()
-        red, _, _ = exch.finish(grads[-1], radii, grads[:-1])
+        red, _, _ = exch.finish(grads[-1], radii, grads[:-1], campos=rs.campos, means3D=g["means3D"].detach(),
+                                sh_degree=deg)
         if timed_exchange:
             xev[1].record()
             xev[1].synchronize()
@@ -411,7 +412,7 @@ def main() -> int:
                 if world > 1 else "single GPU",
             },
             "ranks_seen": dist.get_world_size() if world > 1 else 1,
-            "exchange": ({"bucket_bytes": exch.bucket_bytes,
+            "exchange": ({"bucket_bytes": exch.bucket_bytes, "sh_factored": exch.sh_idx is not None,
                           "early_bucket_bytes": exch.early.nbytes if exch.early is not None else 0,
                           "exposed_ms_per_step": round(xms[0] / max(xms[1], 1), 4),
                           **{k: round(v, 4) for k, v in dp.allreduce_bound_ms(exch.bucket_bytes, world).items()}}

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 5
+#define LSR_ABI_VERSION 6
 
 enum {
     LSR_OK = 0,
@@ -152,6 +152,14 @@ typedef struct lsr_bwd_out {
      * dL_dlang_weights are final (before the preprocess backward), so a
      * data-parallel caller can start their all-reduce early (§8e). */
     void* lang_ready_event;
+    /* View-factored SH gradient (multi-GPU exchange): when set,
+     * (N,3) receives the SH evaluation's colour gradient dL/dRGB of each
+     * Gaussian (0 where the SH colour was clamped, 0 for Gaussians outside the
+     * view).  dL/dsh of this view is basis(dir) (x) that vector, so a
+     * data-parallel caller exchanges these 3 floats (plus the camera centre)
+     * instead of the 3*M of dL_dsh and rebuilds the summed SH gradient with
+     * lsr_sh_grad_from_views.  dL_dsh may then be NULL. */
+    float* dL_drgb_sh;
 } lsr_bwd_out;
 
 /* _C.rasterize_gaussians_backward.  With settings.debug set, every stage is
@@ -159,6 +167,16 @@ typedef struct lsr_bwd_out {
  * (LSR_ENONFINITE; the offending array is named on stderr). */
 int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* b,
                  lsr_bwd_out* out, lsr_alloc_fn alloc, void* alloc_ctx, void* stream);
+
+/* Sum over R views of the SH coefficient gradient, from each view's
+ * dL_drgb_sh (lsr_bwd_out): dL_dsh[i][k][c] = sum_r basis_k(dir_ri) *
+ * drgb[r][i][c] with dir_ri = normalize(means3D[i] - campos[r]) and the basis
+ * of the forward's SH evaluation at `sh_degree` (coefficients above it get 0).
+ * Views are summed in order r = 0..R-1, so every rank computes identical
+ * values.  means3D (N,3), campos (R,3), drgb (R,N,3), dL_dsh (N,M,3): device
+ * pointers; M = max SH coefficients per Gaussian (<= 16). */
+int lsr_sh_grad_from_views(int64_t N, int M, int sh_degree, const float* means3D, int R, const float* campos,
+                           const float* drgb, float* dL_dsh, void* stream);
 
 /* _C.mark_visible: present[i] = (view-space z of means3D[i]) > 0.2. */
 int lsr_mark_visible(int P, const float* means3D, const float* viewmatrix,

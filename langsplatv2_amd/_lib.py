@@ -102,6 +102,7 @@ class BwdOut(ctypes.Structure):
         ("dL_drotations", _vp),
         ("dL_dlang_weights", _vp),
         ("lang_ready_event", _vp),
+        ("dL_drgb_sh", _vp),
     ]
 
 
@@ -109,7 +110,7 @@ ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, c
 
 EXPORTS = ("lsr_forward", "lsr_backward", "lsr_mark_visible", "lsr_quick_decode", "lsr_quick_decode_plan_bytes",
            "lsr_quick_decode_prepare", "lsr_quick_decode_run", "lsr_topk_code_forward",
-           "lsr_topk_code_backward", "lsr_topk_code_backward_sparse", "lsr_knn_dist2", "lsr_lang_loss_forward", "lsr_lang_loss_backward", "lsr_adam_step", "lsr_strerror",
+           "lsr_topk_code_backward", "lsr_topk_code_backward_sparse", "lsr_knn_dist2", "lsr_lang_loss_forward", "lsr_lang_loss_backward", "lsr_adam_step", "lsr_sh_grad_from_views", "lsr_strerror",
            "lsr_abi_version", "lsr_max_lang_dim", "lsr_profile_enable", "lsr_profile_stages", "lsr_profile_reset",
            "lsr_profile_query")
 
@@ -166,6 +167,9 @@ def load(path: str | None = None):
     _cd = ctypes.c_double
     lib.lsr_adam_step.argtypes = [_vp, _vp, _vp, _vp, ctypes.c_int64, _cd, _cd, _cd, _cd, _cd, ctypes.c_int64, _vp]
     lib.lsr_adam_step.restype = ctypes.c_int
+    lib.lsr_sh_grad_from_views.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int, _vp, _vp,
+                                           _vp, _vp]
+    lib.lsr_sh_grad_from_views.restype = ctypes.c_int
     lib.lsr_strerror.argtypes = [ctypes.c_int]
     lib.lsr_strerror.restype = ctypes.c_char_p
     lib.lsr_abi_version.restype = ctypes.c_int

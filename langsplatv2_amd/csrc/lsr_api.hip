@@ -425,6 +425,19 @@ int lsr_knn_dist2(const float* points, int64_t N, float* out, lsr_alloc_fn alloc
     return LSR_OK;
 }
 
+int lsr_sh_grad_from_views(int64_t N, int M, int sh_degree, const float* means3D, int R, const float* campos,
+                           const float* drgb, float* dL_dsh, void* stream)
+{
+    if (N < 0 || M < 1 || M > 16 || sh_degree < 0 || sh_degree > 3 || (sh_degree + 1) * (sh_degree + 1) > M || R < 0)
+        return LSR_EINVAL;
+    if (N == 0) return LSR_OK;
+    if (!means3D || !dL_dsh || (R > 0 && (!campos || !drgb))) return LSR_EINVAL;
+    if (lsr::launch_sh_grad_from_views(N, M, sh_degree, means3D, R, campos, drgb, dL_dsh, (hipStream_t)stream) !=
+        hipSuccess)
+        return LSR_EHIP;
+    return LSR_OK;
+}
+
 int lsr_abi_version(void) { return LSR_ABI_VERSION; }
 
 int lsr_max_lang_dim(void) { return 64; }
@@ -690,13 +703,14 @@ static int guard_bwd_outputs(Guard& g, const lsr_inputs* in, const lsr_bwd_out* 
     LSR_GUARD(g, "dL_dscales", o->dL_dscales, P * 3);
     LSR_GUARD(g, "dL_drotations", o->dL_drotations, P * 4);
     LSR_GUARD(g, "dL_dlang_weights", o->dL_dlang_weights, P * (size_t)in->quick_k);
+    LSR_GUARD(g, "dL_drgb_sh", o->dL_drgb_sh, P * 3);
     return LSR_OK;
 }
 
 static bool geometry_requested(const lsr_bwd_out* o)
 {
     return o->dL_dmeans2D || o->dL_dcolors || o->dL_dopacity || o->dL_dmeans3D || o->dL_dcov3D || o->dL_dsh ||
-           o->dL_dscales || o->dL_drotations;
+           o->dL_dscales || o->dL_drotations || o->dL_drgb_sh;
 }
 
 static int record_lang_ready(const lsr_bwd_out* out, hipStream_t st)

@@ -20,6 +20,8 @@ struct Cam {
 
 // preprocess.hip
 hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, int32_t* radii, hipStream_t st);
+hipError_t launch_sh_grad_from_views(int64_t N, int M, int deg, const float* means3D, int R, const float* campos,
+                                     const float* drgb, float* dL_dsh, hipStream_t st);
 hipError_t launch_preprocess_bwd(const Cam& c, const lsr_inputs& in, const uint8_t* geom, const int32_t* radii,
                                  const float* grad_acc, int VP, const lsr_bwd_out& out, hipStream_t st);
 hipError_t launch_mark_visible(int P, const float* means, const float* view, uint8_t* present, hipStream_t st);

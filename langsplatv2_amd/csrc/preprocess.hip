@@ -198,6 +198,8 @@ __device__ __forceinline__ void preprocess_bwd_one(const Cam& c, const lsr_input
                 for (int k = 0; k < M * 3; k++) out.dL_dsh[(size_t)i * M * 3 + k] = 0.f;
             }
         }
+        if (out.dL_drgb_sh)
+            for (int k = 0; k < 3; k++) out.dL_drgb_sh[3 * i + k] = 0.f;
         if (out.dL_dscales) for (int k = 0; k < 3; k++) out.dL_dscales[3 * i + k] = 0.f;
         if (out.dL_drotations) reinterpret_cast<float4*>(out.dL_drotations)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (out.dL_dcov3D) for (int k = 0; k < 6; k++) out.dL_dcov3D[6 * i + k] = 0.f;
@@ -273,6 +275,8 @@ __device__ __forceinline__ void preprocess_bwd_one(const Cam& c, const lsr_input
         float dRGB[3];
 #pragma unroll
         for (int k = 0; k < 3; k++) dRGB[k] = ((clampm >> k) & 1u) ? 0.f : gcol[k];
+        if (out.dL_drgb_sh)
+            for (int k = 0; k < 3; k++) out.dL_drgb_sh[3 * i + k] = dRGB[k];
         float dir[3], dor[3];
         sh_dir(mx, my, mz, c.campos, dir, dor);
         const float x = dir[0], y = dir[1], z = dir[2];
@@ -360,6 +364,9 @@ __device__ __forceinline__ void preprocess_bwd_one(const Cam& c, const lsr_input
         dm[0] += ((sum2 - dor[0] * dor[0]) * gd0 - dor[1] * dor[0] * gd1 - dor[2] * dor[0] * gd2) * inv32;
         dm[1] += (-dor[0] * dor[1] * gd0 + (sum2 - dor[1] * dor[1]) * gd1 - dor[2] * dor[1] * gd2) * inv32;
         dm[2] += (-dor[0] * dor[2] * gd0 - dor[1] * dor[2] * gd1 + (sum2 - dor[2] * dor[2]) * gd2) * inv32;
+    }
+    else if (out.dL_drgb_sh) {
+        for (int k = 0; k < 3; k++) out.dL_drgb_sh[3 * i + k] = 0.f;
     }
     if (out.dL_dmeans3D) {
         out.dL_dmeans3D[3 * i] = dm[0];
@@ -451,6 +458,79 @@ hipError_t launch_preprocess_bwd(const Cam& c, const lsr_inputs& in, const uint8
         k_preprocess_bwd_sh16<<<(in.P + 63) / 64, 64, 0, st>>>(c, in, geom, radii, grad_acc, VP, out);
     else
         k_preprocess_bwd<<<(in.P + 255) / 256, 256, 0, st>>>(c, in, geom, radii, grad_acc, VP, out);
+    return hipGetLastError();
+}
+
+// dRGB/dsh_k of the forward's SH evaluation (sh_channel) at direction
+// (x, y, z): the basis value multiplying coefficient k, same expressions as
+// preprocess_bwd_one's.
+__device__ __forceinline__ void sh_basis(int deg, float x, float y, float z, float (&bk)[16])
+{
+#pragma unroll
+    for (int k = 0; k < 16; k++) bk[k] = 0.f;
+    bk[0] = 0.28209479177387814f;
+    if (deg > 0) {
+        const float c1 = 0.4886025119029199f;
+        bk[1] = -c1 * y;
+        bk[2] = c1 * z;
+        bk[3] = -c1 * x;
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z;
+            const float xy = x * y, yz = y * z, xz = x * z;
+            bk[4] = LSR_C2_0 * xy;
+            bk[5] = LSR_C2_1 * yz;
+            bk[6] = LSR_C2_2 * (2.f * zz - xx - yy);
+            bk[7] = LSR_C2_3 * xz;
+            bk[8] = LSR_C2_4 * (xx - yy);
+            if (deg > 2) {
+                bk[9] = LSR_C3_0 * y * (3.f * xx - yy);
+                bk[10] = LSR_C3_1 * xy * z;
+                bk[11] = LSR_C3_2 * y * (4.f * zz - xx - yy);
+                bk[12] = LSR_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                bk[13] = LSR_C3_4 * x * (4.f * zz - xx - yy);
+                bk[14] = LSR_C3_5 * z * (xx - yy);
+                bk[15] = LSR_C3_6 * x * (xx - 3.f * yy);
+            }
+        }
+    }
+}
+
+// The view-factored SH gradient: one thread per Gaussian sums R views'
+// basis (x) dRGB products in view order and writes the (M,3) row once.
+__global__ void __launch_bounds__(256) k_sh_grad_from_views(int64_t N, int M, int deg, const float* __restrict__ means3D,
+                                                            int R, const float* __restrict__ campos,
+                                                            const float* __restrict__ drgb, float* __restrict__ dL_dsh)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const float mx = means3D[3 * i], my = means3D[3 * i + 1], mz = means3D[3 * i + 2];
+    float acc[48];
+#pragma unroll
+    for (int k = 0; k < 48; k++) acc[k] = 0.f;
+    for (int r = 0; r < R; r++) {
+        const float* g = drgb + ((size_t)r * N + i) * 3;
+        const float g0 = g[0], g1 = g[1], g2 = g[2];
+        if (g0 == 0.f && g1 == 0.f && g2 == 0.f) continue;   // outside this view (or clamped): adds exact zeros
+        float dir[3], dor[3];
+        sh_dir(mx, my, mz, campos + 3 * r, dir, dor);
+        float bk[16];
+        sh_basis(deg, dir[0], dir[1], dir[2], bk);
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            acc[3 * k] += bk[k] * g0;
+            acc[3 * k + 1] += bk[k] * g1;
+            acc[3 * k + 2] += bk[k] * g2;
+        }
+    }
+    float* o = dL_dsh + (size_t)i * M * 3;
+    for (int k = 0; k < M * 3; k++) o[k] = k < 48 ? acc[k] : 0.f;
+}
+
+hipError_t launch_sh_grad_from_views(int64_t N, int M, int deg, const float* means3D, int R, const float* campos,
+                                     const float* drgb, float* dL_dsh, hipStream_t st)
+{
+    if (N == 0) return hipSuccess;
+    k_sh_grad_from_views<<<(unsigned)((N + 255) / 256), 256, 0, st>>>(N, M, deg, means3D, R, campos, drgb, dL_dsh);
     return hipGetLastError();
 }
 

@@ -48,12 +48,17 @@ import torch.nn as nn
 from . import _lib
 
 
-_SINKS = threading.local()
+# The active sinks, process-wide: autograd runs a CUDA backward on its own
+# device thread, not on the thread that entered the context (a thread-local
+# stack is invisible there).
+_SINKS: list = []
+_SINKS_LOCK = threading.Lock()
 
 
 class GradSink:
     """Destinations for the gradients of the rasterizer backward(s) run while
-    the context is active (on this thread):
+    the context is active (process-wide: the backward runs on autograd's
+    device thread):
 
       buffers     {input name: tensor}: preallocated fp32 outputs, used when
                   shape / device match (the library writes every element), e.g.
@@ -62,31 +67,37 @@ class GradSink:
                   as soon as dL/dlanguage is final (before the preprocess
                   backward), so a collective on another stream can start early;
       on_lang_ready  optional callable run right after the library call has
-                  been enqueued (host side), e.g. to launch that collective.
+                  been enqueued (host side), e.g. to launch that collective;
+      rgb_sh      optional (N,3) fp32 tensor: the view-factored SH gradient
+                  (multi-GPU exchange, dp.py): the backward writes the SH
+                  colour gradient dL/dRGB here instead of dL/dshs, and returns
+                  buffers["shs"] as the SH gradient, which the caller fills
+                  after the exchange (lsr_sh_grad_from_views).  Used only when
+                  buffers has "shs" and the SH input needs a gradient.
 
     Input names: means3D, means2D, shs, colors_precomp, language_feature_precomp,
     language_feature_weights_quick, opacities, scales, rotations, cov3D_precomp."""
 
-    def __init__(self, buffers=None, lang_ready=None, on_lang_ready=None):
+    def __init__(self, buffers=None, lang_ready=None, on_lang_ready=None, rgb_sh=None):
         self.buffers = dict(buffers or {})
         self.lang_ready = lang_ready
         self.on_lang_ready = on_lang_ready
+        self.rgb_sh = rgb_sh
 
     def __enter__(self):
-        st = getattr(_SINKS, "stack", None)
-        if st is None:
-            st = _SINKS.stack = []
-        st.append(self)
+        with _SINKS_LOCK:
+            _SINKS.append(self)
         return self
 
     def __exit__(self, *exc):
-        _SINKS.stack.pop()
+        with _SINKS_LOCK:
+            _SINKS.remove(self)
         return False
 
 
 def _sink() -> Optional[GradSink]:
-    st = getattr(_SINKS, "stack", None)
-    return st[-1] if st else None
+    with _SINKS_LOCK:
+        return _SINKS[-1] if _SINKS else None
 
 
 class GaussianRasterizationSettings(NamedTuple):
@@ -299,8 +310,17 @@ class _RasterizeGaussians(torch.autograd.Function):
         ev = sink.lang_ready if sink is not None else None
         if ev is not None and not ev.cuda_event:
             ev.record(torch.cuda.current_stream(dev))   # materialise the event handle
+        # view-factored SH gradient: the library writes dL/dRGB of the SH
+        # evaluation; g_sh (the sink's buffer) is filled by the exchange
+        rgb_sh = None
+        if (sink is not None and sink.rgb_sh is not None and g_sh is not None and "shs" in sink.buffers
+                and g_sh.data_ptr() == sink.buffers["shs"].data_ptr()):
+            rgb_sh = sink.rgb_sh
+            if tuple(rgb_sh.shape) != (N, 3) or rgb_sh.dtype != torch.float32 or not rgb_sh.is_contiguous():
+                raise ValueError("GradSink.rgb_sh must be a contiguous (N, 3) fp32 tensor")
         bout = _lib.BwdOut(_ptr(g_means2D), _ptr(g_col), _ptr(g_lang), _ptr(g_opac), _ptr(g_means3D), _ptr(g_cov),
-                           _ptr(g_sh), _ptr(g_sc), _ptr(g_rot), _ptr(g_qw), ev.cuda_event if ev is not None else None)
+                           None if rgb_sh is not None else _ptr(g_sh), _ptr(g_sc), _ptr(g_rot), _ptr(g_qw),
+                           ev.cuda_event if ev is not None else None, _ptr(rgb_sh))
         alloc = _Alloc(dev)
         rc = lib.lsr_backward(ctypes.byref(s), ctypes.byref(ins), ctypes.byref(bin_), ctypes.byref(bout), alloc.fn,
                               None, _stream(dev))

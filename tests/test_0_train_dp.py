@@ -121,3 +121,101 @@ def test_rgb_step_two_ranks_equals_accum_iter_two(tmp_path):
     dp_losses = [v for s in range(STEPS) for v in (r0["losses"][s], r1["losses"][s])]
     assert dp_losses[:WORLD] == ref["losses"][:WORLD]
     assert dp_losses == pytest.approx(ref["losses"], rel=1e-5, abs=0)
+
+
+# ---- the zero-copy exchange with the view-factored SH gradient (bench.py's path) ----
+ZKEYS = ("means3D", "shs", "opacities", "scales", "rotations")
+
+
+def _zc_inputs(dev):
+    sys.path.insert(0, ROOT)
+    from langsplatv2_amd.scenes import make_camera, make_gaussians
+    cams = [make_camera(W, H, yaw_deg=y) for y in (-7.0, 7.0)]
+    g = make_gaussians(N, cams[0], seed=12, sh_degree=3)
+    leaves = [g[k].to(dev).contiguous().requires_grad_(True) for k in ZKEYS]
+    return cams, leaves
+
+
+def _zc_view(cam, leaves, dev, seed):
+    sys.path.insert(0, ROOT)
+    import bench
+    from diff_gaussian_rasterization import GaussianRasterizer
+    rs = bench.settings(cam, dev, 3, False)
+    m2d = torch.zeros_like(leaves[0], requires_grad=True)
+    kw = dict(zip(ZKEYS, leaves))
+    color, _, radii = GaussianRasterizer(rs)(means2D=m2d, **kw)
+    dC = torch.randn(color.shape, generator=torch.Generator().manual_seed(seed)).to(dev)
+    return rs, color, radii, m2d, dC
+
+
+def _zc_rank(rank, world, port, outdir):
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    from langsplatv2_amd import dp
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        cams, leaves = _zc_inputs(dev)
+        ex = dp.ViewShardedExchange(leaves, with_stats=True, names=list(ZKEYS))
+        assert ex.sh_idx is not None and ex.world == world
+        rs, color, radii, m2d, dC = _zc_view(cams[rank], leaves, dev, seed=rank)
+        with ex.sink():
+            grads = torch.autograd.grad([color], leaves + [m2d], [dC])
+        red, stats, max_r = ex.finish(grads[-1], radii, grads[:-1], campos=rs.campos, means3D=leaves[0].detach(),
+                                      sh_degree=3)
+        torch.cuda.synchronize()
+        torch.save({"grads": [r.detach().cpu() for r in red], "stats": stats.cpu(), "max_r": max_r.cpu()},
+                   os.path.join(outdir, f"zc{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def _zc_reference(_i, world, outdir):
+    sys.path.insert(0, ROOT)
+    from langsplatv2_amd import dp
+    dev = torch.device("cuda:0")
+    cams, leaves = _zc_inputs(dev)
+    tot, stats, max_r = None, None, None
+    for r in range(world):
+        rs, color, radii, m2d, dC = _zc_view(cams[r], leaves, dev, seed=r)
+        g = torch.autograd.grad([color], leaves + [m2d], [dC])
+        tot = list(g[:-1]) if tot is None else [a + b for a, b in zip(tot, g[:-1])]
+        inc = dp.densify_increment(g[-1], radii)
+        stats = inc if stats is None else stats + inc
+        max_r = radii if max_r is None else torch.maximum(max_r, radii)
+    torch.cuda.synchronize()
+    torch.save({"grads": [t.cpu() for t in tot], "stats": stats.cpu(), "max_r": max_r.cpu()},
+               os.path.join(outdir, "zcref.pt"))
+
+
+def test_zero_copy_exchange_factored_sh_two_ranks(tmp_path):
+    """bench.py's exchange (GradSink buckets, early language all-reduce, the SH
+    gradient rebuilt from the two views' all-gathered colour gradients and
+    camera centres) on two gloo ranks equals the sum of the two views'
+    gradients computed in one process (GRAD-level tolerance: float atomics);
+    both ranks hold bit-identical results."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    out = str(tmp_path)
+    port = _free_port()
+    procs = [ctx.Process(target=_zc_rank, args=(r, WORLD, port, out)) for r in range(WORLD)]
+    procs.append(ctx.Process(target=_zc_reference, args=(0, WORLD, out)))
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=100)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0] * len(procs), f"worker exit codes {codes}"
+    a, b, ref = (torch.load(os.path.join(out, f), weights_only=True) for f in ("zc0.pt", "zc1.pt", "zcref.pt"))
+    for name, x, y, z in zip(ZKEYS, a["grads"], b["grads"], ref["grads"]):
+        assert torch.equal(x, y), f"{name}: the ranks' reduced gradients differ"
+        scale = max(1.0, float(z.abs().max()))
+        err = float((x - z).abs().max())
+        assert err <= 1e-6 + 1e-5 * scale, f"{name}: {err:.3e} vs tolerance {1e-6 + 1e-5 * scale:.3e}"
+    assert float(ref["grads"][1].abs().max()) > 1e-3       # the SH gradient is exercised
+    torch.testing.assert_close(a["stats"], ref["stats"], rtol=1e-5, atol=1e-7)
+    assert torch.equal(a["max_r"], ref["max_r"])

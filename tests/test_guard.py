@@ -15,7 +15,7 @@ from langsplatv2_amd import _lib
 def test_status_codes_have_text():
     lib = _lib.load()
     assert b"non-finite" in lib.lsr_strerror(_lib.LSR_ENONFINITE).lower()
-    assert lib.lsr_abi_version() == 5
+    assert lib.lsr_abi_version() == 6
 
 
 def _render(case, dev, debug, poison=None):
