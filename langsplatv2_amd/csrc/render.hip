@@ -77,6 +77,10 @@
 #ifndef LSR_FWD_2PX
 #define LSR_FWD_2PX 0       // fwd (VALU blend, D <= 32): two pixels per lane, one wave per 16x8 half tile (measured slower: cfg3 0.356 -> 0.361, cfg5 1.94 -> 2.09 ms)
 #endif
+#ifndef LSR_FWD_LASTJ
+#define LSR_FWD_LASTJ 1     // fwd: the last contributor tracked as a staged index (one select per candidate),
+                            // its tile-list position read from LDS once per chunk
+#endif
 #ifndef LSR_EXACT_CULL
 #define LSR_EXACT_CULL 1
 #endif
@@ -461,6 +465,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
         // blends it with weight 0 and keeps T.  The two exp chains are
         // independent (ILP); T carries from the first to the second exactly
         // as in the sequential per-pixel order.
+        int lastj = -1;   // LASTJ: staged index of the chunk's last contributor
         for (int j0 = 0; j0 < n; j0 += 2) {
             if (wave_ballot(!done) == 0) break;
             const bool two = j0 + 1 < n;
@@ -530,7 +535,8 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                     }
                 }
                 T = ok0 ? test_T : T;
-                last = ok0 ? (uint32_t)st.pos[j0] : last;
+                if (LSR_FWD_LASTJ) lastj = ok0 ? j0 : lastj;
+                else last = ok0 ? (uint32_t)st.pos[j0] : last;
             }
             if (!LSR_FWD_SKIPVOTE || wave_any(ok1)) {
                 const float test_T = T * (1.0f - al1);
@@ -557,9 +563,11 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                     }
                 }
                 T = ok1 ? test_T : T;
-                last = ok1 ? (uint32_t)st.pos[j1] : last;
+                if (LSR_FWD_LASTJ) lastj = ok1 ? j1 : lastj;
+                else last = ok1 ? (uint32_t)st.pos[j1] : last;
             }
         }
+        if (LSR_FWD_LASTJ && lastj >= 0) last = (uint32_t)st.pos[lastj];
         wave_lds_fence();
     }
     if (inside) {
