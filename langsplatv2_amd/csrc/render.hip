@@ -77,6 +77,9 @@
 #ifndef LSR_FWD_2PX
 #define LSR_FWD_2PX 0       // fwd (VALU blend, D <= 32): two pixels per lane, one wave per 16x8 half tile (measured slower: cfg3 0.356 -> 0.361, cfg5 1.94 -> 2.09 ms)
 #endif
+#ifndef LSR_FWD_SPF
+#define LSR_FWD_SPF 1       // fwd: chunk records loaded one chunk ahead (ids two ahead)
+#endif
 #ifndef LSR_FWD_LASTJ
 #define LSR_FWD_LASTJ 1     // fwd: the last contributor tracked as a staged index (one select per candidate),
                             // its tile-list position read from LDS once per chunk
@@ -383,16 +386,11 @@ __device__ __forceinline__ void feature_row_uniform(float (&row)[F4 * 4], const 
 }
 
 template <int NL, int F4>
-__device__ __forceinline__ int stage_candidates_p(WaveStageP<F4, fwd_sfeat<NL>()>& st, bool valid, uint32_t gid, int pos, int bx,
-                                                  int by, const float4* __restrict__ splatA,
-                                                  const float4* __restrict__ splatB, const float* __restrict__ rgb,
-                                                  const float* __restrict__ lang, int D)
+__device__ __forceinline__ int stage_candidates_p_rec(WaveStageP<F4, fwd_sfeat<NL>()>& st, bool valid, uint32_t gid,
+                                                      int pos, int bx, int by, float4 A, float4 B,
+                                                      const float* __restrict__ rgb, const float* __restrict__ lang,
+                                                      int D)
 {
-    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
-    if (valid) {
-        A = splatA[gid];
-        B = splatB[gid];
-    }
     const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by) &&
                     block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, bx, by);
     const uint64_t m = wave_ballot(ok);
@@ -416,6 +414,20 @@ __device__ __forceinline__ int stage_candidates_p(WaveStageP<F4, fwd_sfeat<NL>()
     }
     wave_lds_fence();
     return cnt;
+}
+
+template <int NL, int F4>
+__device__ __forceinline__ int stage_candidates_p(WaveStageP<F4, fwd_sfeat<NL>()>& st, bool valid, uint32_t gid, int pos, int bx,
+                                                  int by, const float4* __restrict__ splatA,
+                                                  const float4* __restrict__ splatB, const float* __restrict__ rgb,
+                                                  const float* __restrict__ lang, int D)
+{
+    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
+    if (valid) {
+        A = splatA[gid];
+        B = splatB[gid];
+    }
+    return stage_candidates_p_rec<NL, F4>(st, valid, gid, pos, bx, by, A, B, rgb, lang, D);
 }
 
 template <int NL>
@@ -447,16 +459,49 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
     bool done = !inside;
 
     uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
+#if LSR_FWD_PK && LSR_FWD_SPF
+    // SPF: a chunk's ids are loaded two chunks ahead and its records one chunk
+    // ahead, issued after the current chunk's feature loads: the staging then
+    // waits for one dependent gather (the feature rows) instead of two.
+    // Positions past the list read gid 0 (a valid record, never staged).
+    // (not with scalar feature rows, D >= LSR_FWD_SFEAT: cfg5 1.73 -> 1.82 ms)
+    constexpr bool FSPF = !SF;
+    uint32_t next_gid2 = 0u;
+    float4 A1 = make_float4(0.f, 0.f, 0.f, 0.f), B1 = A1;
+    if (FSPF && rs < re) {
+        next_gid2 = (rs + 64 + lane < re) ? a.point_list[rs + 64 + lane] : 0u;
+        A1 = a.splatA[next_gid];
+        B1 = a.splatB[next_gid];
+    }
+#endif
     for (uint32_t base = rs; base < re; base += 64) {
         if (wave_ballot(!done) == 0) break;
         const uint32_t idx = base + lane;
         const bool valid = idx < re;
         const uint32_t gid = next_gid;
+#if LSR_FWD_PK && LSR_FWD_SPF
+        int n;
+        if constexpr (FSPF) {
+            const float4 Ac = A1, Bc = B1;
+            n = stage_candidates_p_rec<NL, F4>(st, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, Ac, Bc, a.rgb,
+                                               a.lang, D);
+            next_gid = next_gid2;
+            A1 = a.splatA[next_gid];
+            B1 = a.splatB[next_gid];
+            const uint32_t q = min(idx + 128, re - 1);   // re > base: a valid position
+            const uint32_t v = a.point_list[q];
+            next_gid2 = idx + 128 < re ? v : 0u;
+        } else {
+            next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;
+            n = stage_candidates_p<NL, F4>(st, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, a.splatA, a.splatB,
+                                           a.rgb, a.lang, D);
+        }
+#elif LSR_FWD_PK
         next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;   // prefetch the next chunk's ids
-#if LSR_FWD_PK
         const int n = stage_candidates_p<NL, F4>(st, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, a.splatA,
                                                  a.splatB, a.rgb, a.lang, D);
 #else
+        next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;   // prefetch the next chunk's ids
         const int n = stage_candidates<NL, F4>(st, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, a.splatA, a.splatB,
                                                a.rgb, a.lang, D);
 #endif
