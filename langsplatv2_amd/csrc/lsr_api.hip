@@ -846,7 +846,9 @@ int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* 
     // D = 16 / 32 with dL/dlang requested: the render backward adds the
     // language gradients straight into the output; the rows keep geometry +
     // colour (one 64-B line) and preprocess_bwd no longer copies language
-    const bool lang_direct = Dd > 0 && out->dL_dlang && bwd_lang_direct(Dd);
+    // (and 16-B aligned language rows: the kernel gathers them as float4 lines)
+    const bool lang_direct = Dd > 0 && out->dL_dlang && bwd_lang_direct(Dd) &&
+                             (uintptr_t)in->language_feature_precomp % 16 == 0;
     const int VP = lang_direct ? 16 : grad_row_width(Dd);
     float* gacc = (float*)alloc(ctx, (size_t)P * VP * 4, LSR_BUF_GRAD);
     if (!gacc) return LSR_ENOMEM;

@@ -1600,6 +1600,9 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
 #ifndef LSR_BWD_RSCAT
 #define LSR_BWD_RSCAT 1     // bwd: phase-3 sums reduced two values per permlane swap, parked in LDS
 #endif
+#ifndef LSR_BWD_VEC_FEAT
+#define LSR_BWD_VEC_FEAT 1     // bwd, direct dL/dlang: feature rows gathered as float4 lines (dot_channel)
+#endif
 #ifndef LSR_BWD_ATOM_BATCH
 #define LSR_BWD_ATOM_BATCH 1   // bwd: the group's atomic values and ids read from LDS before any atomic issues
 #endif
@@ -1688,6 +1691,47 @@ __device__ __forceinline__ float feature_at(const RenderArgs& a, uint32_t gid, i
 #endif
 }
 
+// Channel of the dot product's K-step t in lane group lg.  Default: channel
+// 4t + lg.  VEC (whole 16-channel language rows, D = NL, rows 16-B aligned):
+// the K order follows the rows' float4 layout, so a candidate's features are
+// gathered with one 16-B load per 16-channel line and lane group (lane group
+// lg takes float4 lg of each line: K-steps 4r..4r+3 are line r's channels
+// 16r + 4lg + u) plus one load of its colour (the last K-step: channel lg,
+// lane group 3 none).  The dot is the same sum over channels in another order.
+template <int NL, bool VEC>
+__device__ __forceinline__ int dot_channel(int t, int lg)
+{
+    if constexpr (VEC) {
+        if (t < NL / 4) return 3 + 16 * (t >> 2) + 4 * lg + (t & 3);
+        return lg < 3 ? lg : 3 + NL;   // past the channels: 0
+    }
+    return 4 * t + lg;
+}
+
+// The dot product's A fragments of candidate gid for lane group lg, in
+// dot_channel order.
+template <int NL, bool VEC, int KS>
+__device__ __forceinline__ void dot_features(const RenderArgs& a, uint32_t gid, int lg, float (&af)[KS])
+{
+    if constexpr (VEC) {
+        static_assert(NL % 16 == 0 && KS == NL / 4 + 1, "VEC: whole 16-channel lines");
+        const float4* row = reinterpret_cast<const float4*>(a.lang) + (size_t)gid * (NL / 4) + lg;
+#pragma unroll
+        for (int r = 0; r < NL / 16; r++) {
+            const float4 v = row[4 * r];
+            af[4 * r + 0] = v.x;
+            af[4 * r + 1] = v.y;
+            af[4 * r + 2] = v.z;
+            af[4 * r + 3] = v.w;
+        }
+        const float c = a.rgb[3 * (size_t)gid + min(lg, 2)];
+        af[NL / 4] = lg < 3 ? c : 0.f;
+    } else {
+#pragma unroll
+        for (int t = 0; t < KS; t++) af[t] = feature_at<NL>(a, gid, 4 * t + lg);
+    }
+}
+
 #ifdef LSR_EXP_NOMF   // timing experiment only (wrong results): no matrix-core work
 #define BWD_MFMA(a, b_, c) (c)
 #else
@@ -1727,6 +1771,8 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     static_assert(!LD || (LSR_BWD_VMOM && !LO && NL % 16 == 0), "direct dL/dlang needs VMOM and whole 16-channel lines");
     using FR = BwdFrags<NL>;
     constexpr int KS = FR::KS;
+    // LD implies D == NL (launch_render_bwd) and 16-B aligned rows (lsr_api)
+    constexpr bool VEC = LD && LSR_BWD_VEC_FEAT;
 #if LSR_BWD_VMOM
     // MFMA channel blocks cover the language channels only; RGB (3) and the
     // six geometry moments are summed on the VALU (see phase 3)
@@ -1841,7 +1887,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #ifdef LSR_PROBE_NOPRO   // timing probe only (wrong results): no prologue dL/dout loads
                 dotB[t][pb] = (float)(t * 4 + pb + lane);
 #else
-                dotB[t][pb] = gd_at<NL>(b, 4 * t + lg, pb * 16 + li, pm.bx, pm.by);
+                dotB[t][pb] = gd_at<NL>(b, dot_channel<NL, VEC>(t, lg), pb * 16 + li, pm.bx, pm.by);
 #endif
     }
 #if LSR_BWD_VMOM
@@ -1924,12 +1970,11 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #endif
             if constexpr (!LO) {
                 const uint32_t gi = st.gid[g0 + (li < kn ? li : 0)];
-#pragma unroll
-                for (int t = 0; t < KS; t++)
 #ifdef LSR_PROBE_NOFEAT   // timing probe only (wrong results): no feature gather
-                    af[t] = __uint_as_float(gi) * 1e-30f;
+#pragma unroll
+                for (int t = 0; t < KS; t++) af[t] = __uint_as_float(gi) * 1e-30f;
 #else
-                    af[t] = feature_at<NL>(a, gi, 4 * t + lg);
+                dot_features<NL, VEC>(a, gi, lg, af);
 #endif
             }
             // phase 1: G of the 16 candidates (0 where the pair does not
@@ -2004,8 +2049,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             if (af_ready) {
                 const int kn2 = min(16, nfull - g0 - 16);
                 const uint32_t gi = st.gid[g0 + 16 + (li < kn2 ? li : 0)];
-#pragma unroll
-                for (int t = 0; t < KS; t++) af[t] = feature_at<NL>(a, gi, 4 * t + lg);
+                dot_features<NL, VEC>(a, gi, lg, af);
             }
 #endif
             wave_lds_fence();
@@ -2965,7 +3009,7 @@ hipError_t launch_render_bwd(const RenderBwdArgs& b, hipStream_t st)
     const int T = b.f.cam.gx * b.f.cam.gy;
     if (T == 0) return hipSuccess;
     if (b.lang_acc) {
-        if (!bwd_lang_direct(b.f.D)) return hipErrorInvalidValue;
+        if (!bwd_lang_direct(b.f.D) || (uintptr_t)b.f.lang % 16 != 0) return hipErrorInvalidValue;
 #if LSR_BWD_MF && LSR_BWD_VMOM
         if (b.f.D == 16) k_render_bwd_mf<16, false, true><<<4 * T, 64, 0, st>>>(b);
 #if LSR_BWD_MF_WIDE
