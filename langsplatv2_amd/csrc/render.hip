@@ -1600,6 +1600,10 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
 #ifndef LSR_BWD_RSCAT
 #define LSR_BWD_RSCAT 1     // bwd: phase-3 sums reduced two values per permlane swap, parked in LDS
 #endif
+#ifndef LSR_BWD_BUF_ATOM
+#define LSR_BWD_BUF_ATOM 1     // bwd: gradient atomics through raw buffer descriptors, masked by offset
+#endif
+#define LSR_BUF_OOB 0x7ffffffc  // a byte offset past every buffer the backward addresses this way
 #ifndef LSR_BWD_VEC_FEAT
 #define LSR_BWD_VEC_FEAT 1     // bwd, direct dL/dlang: feature rows gathered as float4 lines (dot_channel)
 #endif
@@ -1827,6 +1831,17 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     const int D = a.D;
     const int VP = b.VP;
     const float ddelx_dx = 0.5f * (float)c.W, ddely_dy = 0.5f * (float)c.H;
+#if LSR_BWD_BUF_ATOM
+    // gradient rows (and LD: the language output) as raw buffers when every
+    // byte offset fits 31 bits (uniform; otherwise 64-bit global atomics)
+    const uint64_t nbg = (uint64_t)a.P * (uint64_t)VP * 4u;
+    const uint64_t nbl = LD ? (uint64_t)a.P * (uint64_t)D * 4u : 0u;
+    const bool buf_atom = nbg < (uint64_t)LSR_BUF_OOB && nbl < (uint64_t)LSR_BUF_OOB;
+    const __amdgpu_buffer_rsrc_t rg =
+        __builtin_amdgcn_make_buffer_rsrc(b.grad_acc, 0, (int)min(nbg, (uint64_t)LSR_BUF_OOB), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+        LD ? b.lang_acc : b.grad_acc, 0, (int)min(LD ? nbl : nbg, (uint64_t)LSR_BUF_OOB), 0x00020000);
+#endif
 
     const float T_final = inside ? a.final_T[pix] : 0.f;
     const int last = inside ? (int)a.n_contrib[pix] : 0;
@@ -2320,6 +2335,33 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 for (int h = 0; h < GRL; h++)
 #pragma unroll
                     for (int q = 0; q < 4; q++) vq[h][q] = sGr[(4 * q + lg) * GRS + 16 * h + li];
+#if LSR_BWD_BUF_ATOM
+                if (buf_atom) {
+                    // buffer atomics: 32-bit offsets, and a lane with nothing
+                    // to add gets an offset past the buffer (the range check
+                    // drops it: tools/micro/buf_oob_atomic.hip) instead of an
+                    // exec-masked branch per atomic
+#pragma unroll
+                    for (int h = 0; h < GRL; h++) {
+                        const int f = 16 * h + li;
+                        const bool fcol = LO ? (f < D)
+                                          : LD ? (h == 0 ? (f < 9) : (f - 16 < D))
+                                               : ((f < 9) | ((f >= LSR_GROW_LANG) & (f < LSR_GROW_LANG + D)));
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const float v = vq[h][q];
+                            const bool on = fcol & (4 * q + lg < kn) & (v != 0.f);
+                            if (LD && h > 0) {
+                                const int off = (int)(gq[q] * (uint32_t)D + (uint32_t)(f - 16)) * 4;
+                                __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, rl, on ? off : LSR_BUF_OOB, 0, 0);
+                            } else {
+                                const int off = (int)(gq[q] * (uint32_t)VP + (uint32_t)f) * 4;
+                                __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, rg, on ? off : LSR_BUF_OOB, 0, 0);
+                            }
+                        }
+                    }
+                } else
+#endif
 #pragma unroll
                 for (int h = 0; h < GRL; h++) {
                     const int f = 16 * h + li;
