@@ -1600,6 +1600,9 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
 #ifndef LSR_BWD_RSCAT
 #define LSR_BWD_RSCAT 1     // bwd: phase-3 sums reduced two values per permlane swap, parked in LDS
 #endif
+#ifndef LSR_BWD_GREG
+#define LSR_BWD_GREG 1         // bwd: phase 1's G kept in VGPRs for phase 2 (no sAT round trip)
+#endif
 #ifndef LSR_BWD_BUF_ATOM
 #define LSR_BWD_BUF_ATOM 1     // bwd: gradient atomics through raw buffer descriptors, masked by offset
 #endif
@@ -2000,7 +2003,14 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             // as a lane mask (scalar ORs), not per-lane flags.
             uint64_t near_m = 0u;
             const int kn_u = __builtin_amdgcn_readfirstlane(kn);   // uniform: scalar compares below
+            // GREG: G stays in registers from phase 1 to phase 2 (no LDS round trip)
+            float Gr[16];
+            (void)Gr;
+#if LSR_BWD_GREG
+#pragma unroll
+#else
 #pragma unroll LSR_P1_UNROLL
+#endif
             for (int k = 0; k < 16; k++) {
                 const float4 A = st.A[g0 + k];
                 const float4 B = st.B[g0 + k];
@@ -2010,12 +2020,22 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 const float G = cj ? __builtin_amdgcn_exp2f(power * LSR_LOG2E) : 0.f;
                 const float d = fminf(0.99f, B.y * G) - (1.0f / 255.0f);
                 near_m |= lanes_abs_lt(d, 2e-8f);
+#if LSR_BWD_GREG
+                Gr[k] = d >= 0.f ? G : 0.f;
+#else
                 sAT[k * GS + lane] = d >= 0.f ? G : 0.f;
+#endif
             }
             if (near_m != 0u) {
                 // the 1/255 decision must be the forward's: lanes inside the fast
                 // exp's error band re-evaluate with the forward's exp (rare)
+#if LSR_BWD_GREG
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    if (k >= kn) break;
+#else
                 for (int k = 0; k < kn; k++) {
+#endif
                     const int j = g0 + k;
                     const float4 A = st.A[j];
                     const float4 B = st.B[j];
@@ -2025,7 +2045,11 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                     if (cj & (fabsf(af2 - (1.0f / 255.0f)) < 2e-8f)) {
                         const float G = expf_det(power);
                         const float alpha = fminf(0.99f, B.y * G);
+#if LSR_BWD_GREG
+                        Gr[k] = !(alpha < 1.0f / 255.0f) ? G : 0.f;
+#else
                         sAT[k * GS + lane] = !(alpha < 1.0f / 255.0f) ? G : 0.f;
+#endif
                     }
                 }
             }
@@ -2079,7 +2103,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 // transmittance only: aT_k = alpha_k T_k (T_k recovered back to front)
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
-                    const float G = sAT[k * GS + lane];
+                    const float G = LSR_BWD_GREG ? Gr[k] : sAT[k * GS + lane];
                     const float al = fminf(0.99f, st.B[g0 + k].y * G);
                     T = T * __builtin_amdgcn_rcpf(1.f - al);
                     sAT[k * GS + lane] = al * T;
@@ -2087,7 +2111,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             } else if (has_bg) {
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
-                    const float G = sAT[k * GS + lane];
+                    const float G = LSR_BWD_GREG ? Gr[k] : sAT[k * GS + lane];
                     const float dot = sDU[k * GS + lane];
                     const float al = fminf(0.99f, st.B[g0 + k].y * G);
                     const float om = 1.f - al;
@@ -2101,7 +2125,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             } else {
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
-                    const float G = sAT[k * GS + lane];
+                    const float G = LSR_BWD_GREG ? Gr[k] : sAT[k * GS + lane];
                     const float dot = sDU[k * GS + lane];
                     const float al = fminf(0.99f, st.B[g0 + k].y * G);
                     const float om = 1.f - al;
