@@ -1603,6 +1603,12 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
 #ifndef LSR_BWD_GREG
 #define LSR_BWD_GREG 1         // bwd: phase 1's G kept in VGPRs for phase 2 (no sAT round trip)
 #endif
+#ifndef LSR_BWD_ROWREG
+#define LSR_BWD_ROWREG 1       // bwd, direct dL/dlang: language atomics straight from the MFMA accumulators
+#endif
+#ifndef LSR_BWD_OPLANE
+#define LSR_BWD_OPLANE 1       // bwd: phase 2's opacities by v_readlane from one per-lane LDS read
+#endif
 #ifndef LSR_BWD_BUF_ATOM
 #define LSR_BWD_BUF_ATOM 1     // bwd: gradient atomics through raw buffer descriptors, masked by offset
 #endif
@@ -1780,6 +1786,10 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     constexpr int KS = FR::KS;
     // LD implies D == NL (launch_render_bwd) and 16-B aligned rows (lsr_api)
     constexpr bool VEC = LD && LSR_BWD_VEC_FEAT;
+    // RREG (direct dL/dlang): the language lines' atomics take their values
+    // straight from the MFMA accumulators, lane (li, lg) adding candidate
+    // 4 lg + q's channel li (the C layout), so those rows skip LDS
+    constexpr bool RREG = LD && LSR_BWD_ROWREG && LSR_BWD_ATOM_BATCH && LSR_BWD_VMOM;
 #if LSR_BWD_VMOM
     // MFMA channel blocks cover the language channels only; RGB (3) and the
     // six geometry moments are summed on the VALU (see phase 3)
@@ -2003,6 +2013,14 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             // as a lane mask (scalar ORs), not per-lane flags.
             uint64_t near_m = 0u;
             const int kn_u = __builtin_amdgcn_readfirstlane(kn);   // uniform: scalar compares below
+#if LSR_BWD_OPLANE
+            // candidate li's opacity in lane li: phase 2 takes candidate k's
+            // from lane k (v_readlane) instead of a broadcast LDS read per k
+            const int opl = __float_as_int(st.B[g0 + li].y);
+#define BWD_OP(k) __int_as_float(__builtin_amdgcn_readlane(opl, (k)))
+#else
+#define BWD_OP(k) st.B[g0 + (k)].y
+#endif
             // GREG: G stays in registers from phase 1 to phase 2 (no LDS round trip)
             float Gr[16];
             (void)Gr;
@@ -2104,7 +2122,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
                     const float G = LSR_BWD_GREG ? Gr[k] : sAT[k * GS + lane];
-                    const float al = fminf(0.99f, st.B[g0 + k].y * G);
+                    const float al = fminf(0.99f, BWD_OP(k) * G);
                     T = T * __builtin_amdgcn_rcpf(1.f - al);
                     sAT[k * GS + lane] = al * T;
                 }
@@ -2113,7 +2131,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 for (int k = 0; k < 16; k++) {
                     const float G = LSR_BWD_GREG ? Gr[k] : sAT[k * GS + lane];
                     const float dot = sDU[k * GS + lane];
-                    const float al = fminf(0.99f, st.B[g0 + k].y * G);
+                    const float al = fminf(0.99f, BWD_OP(k) * G);
                     const float om = 1.f - al;
                     const float rcp = __builtin_amdgcn_rcpf(om);
                     T = T * rcp;
@@ -2127,7 +2145,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 for (int k = 0; k < 16; k++) {
                     const float G = LSR_BWD_GREG ? Gr[k] : sAT[k * GS + lane];
                     const float dot = sDU[k * GS + lane];
-                    const float al = fminf(0.99f, st.B[g0 + k].y * G);
+                    const float al = fminf(0.99f, BWD_OP(k) * G);
                     const float om = 1.f - al;
                     T = T * __builtin_amdgcn_rcpf(om);
                     sDU[k * GS + lane] = ((dot - S) * T) * G;
@@ -2224,7 +2242,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             // line-coalesced atomics: each 16-lane group covers one 64-B line of
             // one Gaussian's row.  Language: lane holds slot 4*lg+r, channel nb*16+li.
 #pragma unroll
-            for (int nb = 0; nb < NBC; nb++) {
+            for (int nb = 0; nb < (RREG ? 0 : NBC); nb++) {
                 const int chn = nb * 16 + li;
                 if (chn < NL) {
 #pragma unroll
@@ -2353,12 +2371,21 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 // first (one wait), then the atomics issue back to back
                 uint32_t gq[4];
                 float vq[GRL][4];
+                // slot of the q-th atomic of this lane: 4q + lg, or (RREG) 4 lg + q
+                auto slot_of = [&](int q) { return RREG ? 4 * lg + q : 4 * q + lg; };
 #pragma unroll
-                for (int q = 0; q < 4; q++) gq[q] = st.gid[g0 + 4 * q + lg];
+                for (int q = 0; q < 4; q++) gq[q] = st.gid[g0 + slot_of(q)];
 #pragma unroll
                 for (int h = 0; h < GRL; h++)
 #pragma unroll
-                    for (int q = 0; q < 4; q++) vq[h][q] = sGr[(4 * q + lg) * GRS + 16 * h + li];
+                    for (int q = 0; q < 4; q++) {
+#if LSR_BWD_VMOM
+                        if (RREG && h > 0)
+                            vq[h][q] = ch[h - 1][q];
+                        else
+#endif
+                            vq[h][q] = sGr[slot_of(q) * GRS + 16 * h + li];
+                    }
 #if LSR_BWD_BUF_ATOM
                 if (buf_atom) {
                     // buffer atomics: 32-bit offsets, and a lane with nothing
@@ -2374,7 +2401,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #pragma unroll
                         for (int q = 0; q < 4; q++) {
                             const float v = vq[h][q];
-                            const bool on = fcol & (4 * q + lg < kn) & (v != 0.f);
+                            const bool on = fcol & (slot_of(q) < kn) & (v != 0.f);
                             if (LD && h > 0) {
                                 const int off = (int)(gq[q] * (uint32_t)D + (uint32_t)(f - 16)) * 4;
                                 __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, rl, on ? off : LSR_BUF_OOB, 0, 0);
@@ -2395,7 +2422,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #pragma unroll
                     for (int q = 0; q < 4; q++) {
                         const float v = vq[h][q];
-                        if (fcol & (4 * q + lg < kn) & (v != 0.f)) {
+                        if (fcol & (slot_of(q) < kn) & (v != 0.f)) {
                             if (LD && h > 0)
                                 LSR_MF_ATOMIC(b.lang_acc + (size_t)gq[q] * D + (f - 16), v);
                             else
