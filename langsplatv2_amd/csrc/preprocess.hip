@@ -40,21 +40,28 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
     uint32_t* tiles = (uint32_t*)(geom + L.tiles);
     uint32_t* clampm = (uint32_t*)(geom + L.clamped);
 
-    radii[i] = 0;
-    tiles[i] = 0;
-    clampm[i] = 0;
-    depth[i] = 0.f;
-    splatA[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    splatB[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (!in.colors_precomp) {
-        rgbo[3 * i + 0] = 0.f;
-        rgbo[3 * i + 1] = 0.f;
-        rgbo[3 * i + 2] = 0.f;
-    }
+    // every output is written exactly once: zeros on the invisible exits,
+    // the values on the visible path
+    auto invisible = [&]() {
+        radii[i] = 0;
+        tiles[i] = 0;
+        clampm[i] = 0;
+        depth[i] = 0.f;
+        splatA[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        splatB[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!in.colors_precomp) {
+            rgbo[3 * i + 0] = 0.f;
+            rgbo[3 * i + 1] = 0.f;
+            rgbo[3 * i + 2] = 0.f;
+        }
+    };
 
     const float mx = in.means3D[3 * i], my = in.means3D[3 * i + 1], mz = in.means3D[3 * i + 2];
     const float3 pv = xform43(c.view, mx, my, mz);
-    if (pv.z <= 0.2f) return;
+    if (pv.z <= 0.2f) {
+        invisible();
+        return;
+    }
     const float4 ph = xform44(c.proj, mx, my, mz);
     const float pw = 1.0f / (ph.w + 0.0000001f);
     const float ppx = ph.x * pw, ppy = ph.y * pw;
@@ -72,7 +79,10 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
     float a, b, cc;
     ewa_cov2D(e, cov, a, b, cc);
     const float det = a * cc - b * b;
-    if (det == 0.0f) return;
+    if (det == 0.0f) {
+        invisible();
+        return;
+    }
     const float det_inv = 1.f / det;
     const float mid = 0.5f * (a + cc);
     const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
@@ -82,7 +92,10 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
     int x0, y0, x1, y1;
     get_rect(px, py, r, c.gx, c.gy, x0, y0, x1, y1);
     const int area = (x1 - x0) * (y1 - y0);
-    if (area == 0 || r <= 0) return;
+    if (area == 0 || r <= 0) {
+        invisible();
+        return;
+    }
 
     if (!in.colors_precomp) {
         float dir[3], dor[3];
@@ -111,6 +124,8 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
             rgbo[3 * i + ch] = fmaxf(out[ch], 0.f);
         }
         clampm[i] = m;
+    } else {
+        clampm[i] = 0;
     }
     const float o = in.opacities[i];
     depth[i] = pv.z;
