@@ -1603,6 +1603,9 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
 #ifndef LSR_BWD_GREG
 #define LSR_BWD_GREG 1         // bwd: phase 1's G kept in VGPRs for phase 2 (no sAT round trip)
 #endif
+#ifndef LSR_BWD_GD_BUF
+#define LSR_BWD_GD_BUF 1       // bwd (VEC): dL/dout fragments by buffer loads, out-of-image pixels by offset
+#endif
 #ifndef LSR_BWD_ROWREG
 #define LSR_BWD_ROWREG 1       // bwd, direct dL/dlang: language atomics straight from the MFMA accumulators
 #endif
@@ -1907,6 +1910,45 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
         dr2 = gd_at<NL>(b, 2, lane, pm.bx, pm.by);
     }
     float dotB[KS][4], chB[NBA][16];
+#if LSR_BWD_GD_BUF
+    // VEC: the dL/dout fragments through raw buffer descriptors when every
+    // byte offset fits 31 bits (uniform): a fragment's offset is its
+    // channel's plane plus the pixel's, and a pixel outside the image gets an
+    // offset past both buffers (the load returns 0), so no clamps or selects
+    const uint64_t HW4 = (uint64_t)HW * 4u;
+    const bool gd_buf = VEC && HW4 * (uint64_t)(D > 3 ? D : 3) < 0x7fffffffull;
+    if (VEC && gd_buf) {
+        const __amdgpu_buffer_rsrc_t rcol = __builtin_amdgcn_make_buffer_rsrc((void*)b.dout_color, 0, (int)(HW4 * 3u), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rlng = __builtin_amdgcn_make_buffer_rsrc((void*)b.dout_lang, 0, (int)(HW4 * (uint64_t)D), 0x00020000);
+        const uint32_t hw4 = (uint32_t)HW4;
+        auto poff = [&](int q) -> uint32_t {
+            const int qx = pm.bx + (q & 7), qy = pm.by + (q >> 3);
+            return (qx < c.W && qy < c.H) ? (uint32_t)(qy * c.W + qx) * 4u : 0x80000000u;
+        };
+        auto ld = [&](__amdgpu_buffer_rsrc_t r, uint32_t off) {
+            return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+        };
+        uint32_t pa[4];
+#pragma unroll
+        for (int pb = 0; pb < 4; pb++) pa[pb] = poff(pb * 16 + li);
+#pragma unroll
+        for (int t = 0; t < KS; t++)
+#pragma unroll
+            for (int pb = 0; pb < 4; pb++) {
+                if (t < NL / 4) {
+                    const int chl = dot_channel<NL, VEC>(t, lg) - 3;   // a language channel
+                    dotB[t][pb] = ld(rlng, (uint32_t)chl * hw4 + pa[pb]);
+                } else {   // colour channel lg; lane group 3 none
+                    dotB[t][pb] = ld(rcol, lg < 3 ? (uint32_t)lg * hw4 + pa[pb] : 0x80000000u);
+                }
+            }
+#pragma unroll
+        for (int nb = 0; nb < NBC; nb++)
+#pragma unroll
+            for (int t = 0; t < 16; t++) chB[nb][t] = ld(rlng, (uint32_t)(nb * 16 + li) * hw4 + poff(4 * t + lg));
+    } else
+#endif
+    {
     if constexpr (!LO) {
 #pragma unroll
         for (int t = 0; t < KS; t++)
@@ -1928,6 +1970,9 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #else
             chB[nb][t] = gd_at<NL>(b, 3 + nb * 16 + li, 4 * t + lg, pm.bx, pm.by);
 #endif
+#endif
+    }
+#if LSR_BWD_VMOM
     // block-centred x of the pixels this lane's fragments cover: columns lg
     // (even K-steps) and 4 + lg (odd K-steps)
     const float lxe = (float)lg - 3.5f, lxo = (float)lg + 0.5f;
