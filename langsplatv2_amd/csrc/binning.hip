@@ -26,6 +26,9 @@
 #ifndef LSR_SCATTER_PROBE
 #define LSR_SCATTER_PROBE 0
 #endif
+#ifndef LSR_SORT_WAVE_MAX
+#define LSR_SORT_WAVE_MAX 1024  // largest tile sorted by one wave in registers (512, 1024 or 2048): cfg3 tile_sort 0.079 -> 0.073 ms at 1024
+#endif
 #ifndef LSR_SORT_DPP
 #define LSR_SORT_DPP 1
 #endif
@@ -159,7 +162,7 @@ hipError_t launch_publish_total(const uint64_t* total, uint32_t* tile_end, uint6
 __device__ __forceinline__ int tile_class(int n)
 {
     if (n <= 0) return -1;
-    if (n <= 512) return 0;
+    if (n <= LSR_SORT_WAVE_MAX) return 0;
     if (n <= 1024) return 1;
     if (n <= 2048) return 2;
     if (n <= 4096) return 3;
@@ -957,7 +960,9 @@ __global__ void __launch_bounds__(256) k_tile_sort_wave(int T, const uint32_t* _
         } else if (n <= 64) wave_sort_tile<1>(g, o, n);
         else if (n <= 128) wave_sort_tile<2>(g, o, n);
         else if (n <= 256) wave_sort_tile<4>(g, o, n);
-        else wave_sort_tile<8>(g, o, n);
+        else if (LSR_SORT_WAVE_MAX <= 512 || n <= 512) wave_sort_tile<8>(g, o, n);
+        else if (LSR_SORT_WAVE_MAX <= 1024 || n <= 1024) wave_sort_tile<16>(g, o, n);
+        else wave_sort_tile<32>(g, o, n);
     }
 }
 
