@@ -9,7 +9,7 @@
 //    k_duplicate / k_scatter pair with one global atomic per instance remains
 //    as the fallback when T does not fit LDS.)
 //  - per-tile sort of the bucket's unique u64 keys (depth bits << 32 | id):
-//    one wave per tile with the keys in registers (k_tile_sort_wave, n <= 2048);
+//    one wave per tile with the keys in registers (k_tile_sort_wave, n <= 1024);
 //    a workgroup in LDS for n <= 4096, chunked LDS + global merge above.
 // The result equals a stable sort by (tile, depth bits) with ties broken by
 // Gaussian id — the order of the reference's stable radix sort over
