@@ -26,6 +26,9 @@
 #ifndef LSR_SCATTER_PROBE
 #define LSR_SCATTER_PROBE 0
 #endif
+#ifndef LSR_BIN_TARGET
+#define LSR_BIN_TARGET 512   // (chunk x band) blocks of the privatised count / scatter
+#endif
 #ifndef LSR_SORT_WAVE_MAX
 #define LSR_SORT_WAVE_MAX 1024  // largest tile sorted by one wave in registers (512, 1024 or 2048): cfg3 tile_sort 0.079 -> 0.073 ms at 1024
 #endif
@@ -554,7 +557,10 @@ int bin_blocks(int P, const Cam& c, int& chunk)
     // chunks when there are several bands keeps the B x T table small
     const int rows = bin_band_rows(c);
     const int S = (c.gy + rows - 1) / rows;
-    const int target = std::max(64, 512 / S);
+    // twice the blocks from 4M Gaussians up: cfg5 (5M) bin_scatter 1.20 ->
+    // 1.02 ms; at cfg3 (1M) 1024 blocks make the count + table pass slower
+    const int total = P >= (4 << 20) ? 2 * LSR_BIN_TARGET : LSR_BIN_TARGET;
+    const int target = std::max(64, total / S);
     chunk = max(1024, (P + target - 1) / target);
     chunk = (chunk + BIN_BLOCK - 1) / BIN_BLOCK * BIN_BLOCK;
     return (P + chunk - 1) / chunk;
