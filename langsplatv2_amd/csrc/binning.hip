@@ -284,11 +284,14 @@ hipError_t launch_scatter(const Cam& c, int P, const uint8_t* geom, const int32_
 #ifndef LSR_BAND_LDS
 #define LSR_BAND_LDS 32768
 #endif
+#ifndef LSR_COUNT_XCD
+#define LSR_COUNT_XCD 1   // chunk-major count grid: cfg5 bin_count 0.627 -> 0.604 ms (cfg3 ±0)
+#endif
 struct Band {
     int ty0, ty1, t0, nt;
-    __device__ Band(const Cam& c, int rows)
+    __device__ Band(const Cam& c, int rows, int band)
     {
-        ty0 = blockIdx.y * rows;
+        ty0 = band * rows;
         ty1 = min(c.gy, ty0 + rows);
         t0 = ty0 * c.gx;
         nt = (ty1 - ty0) * c.gx;
@@ -400,7 +403,7 @@ __device__ __forceinline__ int band_rect(const Cam& c, const Band& bd, const uin
     return (y1 > y0 && w > 0) ? w * (y1 - y0) : 0;
 }
 
-__global__ void __launch_bounds__(BIN_BLOCK) k_bin_count(Cam c, int P, int chunk, int rows,
+__global__ void __launch_bounds__(BIN_BLOCK) k_bin_count(Cam c, int P, int chunk, int rows, int S,
                                                          const uint8_t* __restrict__ geom,
                                                          const int32_t* __restrict__ radii, uint32_t* __restrict__ table,
                                                          uint32_t* __restrict__ cls_cnt)
@@ -408,13 +411,21 @@ __global__ void __launch_bounds__(BIN_BLOCK) k_bin_count(Cam c, int P, int chunk
     extern __shared__ uint32_t hist[];
     __shared__ WaveRects wrs[BIN_BLOCK / 64];
     const int T = c.gx * c.gy;
-    const Band bd(c, rows);
+#if LSR_COUNT_XCD
+    // chunk-major, XCD-aware (as k_bin_scatter): a chunk's bands share an L2
+    const int o = xcd_remap(blockIdx.x, gridDim.x);
+    const int blk = o / S;
+    const Band bd(c, rows, o - blk * S);
+#else
+    const int blk = blockIdx.x;
+    const Band bd(c, rows, blockIdx.y);
+#endif
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < SORT_NCLS) cls_cnt[threadIdx.x] = 0;   // k_bin_table appends after us
     for (int k = threadIdx.x; k < bd.nt; k += BIN_BLOCK) hist[k] = 0;
     __syncthreads();
     WaveRects& wr = wrs[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
-    const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
+    const int g0 = blk * chunk, g1 = min(P, g0 + chunk);
     for (int i0 = g0 + (threadIdx.x & ~63); i0 < g1; i0 += BIN_BLOCK) {
         int x0, y0, w;
         float4 A, B;
@@ -434,7 +445,7 @@ __global__ void __launch_bounds__(BIN_BLOCK) k_bin_count(Cam c, int P, int chunk
         wave_lds_fence();
     }
     __syncthreads();
-    uint32_t* row = table + (size_t)blockIdx.x * T + bd.t0;
+    uint32_t* row = table + (size_t)blk * T + bd.t0;
     for (int k = threadIdx.x; k < bd.nt; k += BIN_BLOCK) row[k] = hist[k];
 }
 
@@ -483,7 +494,13 @@ __global__ void __launch_bounds__(256) k_bin_table(int T, int B, uint32_t* __res
     }
 }
 
-__global__ void __launch_bounds__(BIN_BLOCK) k_bin_scatter(Cam c, int P, int chunk, int rows,
+// The scatter's bands are its own (rows of its own, not the count's): the
+// table row of (chunk, tile) does not depend on how tiles are grouped.  The
+// 1-D grid is chunk-major and XCD-aware (xcd_remap): the S bands of one chunk
+// run back to back on one XCD, so a chunk's geometry is read from that XCD's
+// L2 and the partial key lines the XCD has open at once span ~one chunk's
+// tiles instead of one per resident block.
+__global__ void __launch_bounds__(BIN_BLOCK) k_bin_scatter(Cam c, int P, int chunk, int rows, int S,
                                                            const uint8_t* __restrict__ geom,
                                                            const int32_t* __restrict__ radii,
                                                            const uint32_t* __restrict__ table,
@@ -493,15 +510,17 @@ __global__ void __launch_bounds__(BIN_BLOCK) k_bin_scatter(Cam c, int P, int chu
     extern __shared__ uint32_t base[];
     __shared__ WaveRects wrs[BIN_BLOCK / 64];
     const int T = c.gx * c.gy;
-    const Band bd(c, rows);
-    const uint32_t* row = table + (size_t)blockIdx.x * T + bd.t0;
+    const int o = xcd_remap(blockIdx.x, gridDim.x);
+    const int blk = o / S;
+    const Band bd(c, rows, o - blk * S);
+    const uint32_t* row = table + (size_t)blk * T + bd.t0;
     for (int k = threadIdx.x; k < bd.nt; k += BIN_BLOCK) base[k] = tile_start[bd.t0 + k] + row[k];
     __syncthreads();
     const GeomLayout L = geom_layout(P);
     const float* depth = (const float*)(geom + L.depth);
     WaveRects& wr = wrs[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
-    const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
+    const int g0 = blk * chunk, g1 = min(P, g0 + chunk);
     for (int i0 = g0 + (threadIdx.x & ~63); i0 < g1; i0 += BIN_BLOCK) {
         const int i = i0 + lane;
         int x0, y0, w;
@@ -551,6 +570,17 @@ static int bin_band_rows(const Cam& c)
     return std::max(1, std::min(c.gy, LSR_BAND_LDS / (4 * c.gx)));
 }
 
+// Tile rows per scatter band: the largest band whose LDS bases fit
+// LSR_SCATTER_LDS bytes (narrower bands than the count's measured slower:
+// every band re-walks its chunk).
+#ifndef LSR_SCATTER_LDS
+#define LSR_SCATTER_LDS LSR_BAND_LDS
+#endif
+static int bin_scatter_rows(const Cam& c)
+{
+    return std::max(1, std::min(c.gy, LSR_SCATTER_LDS / (4 * c.gx)));
+}
+
 int bin_blocks(int P, const Cam& c, int& chunk)
 {
     // ~512 (chunk x band) blocks, 2 per CU, of >= 1024 Gaussians; fewer
@@ -576,14 +606,15 @@ hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t
 {
     const int T = c.gx * c.gy;
     const int rows = bin_band_rows(c);
-    const dim3 grid(B, (c.gy + rows - 1) / rows);
+    const int S = (c.gy + rows - 1) / rows;
+    const dim3 grid(LSR_COUNT_XCD ? B * S : B, LSR_COUNT_XCD ? 1 : S);
     const size_t lds = (size_t)rows * c.gx * 4;
     if (lds > 65536) {
         (void)hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         (void)hipFuncSetAttribute((const void*)k_bin_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
     if (B > 0) {
-        k_bin_count<<<grid, BIN_BLOCK, lds, st>>>(c, P, chunk, rows, geom, radii, table, cls_cnt);
+        k_bin_count<<<grid, BIN_BLOCK, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt);
         k_bin_table<<<(T + TBL_COLS - 1) / TBL_COLS, 256, 0, st>>>(T, B, table, tile_cnt, cls_cnt, cls_list);
     } else {
         (void)hipMemsetAsync(tile_cnt, 0, (size_t)T * 4, st);
@@ -595,11 +626,14 @@ hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t
 hipError_t launch_bin_scatter(const Cam& c, int P, int chunk, int B, const uint8_t* geom, const int32_t* radii,
                               const uint32_t* table, const uint32_t* tile_start, uint64_t* keys, hipStream_t st)
 {
-    const int rows = bin_band_rows(c);
-    const dim3 grid(B, (c.gy + rows - 1) / rows);
+    const int rows = bin_scatter_rows(c);
+    const int S = (c.gy + rows - 1) / rows;
+    const size_t lds = (size_t)rows * c.gx * 4;
+    if (lds > 65536)
+        (void)hipFuncSetAttribute((const void*)k_bin_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (B > 0)
-        k_bin_scatter<<<grid, BIN_BLOCK, (size_t)rows * c.gx * 4, st>>>(c, P, chunk, rows, geom, radii, table,
-                                                                       tile_start, keys);
+        k_bin_scatter<<<B * S, BIN_BLOCK, (size_t)rows * c.gx * 4, st>>>(c, P, chunk, rows, S, geom, radii, table,
+                                                                        tile_start, keys);
     return hipGetLastError();
 }
 

@@ -221,5 +221,124 @@ def accumulate_views(gs: GaussianState, opt, cams: list, gts: list, bg: torch.Te
     return losses
 
 
+# ----------------------------------------------------------- feature phase ---
+# The language-feature phase (BASELINE.json cfg4's step; train.py:139-173 with
+# --include_feature --cos_loss, vq_layer_num 1 as the paper and train.sh use):
+# geometry frozen, the trainable parameters are the per-Gaussian code logits
+# (N, 64) and the codebooks (1, 64, Df) (scene/gaussian_model.py:238-243), the
+# render weights are the top-k soft codes (get_render_weights,
+# scene/gaussian_model.py:510-518 -> the fused producer), the loss is the cosine
+# loss of the decoded feature map against the view's ground truth under its
+# mask (train.py:151-166 -> the fused loss, which never forms the Df-wide map).
+# No densification in this phase (train.py:245: `if not opt.include_feature`).
+
+LANG_PARAM_NAMES = ("logits", "codebooks")
+
+
+class LanguageState:
+    """Frozen geometry + the trainable language parameters, Adam groups as
+    training_setup with include_feature (lr 0.0025 on both, eps 1e-15)."""
+
+    def __init__(self, means3D, shs, opacities, scales, rotations, logits, codebooks, topk: int = 4):
+        self.geo = {"means3D": means3D.detach(), "shs": shs.detach(), "opacities": opacities.detach(),
+                    "scales": scales.detach(), "rotations": rotations.detach()}
+        self.logits = logits.detach().clone().contiguous().requires_grad_(True)
+        self.codebooks = codebooks.detach().clone().contiguous().requires_grad_(True)
+        if self.codebooks.dim() != 3 or self.codebooks.shape[0] != 1:
+            raise ValueError("LanguageState: codebooks must be (1, K, Df): vq_layer_num 1 (the paper's setting)")
+        self.topk = topk
+        self.active_sh_degree = 3
+
+    def params(self):
+        return [self.logits, self.codebooks]
+
+    def optimizer(self, fused: bool = True):
+        groups = [{"params": [self.logits, self.codebooks], "lr": 0.0025, "name": "language_feature"}]
+        if fused:
+            return FusedAdam(groups, lr=0.0, eps=1e-15)
+        return torch.optim.Adam(groups, lr=0.0, eps=1e-15)
+
+
+def render_language(cam: dict, ls: LanguageState, bg: torch.Tensor) -> dict:
+    """gaussian_renderer/__init__.py:19-129 for include_feature = True: dense
+    top-k render weights, (1,) placeholders for the quick inputs, screen-space
+    points `zeros_like(xyz, requires_grad=True) + 0` with retain_grad."""
+    from . import lang_codes
+    xyz = ls.geo["means3D"]
+    dev = xyz.device
+    screenspace_points = torch.zeros_like(xyz, requires_grad=True) + 0
+    screenspace_points.retain_grad()
+    K = ls.codebooks.shape[1]
+    weights = lang_codes.get_render_weights(ls.logits, 1, K, ls.topk)
+    placeholder = torch.zeros((1,), dtype=xyz.dtype, device=dev)
+    rs = GaussianRasterizationSettings(
+        image_height=cam["H"], image_width=cam["W"], tanfovx=cam["tanfovx"], tanfovy=cam["tanfovy"], bg=bg,
+        scale_modifier=1.0, viewmatrix=cam["viewmatrix"].to(dev), projmatrix=cam["projmatrix"].to(dev),
+        sh_degree=ls.active_sh_degree, campos=cam["campos"].to(dev), prefiltered=False, debug=False,
+        include_feature=True)
+    image, weight_map, radii = GaussianRasterizer(rs)(
+        means3D=xyz, means2D=screenspace_points, shs=ls.geo["shs"], colors_precomp=None,
+        language_feature_precomp=weights, language_feature_weights_quick=placeholder,
+        language_feature_indices=placeholder, opacities=ls.geo["opacities"], scales=ls.geo["scales"],
+        rotations=ls.geo["rotations"], cov3D_precomp=None)
+    return {"render": image, "language_feature_weight_map": weight_map, "viewspace_points": screenspace_points,
+            "radii": radii}
+
+
+def language_view_loss(pkg: dict, ls: LanguageState, seg: torch.Tensor, features: torch.Tensor) -> torch.Tensor:
+    """train.py:151-166 with --cos_loss: 1 - cos(CB^T W * mask, gt * mask), the
+    ground truth gathered from the view's (S, Df) table by its segment map."""
+    from .lang_loss import language_cos_loss
+    return language_cos_loss(pkg["language_feature_weight_map"], ls.codebooks, seg, features)
+
+
+class LanguageTrainer:
+    """One optimizer step per call in the feature phase: this rank renders its
+    view, the exchange sums the R ranks' (logits, codebooks) gradients in one
+    bucket, every rank steps its replica (= --accum_iter R on one GPU)."""
+
+    def __init__(self, ls: LanguageState, bg: torch.Tensor, group=None, fused_adam: bool = True):
+        self.ls = ls
+        self.bg = bg
+        self.opt = ls.optimizer(fused=fused_adam)
+        self.exchange = dp.ViewShardedExchange(ls.params(), with_stats=False, group=group,
+                                               names=list(LANG_PARAM_NAMES))
+        self.world = self.exchange.world
+        self.iteration = 0
+
+    def step(self, cam: dict, seg: torch.Tensor, features: torch.Tensor) -> float:
+        pkg = render_language(cam, self.ls, self.bg)
+        loss = language_view_loss(pkg, self.ls, seg, features)
+        loss.backward()
+        params = self.ls.params()
+        grads, _, _ = self.exchange.exchange([p.grad for p in params])
+        self.last_grads = grads   # views of the reduced bucket (valid until the next step)
+        for p, g in zip(params, grads):
+            p.grad = g
+        self.opt.step()
+        self.opt.zero_grad(set_to_none=True)
+        self.iteration += self.world
+        return float(loss.detach())
+
+
+def accumulate_language_views(ls: LanguageState, opt, cams: list, segs: list, feats: list, bg: torch.Tensor,
+                              grads_out: list | None = None):
+    """Single-GPU reference of one feature-phase DP step: len(cams) iterations
+    with accum_iter = len(cams) (train.py:261-263), one optimizer step
+    (`grads_out` receives copies of the accumulated gradients it steps with)."""
+    losses = []
+    for cam, seg, feat in zip(cams, segs, feats):
+        pkg = render_language(cam, ls, bg)
+        loss = language_view_loss(pkg, ls, seg, feat)
+        loss.backward()
+        losses.append(float(loss.detach()))
+    if grads_out is not None:
+        grads_out[:] = [p.grad.detach().clone() for p in ls.params()]
+    opt.step()
+    opt.zero_grad(set_to_none=True)
+    return losses
+
+
 __all__ = ["GaussianState", "render_rgb", "sh_ramp", "l1_loss", "ssim", "view_loss", "apply_view_stats", "RGBTrainer",
-           "accumulate_views", "PARAM_NAMES"]
+           "accumulate_views", "PARAM_NAMES", "LanguageState", "render_language", "language_view_loss",
+           "LanguageTrainer", "accumulate_language_views", "LANG_PARAM_NAMES"]
