@@ -565,9 +565,16 @@ __global__ void __launch_bounds__(BIN_BLOCK) k_bin_scatter(Cam c, int P, int chu
 }
 
 // Tile rows per band: the largest band whose histogram fits LSR_BAND_LDS.
+// At most LSR_BAND_ROWS rows: at cfg3 (68 tile rows) two bands of 34 halve
+// the chunk count for the same ~512 blocks — a smaller B x T table and longer
+// per-(chunk, tile) key runs: bin_count 0.0756 -> 0.0691 ms, scatter +0.002 (r02
+// A/B; cfg2 count -10 %; cfg5 already has 34-row bands, 24 / 17 were slower).
+#ifndef LSR_BAND_ROWS
+#define LSR_BAND_ROWS 34
+#endif
 static int bin_band_rows(const Cam& c)
 {
-    return std::max(1, std::min(c.gy, LSR_BAND_LDS / (4 * c.gx)));
+    return std::max(1, std::min(std::min(c.gy, LSR_BAND_ROWS), LSR_BAND_LDS / (4 * c.gx)));
 }
 
 // Tile rows per scatter band: the largest band whose LDS bases fit
