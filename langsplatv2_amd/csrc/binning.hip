@@ -272,11 +272,9 @@ hipError_t launch_scatter(const Cam& c, int P, const uint8_t* geom, const int32_
 // re-walks the chunk and places every instance at tile_start + block base +
 // LDS-atomic rank.  No global atomics; the in-bucket order is arbitrary and
 // fixed by the per-tile sort.
-#ifndef BIN_BLOCK
-#define BIN_BLOCK 512   // 8 waves per (chunk, band) block: bin_count 0.097 -> 0.077 ms at cfg3 with the tile cull (A/B)
-#endif
 
-// Screen bands: blockIdx.y = band of `rows` tile rows, so a block's LDS
+
+// Screen bands: each block owns a band of `rows` tile rows, so a block's LDS
 // histogram covers rows * gx tiles (<= LSR_BAND_LDS bytes) and several blocks
 // stay resident per CU at any resolution; a Gaussian's rect is clipped to the
 // band (each band re-reads the chunk's 20-B records, cheap next to the
@@ -403,13 +401,14 @@ __device__ __forceinline__ int band_rect(const Cam& c, const Band& bd, const uin
     return (y1 > y0 && w > 0) ? w * (y1 - y0) : 0;
 }
 
-__global__ void __launch_bounds__(BIN_BLOCK) k_bin_count(Cam c, int P, int chunk, int rows, int S,
+template <int BB>
+__global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int rows, int S,
                                                          const uint8_t* __restrict__ geom,
                                                          const int32_t* __restrict__ radii, uint32_t* __restrict__ table,
                                                          uint32_t* __restrict__ cls_cnt)
 {
     extern __shared__ uint32_t hist[];
-    __shared__ WaveRects wrs[BIN_BLOCK / 64];
+    __shared__ WaveRects wrs[BB / 64];
     const int T = c.gx * c.gy;
 #if LSR_COUNT_XCD
     // chunk-major, XCD-aware (as k_bin_scatter): a chunk's bands share an L2
@@ -421,12 +420,12 @@ __global__ void __launch_bounds__(BIN_BLOCK) k_bin_count(Cam c, int P, int chunk
     const Band bd(c, rows, blockIdx.y);
 #endif
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < SORT_NCLS) cls_cnt[threadIdx.x] = 0;   // k_bin_table appends after us
-    for (int k = threadIdx.x; k < bd.nt; k += BIN_BLOCK) hist[k] = 0;
+    for (int k = threadIdx.x; k < bd.nt; k += BB) hist[k] = 0;
     __syncthreads();
     WaveRects& wr = wrs[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     const int g0 = blk * chunk, g1 = min(P, g0 + chunk);
-    for (int i0 = g0 + (threadIdx.x & ~63); i0 < g1; i0 += BIN_BLOCK) {
+    for (int i0 = g0 + (threadIdx.x & ~63); i0 < g1; i0 += BB) {
         int x0, y0, w;
         float4 A, B;
         const int n = band_rect(c, bd, geom, P, g1, radii, i0 + lane, x0, y0, w, A, B);
@@ -446,7 +445,7 @@ __global__ void __launch_bounds__(BIN_BLOCK) k_bin_count(Cam c, int P, int chunk
     }
     __syncthreads();
     uint32_t* row = table + (size_t)blk * T + bd.t0;
-    for (int k = threadIdx.x; k < bd.nt; k += BIN_BLOCK) row[k] = hist[k];
+    for (int k = threadIdx.x; k < bd.nt; k += BB) row[k] = hist[k];
 }
 
 // Column scan: table[b][t] <- sum_{b' < b} table[b'][t]; tile_cnt[t] <- total.
@@ -500,7 +499,8 @@ __global__ void __launch_bounds__(256) k_bin_table(int T, int B, uint32_t* __res
 // run back to back on one XCD, so a chunk's geometry is read from that XCD's
 // L2 and the partial key lines the XCD has open at once span ~one chunk's
 // tiles instead of one per resident block.
-__global__ void __launch_bounds__(BIN_BLOCK) k_bin_scatter(Cam c, int P, int chunk, int rows, int S,
+template <int BB>
+__global__ void __launch_bounds__(BB) k_bin_scatter(Cam c, int P, int chunk, int rows, int S,
                                                            const uint8_t* __restrict__ geom,
                                                            const int32_t* __restrict__ radii,
                                                            const uint32_t* __restrict__ table,
@@ -508,20 +508,20 @@ __global__ void __launch_bounds__(BIN_BLOCK) k_bin_scatter(Cam c, int P, int chu
                                                            uint64_t* __restrict__ keys)
 {
     extern __shared__ uint32_t base[];
-    __shared__ WaveRects wrs[BIN_BLOCK / 64];
+    __shared__ WaveRects wrs[BB / 64];
     const int T = c.gx * c.gy;
     const int o = xcd_remap(blockIdx.x, gridDim.x);
     const int blk = o / S;
     const Band bd(c, rows, o - blk * S);
     const uint32_t* row = table + (size_t)blk * T + bd.t0;
-    for (int k = threadIdx.x; k < bd.nt; k += BIN_BLOCK) base[k] = tile_start[bd.t0 + k] + row[k];
+    for (int k = threadIdx.x; k < bd.nt; k += BB) base[k] = tile_start[bd.t0 + k] + row[k];
     __syncthreads();
     const GeomLayout L = geom_layout(P);
     const float* depth = (const float*)(geom + L.depth);
     WaveRects& wr = wrs[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     const int g0 = blk * chunk, g1 = min(P, g0 + chunk);
-    for (int i0 = g0 + (threadIdx.x & ~63); i0 < g1; i0 += BIN_BLOCK) {
+    for (int i0 = g0 + (threadIdx.x & ~63); i0 < g1; i0 += BB) {
         const int i = i0 + lane;
         int x0, y0, w;
         float4 A, B;
@@ -588,6 +588,12 @@ static int bin_scatter_rows(const Cam& c)
     return std::max(1, std::min(c.gy, LSR_SCATTER_LDS / (4 * c.gx)));
 }
 
+// Threads per (chunk, band) block: 16 waves below 4M Gaussians (cfg3
+// bin_count 0.070 -> 0.061 ms: the LDS histogram's clear and flush loops
+// halve), 8 waves from 4M up (16 measured slower at cfg5: count 0.60 -> 0.66,
+// scatter 0.98 -> 1.11 ms).
+static int bin_block(int P) { return P >= (4 << 20) ? 512 : 1024; }
+
 int bin_blocks(int P, const Cam& c, int& chunk)
 {
     // ~512 (chunk x band) blocks, 2 per CU, of >= 1024 Gaussians; fewer
@@ -599,7 +605,8 @@ int bin_blocks(int P, const Cam& c, int& chunk)
     const int total = P >= (4 << 20) ? 2 * LSR_BIN_TARGET : LSR_BIN_TARGET;
     const int target = std::max(64, total / S);
     chunk = max(1024, (P + target - 1) / target);
-    chunk = (chunk + BIN_BLOCK - 1) / BIN_BLOCK * BIN_BLOCK;
+    const int bb = bin_block(P);
+    chunk = (chunk + bb - 1) / bb * bb;
     return (P + chunk - 1) / chunk;
 }
 
@@ -617,11 +624,16 @@ hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t
     const dim3 grid(LSR_COUNT_XCD ? B * S : B, LSR_COUNT_XCD ? 1 : S);
     const size_t lds = (size_t)rows * c.gx * 4;
     if (lds > 65536) {
-        (void)hipFuncSetAttribute((const void*)k_bin_count, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        (void)hipFuncSetAttribute((const void*)k_bin_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)k_bin_count<512>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)k_bin_count<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)k_bin_scatter<512>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)k_bin_scatter<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
     if (B > 0) {
-        k_bin_count<<<grid, BIN_BLOCK, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt);
+        if (bin_block(P) == 1024)
+            k_bin_count<1024><<<grid, 1024, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt);
+        else
+            k_bin_count<512><<<grid, 512, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt);
         k_bin_table<<<(T + TBL_COLS - 1) / TBL_COLS, 256, 0, st>>>(T, B, table, tile_cnt, cls_cnt, cls_list);
     } else {
         (void)hipMemsetAsync(tile_cnt, 0, (size_t)T * 4, st);
@@ -636,11 +648,14 @@ hipError_t launch_bin_scatter(const Cam& c, int P, int chunk, int B, const uint8
     const int rows = bin_scatter_rows(c);
     const int S = (c.gy + rows - 1) / rows;
     const size_t lds = (size_t)rows * c.gx * 4;
-    if (lds > 65536)
-        (void)hipFuncSetAttribute((const void*)k_bin_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (B > 0)
-        k_bin_scatter<<<B * S, BIN_BLOCK, (size_t)rows * c.gx * 4, st>>>(c, P, chunk, rows, S, geom, radii, table,
-                                                                        tile_start, keys);
+    if (lds > 65536) {
+        (void)hipFuncSetAttribute((const void*)k_bin_scatter<512>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)k_bin_scatter<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    }
+    if (B > 0 && bin_block(P) == 1024)
+        k_bin_scatter<1024><<<B * S, 1024, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, tile_start, keys);
+    else if (B > 0)
+        k_bin_scatter<512><<<B * S, 512, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, tile_start, keys);
     return hipGetLastError();
 }
 
