@@ -253,18 +253,127 @@ def self_launch(args) -> int:
     return subprocess.call(cmd, env=env)
 
 
-def dry_run(world, rank) -> int:
-    """Rank bring-up only (gloo, no GPU): every rank reports (rank, world size) to rank 0."""
+def dry_run(world, rank, config=3) -> int:
+    """Rank bring-up only (gloo, no GPU): every rank reports (rank, world size, its view's
+    yaw) to rank 0."""
+    yaw = dp.rank_yaw(rank, world)
     if world > 1:
         dist.init_process_group("gloo")
         seen = [None] * world
-        dist.all_gather_object(seen, (rank, dist.get_world_size()))
+        dist.all_gather_object(seen, (rank, dist.get_world_size(), yaw))
         dist.destroy_process_group()
     else:
-        seen = [(0, 1)]
+        seen = [(0, 1, yaw)]
     if rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": sorted(r for r, _ in seen),
-                          "world_sizes_seen": sorted({w for _, w in seen})}), flush=True)
+        print(json.dumps({"dry_run": True, "n_gpus": world, "config": config,
+                          "mode": CONFIG_MODES[config], "ranks": sorted(r for r, _, _ in seen),
+                          "world_sizes_seen": sorted({w for _, w, _ in seen}),
+                          "yaws": [y for _, _, y in sorted(seen)]}), flush=True)
+    return 0
+
+
+# --config 3: the headline (BASELINE metric) — fwd+bwd, views sharded, RCCL gradient exchange.
+# --config 5: BASELINE configs[4] — forward only, replicas only (every rank renders its own
+#             view of the replicated 5M-Gaussian scene; no data-path collective, SURVEY §8e).
+CONFIG_MODES = {3: "fwd+bwd, views sharded + RCCL all-reduce of gradients",
+                5: "forward only, replicas (no collective)"}
+
+
+def main_forward_replicas(args, world, rank, dev) -> int:
+    """BASELINE configs[4]: 5M Gaussians, 3840x2160, SH degree 3 + 32 dense language
+    channels, forward only; one view per rank (yaw within +-20 degrees), Gaussians replicated,
+    nothing exchanged.  value = frames rendered by all ranks / max-over-ranks time."""
+    cfg = CONFIGS[args.config]
+    N, W, H, D, deg = cfg["N"], cfg["W"], cfg["H"], cfg["lang_dim"], cfg["sh_degree"]
+    yaw = dp.rank_yaw(rank, world)
+    cam0 = make_camera(W, H)
+    cam = make_camera(W, H, yaw_deg=yaw)
+    gcpu = make_gaussians(N, cam0, seed=0, sh_degree=deg, lang_dim=D)
+    keys = ("means3D", "shs", "opacities", "scales", "rotations", "language_feature_precomp")
+    g = {k: gcpu[k].to(dev) for k in keys}
+    g["means2D"] = torch.zeros_like(g["means3D"])
+    rs = settings(cam, dev, deg, True)
+    rast = GaussianRasterizer(rs)
+
+    def step():
+        with torch.no_grad():
+            return rast(means3D=g["means3D"], means2D=g["means2D"], opacities=g["opacities"], shs=g["shs"],
+                        language_feature_precomp=g["language_feature_precomp"], scales=g["scales"],
+                        rotations=g["rotations"])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    _lib.profile_stages(None)
+    _lib.profile_reset()
+    _lib.profile_enable(True)
+    for _ in range(max(2, min(args.steps, 5))):
+        step()
+    torch.cuda.synchronize()
+    _lib.profile_enable(False)
+    per_stage = {k: ms / calls for k, (ms, calls) in _lib.profile_query().items() if calls}
+    dom = "render_fwd"
+    _lib.profile_stages([dom])
+    _lib.profile_reset()
+    _lib.profile_enable(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    _lib.profile_enable(False)
+    _lib.profile_stages(None)
+    dom_ms_s, dom_calls = _lib.profile_query()[dom]
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)   # timing only, not on the data path
+        elapsed = float(t.item())
+    if rank == 0:
+        bytes_, info = algorithmic_bytes(g, rs, D, 48)
+        dom_ms = dom_ms_s / dom_calls if dom_calls else 0.0
+        dom_gbps = bytes_[dom] / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+        step_ms = elapsed / args.steps * 1e3
+        fwd_keys = ("preprocess", "bin_count", "scan_tile_counts", "bin_scatter", "tile_sort", "render_fwd")
+        out = {
+            "metric": "frames/s fwd @ 5M Gaussians 4K 3+32ch (BASELINE configs[4], replicas)",
+            "value": round(world * args.steps / elapsed, 3),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(step_ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded; SURVEY.md §8d generator)",
+            "config": {
+                "workload": "BASELINE cfg5: 5M Gaussians, 3840x2160, SH deg 3 + 32 dense language channels, "
+                            "forward only; 1 view per GPU, replicas (no collective)",
+                "gaussians": N, "width": W, "height": H, "lang_dim": D, "sh_degree": deg,
+                "global_batch": world, "parallelism": f"replicas x{world}" if world > 1 else "single GPU",
+            },
+            "ranks_seen": dist.get_world_size() if world > 1 else 1,
+            "roofline": {
+                "bound": "hbm", "kernel": dom, "achieved": round(dom_gbps, 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(dom_gbps / HBM_PEAK_GBPS, 4), "traffic": None,
+                "algorithmic_bytes_per_launch": int(bytes_[dom]),
+                "bytes_formula": "SURVEY.md §8d (bench.py:algorithmic_bytes)",
+                "ms_per_launch": round(dom_ms, 4), "launches_timed": dom_calls,
+            },
+            "stages_ms": {k: round(v, 4) for k, v in per_stage.items()},
+            "stage_bytes": {k: int(bytes_[k]) for k in fwd_keys if k in bytes_},
+            "workload_stats": info,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
     return 0
 
 
@@ -273,7 +382,8 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=3, choices=[3])
+    ap.add_argument("--config", type=int, default=3, choices=[3, 5],
+                    help="3: BASELINE cfg3 fwd+bwd (the headline); 5: BASELINE cfg5 forward-only replicas")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fwd-1mpix", action="store_true")
     ap.add_argument("--no-quick", action="store_true")
@@ -288,7 +398,7 @@ def main() -> int:
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     if args.dry_run:
-        return dry_run(world, rank)
+        return dry_run(world, rank, args.config)
     if world > 1:
         dist.init_process_group("nccl")
         if dist.get_world_size() != args.gpus:
@@ -296,6 +406,8 @@ def main() -> int:
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     _lib.load()
+    if args.config == 5:
+        return main_forward_replicas(args, world, rank, dev)
 
     cfg = CONFIGS[args.config]
     N, W, H, D, deg = cfg["N"], cfg["W"], cfg["H"], cfg["lang_dim"], cfg["sh_degree"]

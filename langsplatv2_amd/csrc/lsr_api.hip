@@ -719,6 +719,9 @@ static int record_lang_ready(const lsr_bwd_out* out, hipStream_t st)
     return LSR_OK;
 }
 
+static int backward_dense(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* b, lsr_bwd_out* out,
+                          lsr_alloc_fn alloc, void* ctx, hipStream_t st, Guard& guard);
+
 // Quick (sparse) language input: weights (P,K) + codes (P,K) rendered into
 // Dq channels.  dL/dweights[j][m] = sum_p aT_j(p) dL/dout_lang[idx[j][m]][p].
 //  - weights alone requested (feature-mode training, geometry frozen): the
@@ -737,7 +740,12 @@ static int backward_quick(const lsr_settings* s, const lsr_inputs* in, const lsr
     float* dw = out->dL_dlang_weights;
     const bool geom = geometry_requested(out);
     if (!dw && !geom) return record_lang_ready(out, st);
-    if (dw && !b->dL_dout_lang) return LSR_EINVAL;
+    if (dw && !geom && !b->dL_dout_lang) {
+        // the weights requested but the language output received no gradient
+        // (autograd passes none when the loss ignores it): dL/dweights = 0
+        LSR_HIP(hipMemsetAsync(dw, 0, (size_t)P * in->quick_k * 4, st));
+        return record_lang_ready(out, st);
+    }
     if (dw && !geom) {
         if (lang_set_for(Dq) < 0) return LSR_EUNSUPPORTED;
         const Cam c = make_cam(s);
@@ -791,7 +799,8 @@ static int backward_quick(const lsr_settings* s, const lsr_inputs* in, const lsr
         b2.dL_dout_lang = nullptr;
         if (dw) LSR_HIP(hipMemsetAsync(dw, 0, (size_t)P * in->quick_k * 4, st));
     }
-    int rc = lsr_backward(&s2, &in2, &b2, &o2, alloc, ctx, st);
+    // the dense backward shares this call's guard (its flag word stays owned by one Guard)
+    int rc = backward_dense(&s2, &in2, &b2, &o2, alloc, ctx, st, guard);
     if (rc != LSR_OK) return rc;
     if (dw && dense_grad)
         LSR_HIP(launch_sparse_gather(dense_grad, in->language_feature_indices, in->quick_index_dtype, P, in->quick_k,
@@ -821,6 +830,19 @@ int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* 
     LSR_GUARD(guard, "dL_dout_color", b->dL_dout_color, 3 * NPIX);
     LSR_GUARD(guard, "dL_dout_lang", b->dL_dout_lang, (size_t)(s->quick_render ? quick_dim(s) : Dd) * NPIX);
     if (s->quick_render) return backward_quick(s, in, b, out, alloc, ctx, st, guard);
+    return backward_dense(s, in, b, out, alloc, ctx, st, guard);
+}
+
+// The dense-input backward (lsr_backward's body past validation; also the
+// geometry path of the quick input, with that call's guard).
+static int backward_dense(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* b, lsr_bwd_out* out,
+                          lsr_alloc_fn alloc, void* ctx, hipStream_t st, Guard& guard)
+{
+    int rc = LSR_OK;
+    const Cam c = make_cam(s);
+    const int P = in->P;
+    const int Dd = dense_dim(s, in);
+    if (Dd > 0 && !b->dL_dout_lang) return LSR_EINVAL;
     // Only dL/dlanguage requested (feature-mode training with frozen geometry
     // and no means2D gradient): the language-only render backward writes the
     // output directly; no gradient rows, no preprocess backward.

@@ -6,6 +6,16 @@
 // counts.  Operation sequence == oracle/lsr_oracle.c lso_preprocess.
 #include "lsr_internal.h"
 
+// Scale gradient convention (a named switch, SURVEY §8a style):
+//  0 (default, upstream 3DGS): dL/dscales is the gradient w.r.t. the MODIFIED
+//    scale s = scale_modifier * scale, i.e. the modifier factor is omitted;
+//  1: the exact derivative dL/dscale = scale_modifier * dL/ds.
+// Only scale_modifier != 1 tells them apart (training always renders at 1).
+#ifndef LSR_SCALE_GRAD_EXACT
+#define LSR_SCALE_GRAD_EXACT 0
+#endif
+#define LSR_SCALE_GRAD_MOD(mod) (LSR_SCALE_GRAD_EXACT ? (mod) : 1.0f)
+
 namespace lsr {
 
 // Backward SH16 path: one wave per 64 Gaussians.  The wave stages its 64 SH
@@ -413,7 +423,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const Cam& c, const lsr_input
         if (out.dL_dscales)
 #pragma unroll
             for (int k = 0; k < 3; k++)
-                out.dL_dscales[3 * i + k] = mod * (dM[0 * 3 + k] * R[0 * 3 + k] + dM[1 * 3 + k] * R[1 * 3 + k] + dM[2 * 3 + k] * R[2 * 3 + k]);
+                out.dL_dscales[3 * i + k] = LSR_SCALE_GRAD_MOD(mod) * (dM[0 * 3 + k] * R[0 * 3 + k] + dM[1 * 3 + k] * R[1 * 3 + k] + dM[2 * 3 + k] * R[2 * 3 + k]);
 #pragma unroll
         for (int r = 0; r < 3; r++)
 #pragma unroll

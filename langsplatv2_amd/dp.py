@@ -181,6 +181,8 @@ class ViewShardedExchange:
         self._ev = None
         self._side = None
         self.cuda = params[0].is_cuda
+        self._params = list(params)
+        self._sink = None
         if self.cuda and self.early is not None and self.world > 1:
             self._ev = torch.cuda.Event()
             self._side = torch.cuda.Stream(device=params[0].device)
@@ -204,6 +206,14 @@ class ViewShardedExchange:
             out[self.sh_idx] = self.sh_grad
         return out
 
+    def _on_lang_ready(self, sink):
+        """GradSink callback: start the early all-reduce only when the backward
+        wrote every early bucket view itself (otherwise finish() packs them first).
+        The condition depends only on which inputs need grad, so every rank
+        decides the same way."""
+        if all(self.names[i] in sink.used for i in self.early_idx):
+            self._launch_early()
+
     def _launch_early(self):
         if self.world <= 1 or self.early is None or self._early_work is not None:
             return
@@ -220,8 +230,11 @@ class ViewShardedExchange:
         from .rasterizer import GradSink
         bufs = {nm: v for nm, v in zip(self.names, self._views()) if nm is not None}
         self._early_work = None
-        return GradSink(bufs, lang_ready=self._ev, on_lang_ready=self._launch_early if self._ev is not None else None,
-                        rgb_sh=self.rgb_mine if self.sh_idx is not None else None)
+        self._sink = GradSink(bufs, lang_ready=self._ev,
+                              on_lang_ready=self._on_lang_ready if self._ev is not None else None,
+                              rgb_sh=self.rgb_mine if self.sh_idx is not None else None,
+                              params={nm: p for nm, p in zip(self.names, self._params) if nm is not None})
+        return self._sink
 
     def _factored_sh(self, campos, means3D, sh_degree):
         """All-gather the views' colour gradients and camera centres, rebuild the
@@ -250,12 +263,26 @@ class ViewShardedExchange:
         factored SH gradient, `campos` (this view's camera centre), `means3D`
         and `sh_degree` (the rasterizer settings') are required."""
         views = self._views()
+        used = self._sink.used if self._sink is not None else set()
+        # factored SH only when the backward wrote dL/dRGB for the bucketed SH leaf;
+        # otherwise (e.g. shs = cat(f_dc, f_rest)) the SH gradient is all-reduced as is
+        factored = self.sh_idx is not None and "shs" in used
         if grads is not None:
             for i, (g, v) in enumerate(zip(grads, views)):
+                if i == self.sh_idx and factored:
+                    continue   # filled by _factored_sh below
+                if g is not None and g.data_ptr() == v.data_ptr():
+                    continue
+                if i in self.early_idx and self._early_work is not None:
+                    # the early all-reduce is in flight on this view: packing it now would race
+                    raise RuntimeError("finish: an early-bucket gradient did not land in its bucket view, "
+                                       "but its all-reduce already started")
                 if g is None:
                     v.zero_()
-                elif g.data_ptr() != v.data_ptr():
+                else:
                     v.copy_(g.reshape(v.shape))
+        elif self.sh_idx is not None and not factored:
+            raise ValueError("finish: the SH gradient was not factored by the backward; pass grads")
         if self.with_stats:
             if means2D_grad is None or radii is None:
                 raise ValueError("finish: densification statistics need means2D.grad and radii")
@@ -264,8 +291,10 @@ class ViewShardedExchange:
         if self.world > 1:
             self._launch_early()   # no-op if the backward already started it
             work = self.main.allreduce(self.group, async_op=True)
-            if self.sh_idx is not None:
+            if factored:
                 self._factored_sh(campos, means3D, sh_degree)
+            elif self.sh_idx is not None:
+                dist.all_reduce(self.sh_grad, op=dist.ReduceOp.SUM, group=self.group)
             if radii is not None:
                 max_radii = radii.clone()
                 dist.all_reduce(max_radii, op=dist.ReduceOp.MAX, group=self.group)
@@ -273,6 +302,7 @@ class ViewShardedExchange:
             if self._early_work is not None:
                 self._early_work.wait()
             self._early_work = None
+        self._sink = None
         return views, self.main.stats(), max_radii
 
     def exchange(self, grads, means2D_grad=None, radii=None):

@@ -58,4 +58,9 @@ class FusedAdam(torch.optim.Optimizer):
                                              float(group["lr"]), float(b1), float(b2), float(group["eps"]),
                                              float(group["weight_decay"]), int(state["step"].item()),
                                              _stream(p.device)), "lsr_adam_step")
+                # the kernel wrote p, m and v through raw pointers: bump their
+                # version counters as an in-place torch op would, so caches keyed
+                # on _version (quick.decode_plan) and autograd's saved-tensor
+                # checks see the update
+                torch.autograd.graph.increment_version((p, m, v))
         return loss

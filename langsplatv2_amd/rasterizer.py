@@ -75,14 +75,41 @@ class GradSink:
                   after the exchange (lsr_sh_grad_from_views).  Used only when
                   buffers has "shs" and the SH input needs a gradient.
 
+      params      optional {input name: leaf tensor}: a buffer is used only when
+                  the rasterizer's input of that name IS this tensor (the bucketed
+                  leaf itself; with the reference glue, e.g. shs = cat(f_dc, f_rest),
+                  the input is a non-leaf and its gradient goes to a fresh tensor).
+
+    `used` collects the names whose buffer a backward wrote; a second backward
+    in the same sink that would write the same buffer raises (autograd would
+    otherwise sum two views of one tensor).  on_lang_ready is called with the
+    sink, after `used` is updated.
+
     Input names: means3D, means2D, shs, colors_precomp, language_feature_precomp,
     language_feature_weights_quick, opacities, scales, rotations, cov3D_precomp."""
 
-    def __init__(self, buffers=None, lang_ready=None, on_lang_ready=None, rgb_sh=None):
+    def __init__(self, buffers=None, lang_ready=None, on_lang_ready=None, rgb_sh=None, params=None):
         self.buffers = dict(buffers or {})
         self.lang_ready = lang_ready
         self.on_lang_ready = on_lang_ready
         self.rgb_sh = rgb_sh
+        self.params = dict(params) if params is not None else None
+        self.used: set = set()
+
+    def take(self, name, shape, dev, input_id) -> Optional[torch.Tensor]:
+        """The buffer for input `name` of a backward (None: allocate a fresh one)."""
+        t = self.buffers.get(name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != torch.float32 or t.device != dev \
+                or not t.is_contiguous():
+            return None
+        if self.params is not None:
+            leaf = self.params.get(name)
+            if leaf is None or id(leaf) != input_id:
+                return None
+        if name in self.used:
+            raise RuntimeError(f"GradSink: the {name} buffer was already written by another backward in this sink")
+        self.used.add(name)
+        return t
 
     def __enter__(self):
         with _SINKS_LOCK:
@@ -248,6 +275,12 @@ class _RasterizeGaussians(torch.autograd.Function):
             language_feature_indices, opacities, scales, rotations, cov3Ds_precomp, raster_settings)
         ctx.raster_settings = raster_settings
         ctx.num_rendered = num_rendered
+        # identities of the inputs (GradSink.params: a sink buffer is used only for its own leaf)
+        ctx.input_ids = {"means3D": id(means3D), "means2D": id(means2D), "shs": id(sh),
+                         "colors_precomp": id(colors_precomp), "language_feature_precomp": id(language_feature_precomp),
+                         "language_feature_weights_quick": id(language_feature_weights_quick),
+                         "opacities": id(opacities), "scales": id(scales), "rotations": id(rotations),
+                         "cov3D_precomp": id(cov3Ds_precomp)}
         ctx.dims = dims
         ctx.save_for_backward(*saved, radii, bufs[_lib.LSR_BUF_GEOM], bufs[_lib.LSR_BUF_BINNING],
                               bufs[_lib.LSR_BUF_IMAGE])
@@ -288,9 +321,8 @@ class _RasterizeGaussians(torch.autograd.Function):
             if not flag:
                 return None
             if sink is not None:
-                t = sink.buffers.get(name)
-                if (t is not None and tuple(t.shape) == tuple(shape) and t.dtype == torch.float32
-                        and t.device == dev and t.is_contiguous()):
+                t = sink.take(name, shape, dev, ctx.input_ids[name])
+                if t is not None:
                     return t
             return torch.empty(shape, dtype=torch.float32, device=dev)
 
@@ -329,7 +361,7 @@ class _RasterizeGaussians(torch.autograd.Function):
                 _dump("snapshot_bw.dump", [grad_color, gl, means3D, sh, col, opac, sc, rot, cov, lang, qw, qi])
             _lib.check(rc, "rasterize_gaussians_backward")
         if sink is not None and sink.on_lang_ready is not None:
-            sink.on_lang_ready()
+            sink.on_lang_ready(sink)
         return (g_means3D if need[0] else None, g_means2D if need[1] else None, g_sh, g_col, g_lang, g_qw, None,
                 g_opac if need[7] else None, g_sc, g_rot, g_cov, None)
 

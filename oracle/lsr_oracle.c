@@ -14,6 +14,11 @@
  */
 #include "lsr_oracle.h"
 #include <float.h>
+/* Scale-gradient convention, mirroring csrc/preprocess.hip's LSR_SCALE_GRAD_EXACT:
+ * 0 (default) = upstream 3DGS (dL/dscales w.r.t. scale_modifier * scale). */
+#ifndef LSO_SCALE_GRAD_EXACT
+#define LSO_SCALE_GRAD_EXACT 0
+#endif
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -830,9 +835,11 @@ void lso_preprocess_bwd(const lso_settings* s, const lso_inputs* in, const lso_g
             for (int r = 0; r < 3; r++)
                 for (int cc = 0; cc < 3; cc++)
                     dM[r * 3 + cc] = 2.f * (Gm[r * 3 + 0] * Mm[0 * 3 + cc] + Gm[r * 3 + 1] * Mm[1 * 3 + cc] + Gm[r * 3 + 2] * Mm[2 * 3 + cc]);
-            /* dL/ds_c = mod Σ_r dM[r][c] R[r][c]; dL/dR[r][c] = dM[r][c] sv[c] */
+            /* dL/ds_c = Σ_r dM[r][c] R[r][c] (upstream: w.r.t. the modified scale;
+             * LSO_SCALE_GRAD_EXACT 1: times mod, the exact derivative);
+             * dL/dR[r][c] = dM[r][c] sv[c] */
             for (int cc = 0; cc < 3; cc++)
-                pg->dscales[3 * i + cc] = mod * (dM[0 * 3 + cc] * R[0 * 3 + cc] + dM[1 * 3 + cc] * R[1 * 3 + cc] + dM[2 * 3 + cc] * R[2 * 3 + cc]);
+                pg->dscales[3 * i + cc] = (LSO_SCALE_GRAD_EXACT ? mod : 1.0f) * (dM[0 * 3 + cc] * R[0 * 3 + cc] + dM[1 * 3 + cc] * R[1 * 3 + cc] + dM[2 * 3 + cc] * R[2 * 3 + cc]);
             float dR[9];
             for (int r = 0; r < 3; r++)
                 for (int cc = 0; cc < 3; cc++) dR[r * 3 + cc] = dM[r * 3 + cc] * sv[cc];

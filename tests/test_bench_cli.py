@@ -40,3 +40,16 @@ def test_gpus1_dry_run_is_single_rank():
 def test_launcher_mismatch_fails_loudly():
     p = _run(["--gpus", "2", "--dry-run"], env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode != 0 and "WORLD_SIZE=1" in (p.stderr + p.stdout)
+
+
+def test_config5_forward_replicas_dry_run():
+    """BASELINE configs[4] (cfg5): forward-only replicas, one view per rank at distinct
+    yaws, no collective on the data path; the ranks come up and agree (no GPU)."""
+    p = _run(["--config", "5", "--gpus", "2", "--dry-run"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    j = _last_json(p.stdout)
+    assert j["config"] == 5 and "replicas" in j["mode"] and "no collective" in j["mode"]
+    assert j["n_gpus"] == 2 and j["ranks"] == [0, 1] and j["world_sizes_seen"] == [2]
+    assert j["yaws"] == [-20.0, 20.0]
+    p1 = _run(["--dry-run"])
+    assert _last_json(p1.stdout)["config"] == 3

@@ -152,3 +152,38 @@ def _finish_worker(rank, world, port):
 
 def test_exchange_finish_two_buckets_gloo_world2():
     mp.spawn(_finish_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def test_grad_sink_leaf_identity_and_reuse():
+    """GradSink hands out a buffer only for its own leaf (params given) and only
+    once per sink (a non-leaf input such as cat(f_dc, f_rest) must
+    not receive the bucket view; a second backward must not reuse it)."""
+    from langsplatv2_amd.rasterizer import GradSink
+    leaf = torch.zeros(4, 3)
+    buf = torch.empty(4, 3)
+    s = GradSink({"means3D": buf}, params={"means3D": leaf})
+    dev = buf.device
+    assert s.take("means3D", (4, 3), dev, id(leaf.clone())) is None     # another tensor
+    assert s.take("means3D", (4, 2), dev, id(leaf)) is None             # wrong shape
+    assert s.take("means3D", (4, 3), dev, id(leaf)) is buf
+    assert s.used == {"means3D"}
+    with pytest.raises(RuntimeError, match="already written"):
+        s.take("means3D", (4, 3), dev, id(leaf))
+    s2 = GradSink({"means3D": buf})                                     # no params: any input of that name
+    assert s2.take("means3D", (4, 3), dev, 12345) is buf
+
+
+def test_early_allreduce_only_when_backward_wrote_the_early_bucket():
+    """The early (language) all-reduce is launched from the sink callback only
+    when every early-bucket view was written by the backward."""
+    names = ["means3D", "language_feature_precomp"]
+    params = [torch.zeros(5, 3), torch.zeros(5, 16)]
+    ex = dp.ViewShardedExchange(params, with_stats=False, names=names)
+    launched = []
+    ex._launch_early = lambda: launched.append(1)
+    sink = ex.sink()
+    ex._on_lang_ready(sink)                       # language input had no grad: nothing written
+    assert launched == []
+    sink.used.add("language_feature_precomp")
+    ex._on_lang_ready(sink)
+    assert launched == [1]

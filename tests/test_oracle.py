@@ -241,7 +241,9 @@ def test_oracle_matches_float64_autograd(oracle_lib, name):
     if "colors_precomp" in params:
         close("colors_precomp", bwd["dcolors"], params["colors_precomp"].grad.numpy())
     if "scales" in params:
-        close("scales", bwd["dscales"], params["scales"].grad.numpy())
+        # upstream convention (LSR_SCALE_GRAD_EXACT 0): the gradient w.r.t. the
+        # modified scale, i.e. the exact derivative divided by scale_modifier
+        close("scales", bwd["dscales"], params["scales"].grad.numpy() / case["scale_modifier"])
         close("rotations", bwd["drot"], params["rotations"].grad.numpy())
     if "cov3D_precomp" in params:
         close("cov3D_precomp", bwd["dcov3D"], params["cov3D_precomp"].grad.numpy())

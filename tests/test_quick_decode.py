@@ -117,3 +117,23 @@ def test_plan_reuse_one_shot_and_invalidation(gpu):
     cb2[:, 32:] = cb2[:, :32]                              # rank 32 per level
     d = quick.decode_language_features(wmap, cb2)
     np.testing.assert_allclose(d.cpu().numpy(), ref_decode(wmap.cpu().numpy(), cb2.cpu().numpy()), atol=DEC_ATOL)
+
+
+@pytest.mark.gpu
+def test_plan_invalidated_by_fused_adam_step(gpu):
+    """FusedAdam writes the codebooks through a raw pointer; it bumps their
+    version counter, so the next decode prepares a new plan."""
+    from langsplatv2_amd.optim import FusedAdam
+    g = np.random.default_rng(11)
+    L, K, Df, H, W = 3, 64, 512, 24, 32
+    wmap = torch.from_numpy((g.random((L * K, H, W)) * (g.random((L * K, H, W)) < 0.2)).astype(np.float32)).to(gpu)
+    cb = torch.from_numpy(g.standard_normal((L, K, Df)).astype(np.float32)).to(gpu).requires_grad_(True)
+    quick.decode_language_features(wmap, cb.detach())
+    v0 = cb._version
+    opt = FusedAdam([cb], lr=0.05)
+    cb.grad = torch.randn(cb.shape, generator=torch.Generator().manual_seed(1)).to(gpu)
+    opt.step()
+    assert cb._version > v0
+    got = quick.decode_language_features(wmap, cb.detach())
+    np.testing.assert_allclose(got.cpu().numpy(), ref_decode(wmap.cpu().numpy(), cb.detach().cpu().numpy()),
+                               atol=DEC_ATOL)

@@ -146,3 +146,34 @@ def test_oracle_quick_expansion_semantics(oracle_lib):
     d = O.expand_quick(qw, codes, 64)
     assert d[0, 0] == 1.0 and d[0, 1] == 2.0 and d[0].sum() == 3.0      # codes >= 64 dropped
     assert d[1, 2] == 0.75 and d[1, 7] == 1.0 and d[1].sum() == 1.75    # duplicates summed, -1 dropped
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("geom_grad", [False, True])
+def test_quick_weights_grad_with_colour_only_loss(gpu, oracle_lib, geom_grad):
+    """Quick render whose weights require grad, with a loss on the colour only
+    (autograd passes no gradient for the language map): dL/dweights is zero and
+    the geometry gradients are the RGB-only ones (this used to raise
+    LSR_EINVAL from the quick backward)."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    case, logits, w, idx = _setup(gpu, seed=23)
+    w.retain_grad()
+    t = _geom(case, gpu, grad=geom_grad)
+    r = GaussianRasterizer(_settings(case, gpu, True, True))
+    color, lmap, _ = r(means3D=t["means3D"], means2D=torch.zeros_like(t["means3D"]), opacities=t["opacities"],
+                       shs=t["shs"], language_feature_weights_quick=w, language_feature_indices=idx,
+                       scales=t["scales"], rotations=t["rotations"])
+    dC = torch.randn(color.shape, generator=torch.Generator().manual_seed(2)).to(gpu)
+    color.backward(dC)
+    assert w.grad is not None and torch.count_nonzero(w.grad) == 0
+    assert logits.grad is not None and torch.count_nonzero(logits.grad) == 0
+    if geom_grad:
+        # the same frame without the language input: identical geometry gradients
+        t2 = _geom(case, gpu, grad=True)
+        r2 = GaussianRasterizer(_settings(case, gpu, False, False))
+        c2, _, _ = r2(means3D=t2["means3D"], means2D=torch.zeros_like(t2["means3D"]), opacities=t2["opacities"],
+                      shs=t2["shs"], scales=t2["scales"], rotations=t2["rotations"])
+        assert torch.equal(c2, color)
+        c2.backward(dC)
+        for k in ("means3D", "shs", "opacities", "scales", "rotations"):
+            assert_grad_close(k, t[k].grad.cpu().numpy(), t2[k].grad.cpu().numpy())
