@@ -502,6 +502,30 @@ __global__ void __launch_bounds__(64 * LSR_DEC2_WAVES, 1)
         load(t);
 #endif
         const int bx = (t % nbx) * 64, y = t / nbx;
+        // per-pixel power-of-two scaling of the weights before the f16 split:
+        // the pixel's largest |w| goes to [0.5, 1), so a nearly transparent
+        // pixel's small weights keep all 22 bits of hi + lo instead of falling
+        // into f16's subnormal range (exact: the scale is undone in `mul`, and
+        // the L2 norm is scale-invariant).  Lane (li, lg) holds pixel (pb, li).
+        float psc[4];   // 2^e of pixel (pb, li): w = psc * w_scaled
+#pragma unroll
+        for (int pb = 0; pb < 4; pb++) {
+            float m = 0.f;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; s2++)
+#pragma unroll
+                for (int j = 0; j < 8; j++) m = fmaxf(m, fabsf(raw[pb][s2][j]));
+            m = fmaxf(m, __shfl_xor(m, 16, 64));
+            m = fmaxf(m, __shfl_xor(m, 32, 64));
+            int e = 0;
+            if (m > 0.f && m < 3.0e38f) (void)frexpf(m, &e);
+            psc[pb] = ldexpf(1.f, e);
+            const float inv = ldexpf(1.f, -e);
+#pragma unroll
+            for (int s2 = 0; s2 < 2; s2++)
+#pragma unroll
+                for (int j = 0; j < 8; j++) raw[pb][s2][j] *= inv;
+        }
         h8 Wh[4][2], Wl[4][2];
 #pragma unroll
         for (int pb = 0; pb < 4; pb++)
@@ -517,11 +541,17 @@ __global__ void __launch_bounds__(64 * LSR_DEC2_WAVES, 1)
 #if LSR_DEC2_PF
         load(t + stride);   // next tile's weights in flight during this tile's products and stores
 #endif
+        // the scale of output pixel (pb, 4 lg + r) (the MFMA result layout)
+        float osc[4][4];
+#pragma unroll
+        for (int pb = 0; pb < 4; pb++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) osc[pb][r] = __shfl(psc[pb], 4 * lg + r, 64);
         float mul[4][4];
 #pragma unroll
         for (int pb = 0; pb < 4; pb++)
 #pragma unroll
-            for (int r = 0; r < 4; r++) mul[pb][r] = sc;
+            for (int r = 0; r < 4; r++) mul[pb][r] = sc * osc[pb][r];
         if constexpr (NORM) {
             // Y^T = W^T L: lane (k = 16 mb + li, lg) gets Y[k] of pixels 4 lg + r; |F_p|^2 = sum_k Y[k]^2
             float sq[4][4];
@@ -545,7 +575,8 @@ __global__ void __launch_bounds__(64 * LSR_DEC2_WAVES, 1)
 #pragma unroll
             for (int pb = 0; pb < 4; pb++)
 #pragma unroll
-                for (int r = 0; r < 4; r++) mul[pb][r] = sc / (sqrtf(fmaxf(row16_sum(sq[pb][r]) * ns2, 0.f)) + eps);
+                for (int r = 0; r < 4; r++)
+                    mul[pb][r] = sc / (sqrtf(fmaxf(row16_sum(sq[pb][r]) * ns2, 0.f)) + eps / osc[pb][r]);
         }
         float* const orow = out + (size_t)(l * Df + li) * HW + (size_t)y * W;
 #pragma unroll 1

@@ -14,7 +14,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_SO = os.path.join(_HERE, "_build", "liblsr_oracle.so")
+# LSO_ORACLE_LIB: another build of the same restatement (tests/test_asan.py: the ASan build)
+_SO = os.environ.get("LSO_ORACLE_LIB", os.path.join(_HERE, "_build", "liblsr_oracle.so"))
 _vp = ctypes.c_void_p
 
 

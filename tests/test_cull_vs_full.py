@@ -90,11 +90,17 @@ def test_cfg3_culled_gpu_equals_full_reference_lists(gpu, oracle_lib):
     dlang = np.zeros((pb.D, H, W), np.float32)
     dcol[:, bys, bxs] = rng.standard_normal((3, bys.size)).astype(np.float32)
     dlang[:, bys, bxs] = rng.standard_normal((pb.D, bys.size)).astype(np.float32)
+    gf = run_gpu_forward(case, gpu)
+    assert gf["num_rendered"] < ref["num_rendered"]
+    np.testing.assert_array_equal(gf["radii"], ref["radii"])
+    np.testing.assert_array_equal(gf["color"][:, ys, xs], ref["color"][:, ys, xs])
+    np.testing.assert_array_equal(gf["lang"][:, ys, xs], ref["lang"][:, ys, xs])
+    np.testing.assert_array_equal(gf["final_T"][ys, xs], ref["final_T"][ys, xs])
+    lc_got, lc_ref = _last_contributor_ids(gf, W, H), _last_contributor_ids(ref, W, H)
+    np.testing.assert_array_equal(lc_got[ys, xs], lc_ref[ys, xs])
+    del gf
     got = run_gpu_fwd_bwd(case, gpu, dcol, dlang)
-    np.testing.assert_array_equal(got["radii"], ref["radii"])
     np.testing.assert_array_equal(got["color"][:, ys, xs], ref["color"][:, ys, xs])
-    np.testing.assert_array_equal(got["lang"][:, ys, xs], ref["lang"][:, ys, xs])
-    np.testing.assert_array_equal(got["final_T"][ys, xs], ref["final_T"][ys, xs])
     rb = oracle_lib.backward(pb, ref, dcol, dlang, tiles=btiles, nthreads=_threads())
     assert_grad_close("means2D", got["grad_means2D"], rb["dmean2D"])
     assert_grad_close("opacities", got["grad_opacities"], rb["dopacity"][:, None])
