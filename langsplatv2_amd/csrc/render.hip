@@ -17,186 +17,25 @@
 // is a serial per-pixel recurrence; two instances per step keep two
 // independent exp chains in flight.
 //
-// Backward: same mapping, instances replayed back to front from the wave's
-// largest n_contrib.  Per (wave, instance) the 9 geometric/colour values are
-// reduced across the wave by recursive halving (gfx950 v_permlane32_swap,
-// v_permlane16_swap, row DPP) and added with one atomic per value; for
-// D >= 16 the language-channel gradients (aT[j][p] x dL/dlang[ch][p] summed
-// over the wave's 64 pixels) are a 16x64 . 64x16 product per 16 staged
-// instances, done exactly in f32 on the matrix cores
-// (v_mfma_f32_16x16x4_f32), with the dL/dlang fragments held in registers.
+// Backward (k_render_bwd_mf): same mapping, instances replayed back to front
+// from the wave's largest n_contrib in groups of 16 candidates: alpha/G per
+// candidate (phase 1), the serial transmittance recurrence (phase 2), then
+// every per-Gaussian pixel sum as a contraction — language on exact-f32 MFMA
+// (v_mfma_f32_16x16x4_f32), colour and the six geometry moments on the VALU —
+// added with line-coalesced buffer atomics (see the comment at the kernel).
 #include "lsr_internal.h"
 
-#ifndef LSR_BWD_PIPE
-#define LSR_BWD_PIPE 0
-#endif
-#ifndef LSR_BF_REGS
-#define LSR_BF_REGS 1
-#endif
-#ifndef LSR_BWD_MF
-#define LSR_BWD_MF 1
-#endif
-#ifndef LSR_FWD_PK
-#define LSR_FWD_PK 1        // fwd: pair-interleaved candidate geometry, packed (v_pk_*) exponent of 2 candidates
-#endif
-#ifndef LSR_FWD_SKIPVOTE
-#define LSR_FWD_SKIPVOTE 0  // fwd: skip a pair / its second candidate when no lane needs it (votes cost more than they save)
-#endif
 #ifndef LSR_BWD_SPLAT_PF
 #define LSR_BWD_SPLAT_PF 1  // bwd: chunk records loaded one chunk ahead (ids two ahead), D <= 32
-#endif
-#ifndef LSR_BWD_AF_PF
-#define LSR_BWD_AF_PF 0     // bwd: next group's feature fragments loaded after the current dot product (slower: +4 %)
 #endif
 #ifndef LSR_MF_WAVES
 #define LSR_MF_WAVES 2      // MFMA render kernels: min waves per SIMD (caps VGPRs at 256)
 #endif
 #define LSR_QUICK_KMAX 12   // quick path: (weight, code) pairs per Gaussian staged with the record
-#ifndef LSR_QUICK_QB
-#define LSR_QUICK_QB 4      // quick path: 64-channel slabs
-#endif
-#ifndef LSR_QUICK_V
-#define LSR_QUICK_V 1       // quick path: per-pixel accumulators in VGPRs, sparse (weight, code) updates
-#endif
-#ifndef LSR_FWD_MF_WIDE
-#define LSR_FWD_MF_WIDE 1   // D = 64: MFMA-accumulated forward
-#endif
-#ifndef LSR_BWD_MF_WIDE
-#define LSR_BWD_MF_WIDE 1   // D = 32, 64: factorised MFMA backward
-#endif
-#ifndef LSR_QUICK_MF
-#define LSR_QUICK_MF 1
-#endif
-#ifndef LSR_FWD_MF
-#define LSR_FWD_MF 0
-#endif
-#ifndef LSR_FWD_PKEXP
-#define LSR_FWD_PKEXP 1     // fwd (VALU blend): the pair's two deterministic exps on packed f32 (the
-                            // MFMA forwards keep the scalar exp: packed pairs there measured 5 % slower)
-#endif
-#ifndef LSR_FWD_2PX
-#define LSR_FWD_2PX 0       // fwd (VALU blend, D <= 32): two pixels per lane, one wave per 16x8 half tile (measured slower: cfg3 0.356 -> 0.361, cfg5 1.94 -> 2.09 ms)
-#endif
-#ifndef LSR_FWD_SPF
-#define LSR_FWD_SPF 1       // fwd: chunk records loaded one chunk ahead (ids two ahead)
-#endif
-#ifndef LSR_FWD_LASTJ
-#define LSR_FWD_LASTJ 1     // fwd: the last contributor tracked as a staged index (one select per candidate),
-                            // its tile-list position read from LDS once per chunk
-#endif
-#ifndef LSR_EXACT_CULL
-#define LSR_EXACT_CULL 1
-#endif
 
 namespace lsr {
 
 // ----------------------------------------------------------- reductions --
-template <int CTRL>
-__device__ __forceinline__ float dpp(float v)
-{
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-
-// Value of lane l ^ M (M = 16 or 32) via the gfx950 permlane swaps.
-template <int M>
-__device__ __forceinline__ float xor_f32(float v)
-{
-    const int lane = threadIdx.x & 63;
-    const uint32_t x = __float_as_uint(v);
-    if constexpr (M == 32) {
-        auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-        return __uint_as_float((lane & 32) ? r[0] : r[1]);
-    } else {
-        static_assert(M == 16, "xor_f32: M must be 16 or 32");
-        auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-        return __uint_as_float((lane & 16) ? r[0] : r[1]);
-    }
-}
-
-// Reduce 32 per-lane values across the wave.  On return, lane l holds the
-// wave-wide sum of value (l >> 1) in v[0].
-__device__ __forceinline__ float wave_reduce32(float (&v)[32])
-{
-    const int lane = threadIdx.x & 63;
-    // bit 5: lanes l <-> l+32 (permlane32_swap)
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[k]), __float_as_uint(v[k + 16]), false, false);
-        v[k] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-    }
-    // bit 4: rows 0<->1, 2<->3 (permlane16_swap)
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[k]), __float_as_uint(v[k + 8]), false, false);
-        v[k] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-    }
-    // bit 3: row_ror:8 (== xor 8 inside a row)
-    {
-        const bool hi = lane & 8;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            float keep = hi ? v[k + 4] : v[k];
-            float send = hi ? v[k] : v[k + 4];
-            v[k] = keep + dpp<0x128>(send);
-        }
-    }
-    // bit 2: row_half_mirror (pairs lanes across bit 2 inside each 8-lane half row)
-    {
-        const bool hi = lane & 4;
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            float keep = hi ? v[k + 2] : v[k];
-            float send = hi ? v[k] : v[k + 2];
-            v[k] = keep + dpp<0x141>(send);
-        }
-    }
-    // bit 1: quad_perm [2,3,0,1]
-    {
-        const bool hi = lane & 2;
-        float keep = hi ? v[1] : v[0];
-        float send = hi ? v[0] : v[1];
-        v[0] = keep + dpp<0x4E>(send);
-    }
-    // bit 0: quad_perm [1,0,3,2]
-    v[0] = v[0] + dpp<0xB1>(v[0]);
-    return v[0];
-}
-
-// Reduce 16 per-lane values across the wave; on return lane l holds the
-// wave-wide sum of value ((l >> 2) & 15).
-__device__ __forceinline__ float wave_reduce16(float (&v)[16])
-{
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[k]), __float_as_uint(v[k + 8]), false, false);
-        v[k] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[k]), __float_as_uint(v[k + 4]), false, false);
-        v[k] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-    }
-    {
-        const bool hi = lane & 8;
-#pragma unroll
-        for (int k = 0; k < 2; k++) {
-            float keep = hi ? v[k + 2] : v[k];
-            float send = hi ? v[k] : v[k + 2];
-            v[k] = keep + dpp<0x128>(send);
-        }
-    }
-    {
-        const bool hi = lane & 4;
-        float keep = hi ? v[1] : v[0];
-        float send = hi ? v[0] : v[1];
-        v[0] = keep + dpp<0x141>(send);
-    }
-    v[0] = v[0] + dpp<0x4E>(v[0]);
-    v[0] = v[0] + dpp<0xB1>(v[0]);
-    return v[0];
-}
-
 __device__ __forceinline__ int wave_max_i(int v)
 {
 #pragma unroll
@@ -245,20 +84,6 @@ __device__ __forceinline__ void stage_features(float4* dst, const float* rgb, co
     for (int q = 0; q < F4; q++) dst[q] = make_float4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
 }
 
-// Mask of instances [q, q+64) of a staged batch that may touch this wave's
-// 8x8 block (one ballot; the result lives in SGPRs and is walked with s_ff1).
-__device__ __forceinline__ uint64_t sub_mask(const float4* sA, const float4* sB, int q, int n, int bx, int by)
-{
-    const int j = q + (threadIdx.x & 63);
-    bool ok = false;
-    if (j < n) {
-        const float4 A = sA[j];
-        const float4 B = sB[j];
-        ok = block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by);
-    }
-    return wave_ballot(ok);
-}
-
 // Work-item mapping for the wave-independent render kernels: one 64-thread
 // workgroup (one wave) per 8x8 block; the four blocks of a tile get
 // consecutive indices inside one XCD's range (xcd_remap), so they share an L2.
@@ -291,51 +116,6 @@ struct WaveTile {
     }
 };
 
-// Per-wave LDS staging of one chunk of up to 64 candidate instances.
-template <int F4>
-struct WaveStage {
-    float4 A[64];
-    float4 B[64];
-    float4 F[64 * F4];
-    uint32_t gid[64];
-    int pos[64];
-};
-
-
-// Stage the candidates of one chunk: lane l holds instance (gid, A, B, pos) if
-// valid; instances that may touch the wave's 8x8 block are compacted (order
-// preserved: rank = popcount of lower candidate lanes) into LDS together with
-// their feature rows.  Returns the candidate count (wave-uniform).
-template <int NL, int F4>
-__device__ __forceinline__ int stage_candidates(WaveStage<F4>& st, bool valid, uint32_t gid, int pos, int bx, int by,
-                                                const float4* __restrict__ splatA, const float4* __restrict__ splatB,
-                                                const float* __restrict__ rgb, const float* __restrict__ lang, int D)
-{
-    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
-    if (valid) {
-        A = splatA[gid];
-        B = splatB[gid];
-    }
-#if LSR_EXACT_CULL
-    const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by) &&
-                    block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, bx, by);
-#else
-    const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by);
-#endif
-    const uint64_t m = wave_ballot(ok);
-    const int cnt = __popcll(m);
-    if (ok) {
-        const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        st.A[r] = A;
-        st.B[r] = B;
-        st.gid[r] = gid;
-        st.pos[r] = pos;
-        stage_features<NL, F4>(&st.F[r * F4], rgb, lang, D, gid);
-    }
-    wave_lds_fence();
-    return cnt;
-}
-
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Forward staging with the candidates' geometry pair-interleaved: entry
@@ -346,9 +126,6 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 #define LSR_FWD_SFEAT 32    // fwd: from this many language channels up, feature rows are read with scalar
                             // loads at blend time instead of staged in LDS (cfg5 D = 32: 2.46 -> 2.02 ms;
                             // at D = 16 the SGPR pressure makes it slower: 0.36 -> 0.61 ms)
-#endif
-#ifndef LSR_FWD_SFEAT_LAZY
-#define LSR_FWD_SFEAT_LAZY 0   // 1: fetch the second row just before its blend (fewer SGPRs live, measured slower)
 #endif
 template <int NL>
 constexpr bool fwd_sfeat() { return LSR_FWD_SFEAT > 0 && NL >= LSR_FWD_SFEAT; }
@@ -435,12 +212,8 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
 {
     constexpr int C = 3 + NL;
     constexpr int F4 = (C + 3) / 4;  // float4 per feature row
-#if LSR_FWD_PK
     constexpr bool SF = fwd_sfeat<NL>();
     __shared__ WaveStageP<F4, SF> st;
-#else
-    __shared__ WaveStage<F4> st;
-#endif
 
     const Cam& c = a.cam;
     const WaveTile wt(c);
@@ -459,7 +232,6 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
     bool done = !inside;
 
     uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
-#if LSR_FWD_PK && LSR_FWD_SPF
     // SPF: a chunk's ids are loaded two chunks ahead and its records one chunk
     // ahead, issued after the current chunk's feature loads: the staging then
     // waits for one dependent gather (the feature rows) instead of two.
@@ -473,13 +245,11 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
         A1 = a.splatA[next_gid];
         B1 = a.splatB[next_gid];
     }
-#endif
     for (uint32_t base = rs; base < re; base += 64) {
         if (wave_ballot(!done) == 0) break;
         const uint32_t idx = base + lane;
         const bool valid = idx < re;
         const uint32_t gid = next_gid;
-#if LSR_FWD_PK && LSR_FWD_SPF
         int n;
         if constexpr (FSPF) {
             const float4 Ac = A1, Bc = B1;
@@ -496,15 +266,6 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
             n = stage_candidates_p<NL, F4>(st, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, a.splatA, a.splatB,
                                            a.rgb, a.lang, D);
         }
-#elif LSR_FWD_PK
-        next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;   // prefetch the next chunk's ids
-        const int n = stage_candidates_p<NL, F4>(st, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, a.splatA,
-                                                 a.splatB, a.rgb, a.lang, D);
-#else
-        next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;   // prefetch the next chunk's ids
-        const int n = stage_candidates<NL, F4>(st, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, a.splatA, a.splatB,
-                                               a.rgb, a.lang, D);
-#endif
         // Two instances per iteration, branch-free per lane: a lane that
         // skips an instance (exponent cut, alpha < 1/255, saturated or done)
         // blends it with weight 0 and keeps T.  The two exp chains are
@@ -515,7 +276,6 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
             if (wave_ballot(!done) == 0) break;
             const bool two = j0 + 1 < n;
             const int j1 = two ? j0 + 1 : j0;
-#if LSR_FWD_PK
             // both candidates' exponents at once (splat_power, lane-wise);
             // a missing second candidate reads a stale slot: ok1 masks it
             const int e = j0 >> 1;
@@ -523,8 +283,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
             float fr0[F4 * 4], fr1[F4 * 4];
             if constexpr (SF) {
                 feature_row_uniform<NL, F4>(fr0, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j0]));
-                if (!LSR_FWD_SFEAT_LAZY)
-                    feature_row_uniform<NL, F4>(fr1, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j1]));
+                feature_row_uniform<NL, F4>(fr1, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j1]));
             }
             const f32x2 dx = st.X[e] - f32x2{pfx, pfx}, dy = st.Y[e] - f32x2{pfy, pfy};
             const f32x2 P = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f},
@@ -534,26 +293,9 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
             const float p0 = P.x, p1 = P.y;
             bool ok0 = !done && !(p0 > 0.0f || p0 < CUT.x);
             bool ok1 = two && !done && !(p1 > 0.0f || p1 < CUT.y);
-            if (LSR_FWD_SKIPVOTE && !wave_any(ok0 || ok1)) continue;
-#if LSR_FWD_PKEXP
             const f32x2 EX = expf_det2(P);   // both exponents packed (bitwise = expf_det)
             const float al0 = fminf(0.99f, OP.x * EX.x);
             const float al1 = fminf(0.99f, OP.y * EX.y);
-#else
-            const float al0 = fminf(0.99f, OP.x * expf_det(p0));
-            const float al1 = fminf(0.99f, OP.y * expf_det(p1));
-#endif
-#else
-            const float4 A0 = st.A[j0], B0 = st.B[j0];
-            const float4 A1 = st.A[j1], B1 = st.B[j1];
-            const float p0 = splat_power(A0.z, A0.w, B0.x, A0.x - pfx, A0.y - pfy);
-            const float p1 = splat_power(A1.z, A1.w, B1.x, A1.x - pfx, A1.y - pfy);
-            bool ok0 = !done && !(p0 > 0.0f || p0 < B0.z);
-            bool ok1 = two && !done && !(p1 > 0.0f || p1 < B1.z);
-            if (!wave_any(ok0 || ok1)) continue;
-            const float al0 = fminf(0.99f, B0.y * expf_det(p0));
-            const float al1 = fminf(0.99f, B1.y * expf_det(p1));
-#endif
             ok0 = ok0 && !(al0 < 1.0f / 255.0f);
             ok1 = ok1 && !(al1 < 1.0f / 255.0f);
             {
@@ -563,12 +305,10 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 ok0 = ok0 && !term;
                 ok1 = ok1 && !term;
                 const float aT = ok0 ? al0 * T : 0.f;
-#if LSR_FWD_PK
                 if constexpr (SF) {
 #pragma unroll
                     for (int k = 0; k < F4 * 4; k++) acc[k] = fmaf(fr0[k], aT, acc[k]);
                 } else
-#endif
                 {
 #pragma unroll
                     for (int f = 0; f < F4; f++) {
@@ -580,23 +320,18 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                     }
                 }
                 T = ok0 ? test_T : T;
-                if (LSR_FWD_LASTJ) lastj = ok0 ? j0 : lastj;
-                else last = ok0 ? (uint32_t)st.pos[j0] : last;
+                lastj = ok0 ? j0 : lastj;
             }
-            if (!LSR_FWD_SKIPVOTE || wave_any(ok1)) {
+            {
                 const float test_T = T * (1.0f - al1);
                 const bool term = ok1 && (test_T < 0.0001f);
                 done = done || term;
                 ok1 = ok1 && !term;
                 const float aT = ok1 ? al1 * T : 0.f;
-#if LSR_FWD_PK
                 if constexpr (SF) {
-                    if (LSR_FWD_SFEAT_LAZY)   // second row fetched here: half the SGPRs live
-                        feature_row_uniform<NL, F4>(fr1, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j1]));
 #pragma unroll
                     for (int k = 0; k < F4 * 4; k++) acc[k] = fmaf(fr1[k], aT, acc[k]);
                 } else
-#endif
                 {
 #pragma unroll
                     for (int f = 0; f < F4; f++) {
@@ -608,11 +343,10 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                     }
                 }
                 T = ok1 ? test_T : T;
-                if (LSR_FWD_LASTJ) lastj = ok1 ? j1 : lastj;
-                else last = ok1 ? (uint32_t)st.pos[j1] : last;
+                lastj = ok1 ? j1 : lastj;
             }
         }
-        if (LSR_FWD_LASTJ && lastj >= 0) last = (uint32_t)st.pos[lastj];
+        if (lastj >= 0) last = (uint32_t)st.pos[lastj];
         wave_lds_fence();
     }
     if (inside) {
@@ -625,211 +359,6 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
 #pragma unroll
         for (int k = 0; k < NL; k++)
             if (k < D) a.out_lang[k * HW + pix] = acc[3 + k];
-    }
-}
-
-// Two pixels per lane (the VALU-blend forward's default): one wave per 16x8
-// half tile, two per tile; lane l owns column l & 15 of rows (l >> 4) and
-// (l >> 4) + 4.  Every broadcast LDS read of a staged candidate (geometry pair,
-// feature row, position) now serves two pixels, which halves the LDS
-// instructions per pixel of the blend; the two pixels share dx (same column),
-// so ca.dx and cb.dx are computed once; the two pixels' recurrences are
-// independent chains.  Per pixel the operation sequence is exactly
-// k_render_fwd's (bit-identical).  Stores: each instruction writes four 64-B
-// row segments.
-template <int NL>
-__global__ void __launch_bounds__(64) k_render_fwd2(RenderArgs a)
-{
-    constexpr int C = 3 + NL;
-    constexpr int F4 = (C + 3) / 4;  // float4 per feature row
-    constexpr bool SF = fwd_sfeat<NL>();
-    __shared__ WaveStageP<F4, SF> st;
-
-    const Cam& c = a.cam;
-    const int o = xcd_remap(blockIdx.x, gridDim.x);
-    const int tile = band_tile(o >> 1, c.gx, c.gy);
-    const int lane = threadIdx.x;
-    const int bx = (tile % c.gx) * LSR_TILE, by = (tile / c.gx) * LSR_TILE + (o & 1) * 8;
-    const int px = bx + (lane & 15), pyA = by + (lane >> 4), pyB = pyA + 4;
-    const bool inA = px < c.W && pyA < c.H, inB = px < c.W && pyB < c.H;
-    const float pfx = (float)px, pfyA = (float)pyA, pfyB = (float)pyB;
-    const uint32_t rs = a.tile_start[tile], re = a.tile_start[tile + 1];
-    const int D = a.D;
-
-    float TA = 1.0f, TB = 1.0f;
-    float accA[F4 * 4], accB[F4 * 4];
-#pragma unroll
-    for (int k = 0; k < F4 * 4; k++) accA[k] = accB[k] = 0.f;
-    uint32_t lastA = 0, lastB = 0;
-    bool doneA = !inA, doneB = !inB;
-
-    uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
-    for (uint32_t base = rs; base < re; base += 64) {
-        if (wave_ballot(!(doneA && doneB)) == 0) break;
-        const uint32_t idx = base + lane;
-        const bool valid = idx < re;
-        const uint32_t gid = next_gid;
-        next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;   // prefetch the next chunk's ids
-        int n;
-        {
-            float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
-            if (valid) {
-                A = a.splatA[gid];
-                B = a.splatB[gid];
-            }
-            const bool ok = valid && rect_overlap(A.x, A.y, __float_as_uint(B.w), bx, by, 15, 7) &&
-                            rect_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, bx, by, 15.f, 7.f);
-            const uint64_t m = wave_ballot(ok);
-            n = __popcll(m);
-            if (ok) {
-                const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                float* sb = reinterpret_cast<float*>(&st) + (r & 1);
-                const int e = (r >> 1) * 2;
-                sb[0 * 64 + e] = A.x;
-                sb[1 * 64 + e] = A.y;
-                sb[2 * 64 + e] = A.z;
-                sb[3 * 64 + e] = A.w;
-                sb[4 * 64 + e] = B.x;
-                sb[5 * 64 + e] = B.y;
-                sb[6 * 64 + e] = B.z;
-                st.pos[r] = (int)(idx - rs) + 1;
-                if constexpr (SF)
-                    st.gid[r] = gid;
-                else
-                    stage_features<NL, F4>(&st.F[r * F4], a.rgb, a.lang, D, gid);
-            }
-            wave_lds_fence();
-        }
-        for (int j0 = 0; j0 < n; j0 += 2) {
-            if (wave_ballot(!(doneA && doneB)) == 0) break;
-            const bool two = j0 + 1 < n;
-            const int j1 = two ? j0 + 1 : j0;
-            const int e = j0 >> 1;
-            float fr0[F4 * 4], fr1[F4 * 4];
-            if constexpr (SF) {
-                feature_row_uniform<NL, F4>(fr0, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j0]));
-                feature_row_uniform<NL, F4>(fr1, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j1]));
-            }
-            // both candidates' exponents at both pixels (splat_power's sequence;
-            // a missing second candidate reads a stale slot: its ok flags mask it)
-            const f32x2 dx = st.X[e] - f32x2{pfx, pfx};
-            const f32x2 cadx = st.CA[e] * dx, cbdx = st.CB[e] * dx, CC = st.CC[e];
-            const f32x2 dyA = st.Y[e] - f32x2{pfyA, pfyA}, dyB = st.Y[e] - f32x2{pfyB, pfyB};
-            const f32x2 PA = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f},
-                                                       __builtin_elementwise_fma(cadx, dx, (CC * dyA) * dyA),
-                                                       -(cbdx * dyA));
-            const f32x2 PB = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f},
-                                                       __builtin_elementwise_fma(cadx, dx, (CC * dyB) * dyB),
-                                                       -(cbdx * dyB));
-            const f32x2 CUT = st.CUT[e], OP = st.OP[e];
-            bool okA0 = !doneA && !(PA.x > 0.0f || PA.x < CUT.x);
-            bool okA1 = two && !doneA && !(PA.y > 0.0f || PA.y < CUT.y);
-            bool okB0 = !doneB && !(PB.x > 0.0f || PB.x < CUT.x);
-            bool okB1 = two && !doneB && !(PB.y > 0.0f || PB.y < CUT.y);
-            const f32x2 EXA = expf_det2(PA), EXB = expf_det2(PB);
-            const float alA0 = fminf(0.99f, OP.x * EXA.x), alA1 = fminf(0.99f, OP.y * EXA.y);
-            const float alB0 = fminf(0.99f, OP.x * EXB.x), alB1 = fminf(0.99f, OP.y * EXB.y);
-            okA0 = okA0 && !(alA0 < 1.0f / 255.0f);
-            okA1 = okA1 && !(alA1 < 1.0f / 255.0f);
-            okB0 = okB0 && !(alB0 < 1.0f / 255.0f);
-            okB1 = okB1 && !(alB1 < 1.0f / 255.0f);
-            const uint32_t pos0 = (uint32_t)st.pos[j0], pos1 = (uint32_t)st.pos[j1];
-            // candidate j0 at both pixels
-            float aTA, aTB;
-            {
-                const float tA = TA * (1.0f - alA0), tB = TB * (1.0f - alB0);
-                const bool termA = okA0 && (tA < 0.0001f), termB = okB0 && (tB < 0.0001f);
-                doneA = doneA || termA;
-                doneB = doneB || termB;
-                okA0 = okA0 && !termA;
-                okA1 = okA1 && !termA;
-                okB0 = okB0 && !termB;
-                okB1 = okB1 && !termB;
-                aTA = okA0 ? alA0 * TA : 0.f;
-                aTB = okB0 ? alB0 * TB : 0.f;
-                TA = okA0 ? tA : TA;
-                TB = okB0 ? tB : TB;
-                lastA = okA0 ? pos0 : lastA;
-                lastB = okB0 ? pos0 : lastB;
-            }
-            if constexpr (SF) {
-#pragma unroll
-                for (int k = 0; k < F4 * 4; k++) {
-                    accA[k] = fmaf(fr0[k], aTA, accA[k]);
-                    accB[k] = fmaf(fr0[k], aTB, accB[k]);
-                }
-            } else {
-#pragma unroll
-                for (int f = 0; f < F4; f++) {
-                    const float4 v = st.F[j0 * F4 + f];
-                    accA[4 * f + 0] = fmaf(v.x, aTA, accA[4 * f + 0]);
-                    accA[4 * f + 1] = fmaf(v.y, aTA, accA[4 * f + 1]);
-                    accA[4 * f + 2] = fmaf(v.z, aTA, accA[4 * f + 2]);
-                    accA[4 * f + 3] = fmaf(v.w, aTA, accA[4 * f + 3]);
-                    accB[4 * f + 0] = fmaf(v.x, aTB, accB[4 * f + 0]);
-                    accB[4 * f + 1] = fmaf(v.y, aTB, accB[4 * f + 1]);
-                    accB[4 * f + 2] = fmaf(v.z, aTB, accB[4 * f + 2]);
-                    accB[4 * f + 3] = fmaf(v.w, aTB, accB[4 * f + 3]);
-                }
-            }
-            // candidate j1
-            {
-                const float tA = TA * (1.0f - alA1), tB = TB * (1.0f - alB1);
-                const bool termA = okA1 && (tA < 0.0001f), termB = okB1 && (tB < 0.0001f);
-                doneA = doneA || termA;
-                doneB = doneB || termB;
-                okA1 = okA1 && !termA;
-                okB1 = okB1 && !termB;
-                aTA = okA1 ? alA1 * TA : 0.f;
-                aTB = okB1 ? alB1 * TB : 0.f;
-                TA = okA1 ? tA : TA;
-                TB = okB1 ? tB : TB;
-                lastA = okA1 ? pos1 : lastA;
-                lastB = okB1 ? pos1 : lastB;
-            }
-            if constexpr (SF) {
-#pragma unroll
-                for (int k = 0; k < F4 * 4; k++) {
-                    accA[k] = fmaf(fr1[k], aTA, accA[k]);
-                    accB[k] = fmaf(fr1[k], aTB, accB[k]);
-                }
-            } else {
-#pragma unroll
-                for (int f = 0; f < F4; f++) {
-                    const float4 v = st.F[j1 * F4 + f];
-                    accA[4 * f + 0] = fmaf(v.x, aTA, accA[4 * f + 0]);
-                    accA[4 * f + 1] = fmaf(v.y, aTA, accA[4 * f + 1]);
-                    accA[4 * f + 2] = fmaf(v.z, aTA, accA[4 * f + 2]);
-                    accA[4 * f + 3] = fmaf(v.w, aTA, accA[4 * f + 3]);
-                    accB[4 * f + 0] = fmaf(v.x, aTB, accB[4 * f + 0]);
-                    accB[4 * f + 1] = fmaf(v.y, aTB, accB[4 * f + 1]);
-                    accB[4 * f + 2] = fmaf(v.z, aTB, accB[4 * f + 2]);
-                    accB[4 * f + 3] = fmaf(v.w, aTB, accB[4 * f + 3]);
-                }
-            }
-        }
-        wave_lds_fence();
-    }
-    const size_t HW = (size_t)c.H * c.W;
-    if (inA) {
-        const size_t pix = (size_t)pyA * c.W + px;
-        a.final_T[pix] = TA;
-        a.n_contrib[pix] = lastA;
-#pragma unroll
-        for (int ch = 0; ch < 3; ch++) a.out_color[ch * HW + pix] = fmaf(TA, c.bg[ch], accA[ch]);
-#pragma unroll
-        for (int k = 0; k < NL; k++)
-            if (k < D) a.out_lang[k * HW + pix] = accA[3 + k];
-    }
-    if (inB) {
-        const size_t pix = (size_t)pyB * c.W + px;
-        a.final_T[pix] = TB;
-        a.n_contrib[pix] = lastB;
-#pragma unroll
-        for (int ch = 0; ch < 3; ch++) a.out_color[ch * HW + pix] = fmaf(TB, c.bg[ch], accB[ch]);
-#pragma unroll
-        for (int k = 0; k < NL; k++)
-            if (k < D) a.out_lang[k * HW + pix] = accB[3 + k];
     }
 }
 
@@ -1165,17 +694,12 @@ int lang_set_for(int D)
 // kernels would default to 1024-thread workgroups and a 128-register cap)
 template <int NL>
 __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_fwd_mf(RenderArgs a);
-template <int QB>
-__global__ void __launch_bounds__(64) k_render_fwd_quick_mf(RenderArgs a);
-template <int QB, int NS>
-__global__ void __launch_bounds__(64 * NS) k_render_fwd_quick_wg(RenderArgs a);
 
 hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
 {
     const int T = a.cam.gx * a.cam.gy;
     if (T == 0) return hipSuccess;
     if (a.qw) {
-#if LSR_QUICK_V
         if (a.K <= 12 && a.Dq <= 192) {
             switch ((a.Dq + 31) / 32) {
                 case 1: k_render_fwd_quick_v<1><<<T * 4, 64, 0, st>>>(a); break;
@@ -1187,52 +711,18 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
             }
             return hipGetLastError();
         }
-#endif
-#if LSR_QUICK_MF
-        if (a.K <= LSR_QUICK_KMAX) {
-            // one workgroup of Dq/64 waves per 8x8 block (64-channel slabs)
-            if (a.Dq == 192) { k_render_fwd_quick_wg<4, 3><<<T * 4, 192, 0, st>>>(a); return hipGetLastError(); }
-            if (a.Dq == 128) { k_render_fwd_quick_wg<4, 2><<<T * 4, 128, 0, st>>>(a); return hipGetLastError(); }
-            if (a.Dq == 64) { k_render_fwd_quick_wg<4, 1><<<T * 4, 64, 0, st>>>(a); return hipGetLastError(); }
-            if (a.Dq % (16 * LSR_QUICK_QB) == 0) {   // other widths: one wave per slab, blend re-run per slab
-                k_render_fwd_quick_mf<LSR_QUICK_QB><<<dim3(T * 4, a.Dq / (16 * LSR_QUICK_QB)), 64, 0, st>>>(a);
-                return hipGetLastError();
-            }
-        }
-#endif
         const size_t sm = (size_t)a.Dq * 64 * 4 + 64 * 32 + 64 * 12 + (size_t)64 * a.K * 8;
         k_render_fwd_quick<<<T * 4, 64, sm, st>>>(a);
         return hipGetLastError();
     }
     switch (lang_set_for(a.D)) {
-#if LSR_FWD_MF
-        case 0: k_render_fwd_mf<0><<<4 * T, 64, 0, st>>>(a); break;
-        case 4: k_render_fwd_mf<4><<<4 * T, 64, 0, st>>>(a); break;
-        case 8: k_render_fwd_mf<8><<<4 * T, 64, 0, st>>>(a); break;
-        case 16: k_render_fwd_mf<16><<<4 * T, 64, 0, st>>>(a); break;
-#elif LSR_FWD_2PX
-        case 0: k_render_fwd2<0><<<2 * T, 64, 0, st>>>(a); break;
-        case 4: k_render_fwd2<4><<<2 * T, 64, 0, st>>>(a); break;
-        case 8: k_render_fwd2<8><<<2 * T, 64, 0, st>>>(a); break;
-        case 16: k_render_fwd2<16><<<2 * T, 64, 0, st>>>(a); break;
-#else
         case 0: k_render_fwd<0><<<4 * T, 64, 0, st>>>(a); break;
         case 4: k_render_fwd<4><<<4 * T, 64, 0, st>>>(a); break;
         case 8: k_render_fwd<8><<<4 * T, 64, 0, st>>>(a); break;
         case 16: k_render_fwd<16><<<4 * T, 64, 0, st>>>(a); break;
-#endif
-#if LSR_FWD_MF_WIDE
         // measured (cfg3 geometry): D = 32 legacy 0.78 vs MFMA 0.81 ms; D = 64 legacy 1.38 vs MFMA 1.13 ms
-#if LSR_FWD_2PX
-        case 32: k_render_fwd2<32><<<2 * T, 64, 0, st>>>(a); break;
-#else
         case 32: k_render_fwd<32><<<4 * T, 64, 0, st>>>(a); break;
-#endif
         case 64: k_render_fwd_mf<64><<<4 * T, 64, 0, st>>>(a); break;
-#else
-        case 32: k_render_fwd<32><<<4 * T, 64, 0, st>>>(a); break;
-        case 64: k_render_fwd<64><<<4 * T, 64, 0, st>>>(a); break;
-#endif
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1248,288 +738,7 @@ int grad_row_width(int D)
     return (nv + 31) / 32 * 32;
 }
 
-// Language-channel gradients on the matrix cores: grad[j][ch] = sum_p aT[j][p] *
-// dL/dout_lang[ch][p] for the 64 pixels p of a wave is a (16 instances x 64
-// pixels) x (64 pixels x 16 channels) product per flush: 16 exact-f32
-// v_mfma_f32_16x16x4_f32 per 16-channel block.  aT rows are staged in LDS
-// (row stride 66 floats: conflict-free A-fragment reads), the dout fragments
-// (B operand) are loaded once per wave into registers.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-#define SLOT_STRIDE 66
-
-template <int NB>
-__device__ __forceinline__ void flush_lang(const float* __restrict__ sw, const uint32_t* __restrict__ sg, int cnt,
-                                           const float (&bf)[NB][16], float* __restrict__ grad, int VP, int D)
-{
-    const int lane = threadIdx.x & 63;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    float a[16];
-#pragma unroll
-    for (int t = 0; t < 16; t++) a[t] = sw[(lane & 15) * SLOT_STRIDE + 4 * t + (lane >> 4)];
-#pragma unroll
-    for (int nb = 0; nb < NB; nb++) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int t = 0; t < 16; t++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], bf[nb][t], acc, 0, 0, 0);
-        const int ch = nb * 16 + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int row = 4 * (lane >> 4) + r;
-            const float v = acc[r];
-            if (row < cnt && ch < D && v != 0.f) atomicAdd(grad + (size_t)sg[row] * VP + LSR_GROW_LANG + ch, v);
-        }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
-// sbf: the wave's dout_lang block in LDS, [channel][pixel] with row stride
-// SLOT_STRIDE; the B fragment of K-step t for lane l is
-// sbf[(nb*16 + (l&15)) * SLOT_STRIDE + 4t + (l>>4)].
-template <int NB>
-__device__ __forceinline__ void flush_lang(const float* __restrict__ sw, const uint32_t* __restrict__ sg, int cnt,
-                                           const float* __restrict__ sbf, float* __restrict__ grad, int VP, int D)
-{
-    const int lane = threadIdx.x & 63;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    float a[16];
-#pragma unroll
-    for (int t = 0; t < 16; t++) a[t] = sw[(lane & 15) * SLOT_STRIDE + 4 * t + (lane >> 4)];
-#pragma unroll
-    for (int nb = 0; nb < NB; nb++) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        const float* bb = sbf + (nb * 16 + (lane & 15)) * SLOT_STRIDE + (lane >> 4);
-#pragma unroll
-        for (int t = 0; t < 16; t++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], bb[4 * t], acc, 0, 0, 0);
-        const int ch = nb * 16 + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const int row = 4 * (lane >> 4) + r;
-            const float v = acc[r];
-            if (row < cnt && ch < D && v != 0.f) atomicAdd(grad + (size_t)sg[row] * VP + LSR_GROW_LANG + ch, v);
-        }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
-// Reduce one instance's 9 geometric + colour values (v16) over the wave and
-// add them to its gradient row (lanes 4v hold value v).
-__device__ __forceinline__ void reduce_geom(float (&v16)[16], float* __restrict__ row)
-{
-    const int lane = threadIdx.x & 63;
-    const float sum = wave_reduce16(v16);
-    const int vi = (lane >> 2) & 15;
-    if (!(lane & 3) && vi < 9 && sum != 0.f) atomicAdd(row + vi, sum);
-}
-
-// Per-lane gradient values [0,9) of one (pixel, instance) pair (row layout of
-// lsr_device.h); dL/dalpha, G and aT are 0 for a non-contributing lane.
-__device__ __forceinline__ void geom_values(float (&v)[16], float dL_dalpha, float G, float aT, float4 A, float4 B,
-                                            float dx, float dy, float ddelx_dx, float ddely_dy, const float* Gd)
-{
-    const float dL_dG = B.y * dL_dalpha;
-    const float gdx = G * dx, gdy = G * dy;
-    const float dG_ddelx = -gdx * A.z - gdy * A.w;
-    const float dG_ddely = -gdy * B.x - gdx * A.w;
-    v[0] = dL_dG * dG_ddelx * ddelx_dx;
-    v[1] = dL_dG * dG_ddely * ddely_dy;
-    v[2] = -0.5f * gdx * dx * dL_dG;
-    v[3] = -gdx * dy * dL_dG;
-    v[4] = -0.5f * gdy * dy * dL_dG;
-    v[5] = G * dL_dalpha;
-    v[6] = aT * Gd[0];
-    v[7] = aT * Gd[1];
-    v[8] = aT * Gd[2];
-#pragma unroll
-    for (int k = 9; k < 16; k++) v[k] = 0.f;
-}
-
-template <int NL>
-__global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs b)
-{
-    constexpr int C = 3 + NL;
-    constexpr int F4 = (C + 3) / 4;
-    constexpr bool MF = NL >= 16;               // language grads on MFMA
-    constexpr int NB = MF ? NL / 16 : 1;        // 16-channel blocks
-    constexpr int NV = MF ? 9 : LSR_GROW_LANG + NL;   // values through the wave reduction
-    constexpr int NG = (NV + 31) / 32;
-    __shared__ WaveStage<F4> st;
-    __shared__ float sW[MF ? 16 * SLOT_STRIDE : 1];
-    __shared__ float sbf[(MF && !LSR_BF_REGS) ? NL * SLOT_STRIDE : 1];
-    __shared__ uint32_t sG[16];
-
-    const RenderArgs& a = b.f;
-    const Cam& c = a.cam;
-    const WaveTile wt(c);
-    const int lane = threadIdx.x;
-    const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
-    const bool inside = pm.px < c.W && pm.py < c.H;
-    const float pfx = (float)pm.px, pfy = (float)pm.py;
-    const uint32_t rs = a.tile_start[wt.tile];
-    const size_t HW = (size_t)c.H * c.W;
-    const size_t pix = (size_t)pm.py * c.W + pm.px;
-    const int D = a.D;
-    const int VP = b.VP;
-    const float ddelx_dx = 0.5f * (float)c.W, ddely_dy = 0.5f * (float)c.H;
-
-    const float T_final = inside ? a.final_T[pix] : 0.f;
-    const int last = inside ? (int)a.n_contrib[pix] : 0;
-    const int wmax = wave_max_i(last);
-    if (wmax == 0) return;
-    float Gd[F4 * 4];
-#pragma unroll
-    for (int k = 0; k < F4 * 4; k++) Gd[k] = 0.f;
-    if (inside) {
-        Gd[0] = b.dout_color[pix];
-        Gd[1] = b.dout_color[HW + pix];
-        Gd[2] = b.dout_color[2 * HW + pix];
-#pragma unroll
-        for (int k = 0; k < NL; k++)
-            if (k < D) Gd[3 + k] = b.dout_lang[k * HW + pix];
-    }
-#if LSR_BF_REGS
-    // the MFMA B operand in registers: lane l holds dout_lang[nb*16 + (l&15)]
-    // at block pixel 4t + (l>>4)
-    float bf[NB][16];
-    if (MF) {
-#pragma unroll
-        for (int t4 = 0; t4 < 16; t4++) {
-            const int p = 4 * t4 + (lane >> 4);
-            const int qx = pm.bx + (p & 7), qy = pm.by + (p >> 3);
-            const bool in = qx < c.W && qy < c.H;
-#pragma unroll
-            for (int nb = 0; nb < NB; nb++) {
-                const int ch = nb * 16 + (lane & 15);
-                bf[nb][t4] = (in && ch < D) ? b.dout_lang[(size_t)ch * HW + (size_t)qy * c.W + qx] : 0.f;
-            }
-        }
-    }
-#define LSR_BFRAG bf
-#else
-    // the MFMA B operand: this wave's dout_lang block in LDS, [channel][pixel]
-    if (MF) {
-#pragma unroll
-        for (int k = 0; k < NL; k++) sbf[k * SLOT_STRIDE + lane] = Gd[3 + k];
-    }
-#define LSR_BFRAG sbf
-#endif
-    const float bg0 = c.bg[0], bg1 = c.bg[1], bg2 = c.bg[2];
-    const bool has_bg = (bg0 != 0.f) || (bg1 != 0.f) || (bg2 != 0.f);   // uniform
-    const float bg_dot = bg0 * Gd[0] + bg1 * Gd[1] + bg2 * Gd[2];
-
-    float T = T_final;
-    float last_alpha = 0.f, last_dot = 0.f, rec = 0.f;
-    int nslot = 0;   // wave-uniform
-
-    // positions [0, wmax) back to front, 64 per chunk
-    uint32_t next_gid = (wmax - 1 - lane >= 0) ? a.point_list[rs + wmax - 1 - lane] : 0u;
-    for (int c0 = 0; c0 < wmax; c0 += 64) {
-        const int p = wmax - 1 - (c0 + lane);
-        const bool valid = p >= 0;
-        const uint32_t gid = next_gid;
-        next_gid = (p - 64 >= 0) ? a.point_list[rs + p - 64] : 0u;
-        const int n = stage_candidates<NL, F4>(st, valid, gid, p, pm.bx, pm.by, a.splatA, a.splatB, a.rgb, a.lang, D);
-#if LSR_BWD_PIPE
-        // software-pipelined LDS reads: instance j+1's record is in flight
-        // while j is processed
-        float4 An = st.A[0], Bn = st.B[0];
-        int posn = st.pos[0];
-#endif
-        for (int j = 0; j < n; j++) {
-#if LSR_BWD_PIPE
-            const float4 A = An;
-            const float4 B = Bn;
-            const int posj = posn;
-            const int jn = j + 1 < n ? j + 1 : j;
-            An = st.A[jn];
-            Bn = st.B[jn];
-            posn = st.pos[jn];
-            float4 fr[F4];
-#pragma unroll
-            for (int q4 = 0; q4 < F4; q4++) fr[q4] = st.F[j * F4 + q4];
-#else
-            const float4 A = st.A[j];
-            const float4 B = st.B[j];
-            const int posj = st.pos[j];
-#endif
-            const float dx = A.x - pfx, dy = A.y - pfy;
-            const float power = splat_power(A.z, A.w, B.x, dx, dy);
-            bool contrib = (posj < last) && !(power > 0.0f || power < B.z);
-            float G = 0.f, alpha = 0.f;
-            if (contrib) {
-                G = expf_det(power);
-                alpha = fminf(0.99f, B.y * G);
-                contrib = alpha >= 1.0f / 255.0f;
-            }
-            if (!wave_any(contrib)) continue;
-            // Branch-free from here: a non-contributing lane carries
-            // alpha = G = 0, so every value it contributes is 0 and its
-            // running state is left unchanged.
-            alpha = contrib ? alpha : 0.f;
-            G = contrib ? G : 0.f;
-            const float one_m = 1.f - alpha;
-            T = T / one_m;
-            const float aT = alpha * T;
-            float f[F4 * 4];
-#pragma unroll
-            for (int q4 = 0; q4 < F4; q4++) {
-#if LSR_BWD_PIPE
-                const float4 v = fr[q4];
-#else
-                const float4 v = st.F[j * F4 + q4];
-#endif
-                f[4 * q4] = v.x; f[4 * q4 + 1] = v.y; f[4 * q4 + 2] = v.z; f[4 * q4 + 3] = v.w;
-            }
-            float dot = f[0] * Gd[0];
-#pragma unroll
-            for (int k = 1; k < C; k++) dot = fmaf(f[k], Gd[k], dot);
-            const float rec_new = fmaf(last_alpha, last_dot, (1.f - last_alpha) * rec);
-            float dL_dalpha = (dot - rec_new) * T;
-            if (has_bg) dL_dalpha = fmaf(-T_final / one_m, bg_dot, dL_dalpha);
-            dL_dalpha = contrib ? dL_dalpha : 0.f;
-            rec = contrib ? rec_new : rec;
-            last_alpha = contrib ? alpha : last_alpha;
-            last_dot = contrib ? dot : last_dot;
-            const uint32_t gidj = st.gid[j];
-            float* row = b.grad_acc + (size_t)gidj * VP;
-            float v16[16];
-            geom_values(v16, dL_dalpha, G, aT, A, B, dx, dy, ddelx_dx, ddely_dy, Gd);
-            if (MF) {
-                reduce_geom(v16, row);
-                // stage this instance's aT column for the MFMA language product
-                sW[nslot * SLOT_STRIDE + lane] = aT;
-                if (lane == 0) sG[nslot] = gidj;
-                if (++nslot == 16) {
-                    flush_lang<NB>(sW, sG, 16, LSR_BFRAG, b.grad_acc, VP, D);
-                    nslot = 0;
-                }
-            } else {
-                float vals[NG * 32];
-#pragma unroll
-                for (int k = 0; k < 9; k++) vals[k] = v16[k];
-#pragma unroll
-                for (int k = 9; k < NG * 32; k++) vals[k] = 0.f;
-#pragma unroll
-                for (int k = 0; k < NL; k++) vals[LSR_GROW_LANG + k] = aT * Gd[3 + k];
-#pragma unroll
-                for (int g = 0; g < NG; g++) {
-                    float v32[32];
-#pragma unroll
-                    for (int k = 0; k < 32; k++) v32[k] = vals[g * 32 + k];
-                    const float sum = wave_reduce32(v32);
-                    const int vi = g * 32 + (lane >> 1);
-                    if (!(lane & 1) && vi < LSR_GROW_LANG + D && sum != 0.f) atomicAdd(row + vi, sum);
-                }
-            }
-        }
-        wave_lds_fence();
-    }
-    if (MF && nslot > 0) {
-        // zero the unused slot rows so stale aT values never enter the product
-        for (int sl = nslot; sl < 16; sl++) sW[sl * SLOT_STRIDE + lane] = 0.f;
-        flush_lang<NB>(sW, sG, nslot, LSR_BFRAG, b.grad_acc, VP, D);
-    }
-}
-
 
 // ------------------------------------------------ factorised backward ----
 // Every per-(pixel, instance) gradient term is a product of a per-pair
@@ -1554,17 +763,11 @@ struct BwdFrags {
     float momB[16];       // moment (l&15) of block pixel 4t + (l>>4)
 };
 
-#ifndef LSR_BWD_BRFREE
-#define LSR_BWD_BRFREE 1   // bwd: loads issued unconditionally at clamped (valid) addresses, results selected:
-                           // no exec-skip branches around loads, so the compiler's vmcnt waits stay exact
-                           // (a conditional load makes every later wait a vmcnt(0), defeating the prefetches)
-#endif
 template <int NL>
 __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int bx, int by)
 {
     const Cam& cm = b.f.cam;
     const int qx = bx + (q & 7), qy = by + (q >> 3);
-#if LSR_BWD_BRFREE
     const bool ok = qx < cm.W && qy < cm.H && c < 3 + b.f.D;
     const size_t HW = (size_t)cm.H * cm.W;
     const size_t pix = (size_t)min(qy, cm.H - 1) * cm.W + min(qx, cm.W - 1);
@@ -1572,58 +775,13 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
     if (c >= 3 && b.f.D == 0) src = b.dout_color;
     const float v = src[pix];
     return ok ? v : 0.f;
-#else
-    if (qx >= cm.W || qy >= cm.H || c >= 3 + b.f.D) return 0.f;
-    const size_t HW = (size_t)cm.H * cm.W;
-    const size_t pix = (size_t)qy * cm.W + qx;
-    return c < 3 ? b.dout_color[c * HW + pix] : b.dout_lang[(size_t)(c - 3) * HW + pix];
-#endif
 }
 
-#define LSR_DOT_STRIDE 68   // sDot row stride: conflict-free fragment stores
-#define LSR_MOM_STRIDE 8
-#ifndef LSR_P1_UNROLL
-#define LSR_P1_UNROLL 4
-#endif
-#ifndef LSR_BWD_VMOM
-#define LSR_BWD_VMOM 1      // bwd: geometry moments and RGB sums on the VALU, MFMA only for dot + language
-#endif
-#ifndef LSR_BWD_LANG_DIRECT
-#define LSR_BWD_LANG_DIRECT 1   // bwd, D = 16 / 32: dL/dlang atomics straight into the output (no row copy)
-#endif
-#ifndef LSR_BWD_ALIAS
-#define LSR_BWD_ALIAS 1
-#endif
 #ifndef LSR_GRP_STRIDE
 #define LSR_GRP_STRIDE 66   // dot/u and aT tiles: conflict-free A-fragment reads (li*66 mod 32 = 2 li)
 #endif
-#ifndef LSR_BWD_RSCAT
-#define LSR_BWD_RSCAT 1     // bwd: phase-3 sums reduced two values per permlane swap, parked in LDS
-#endif
-#ifndef LSR_BWD_GREG
-#define LSR_BWD_GREG 1         // bwd: phase 1's G kept in VGPRs for phase 2 (no sAT round trip)
-#endif
-#ifndef LSR_BWD_GD_BUF
-#define LSR_BWD_GD_BUF 1       // bwd (VEC): dL/dout fragments by buffer loads, out-of-image pixels by offset
-#endif
-#ifndef LSR_BWD_ROWREG
-#define LSR_BWD_ROWREG 1       // bwd, direct dL/dlang: language atomics straight from the MFMA accumulators
-#endif
-#ifndef LSR_BWD_OPLANE
-#define LSR_BWD_OPLANE 1       // bwd: phase 2's opacities by v_readlane from one per-lane LDS read
-#endif
-#ifndef LSR_BWD_BUF_ATOM
-#define LSR_BWD_BUF_ATOM 1     // bwd: gradient atomics through raw buffer descriptors, masked by offset
-#endif
 #define LSR_BUF_OOB 0x7ffffffc  // a byte offset past every buffer the backward addresses this way
-#ifndef LSR_BWD_VEC_FEAT
-#define LSR_BWD_VEC_FEAT 1     // bwd, direct dL/dlang: feature rows gathered as float4 lines (dot_channel)
-#endif
-#ifndef LSR_BWD_ATOM_BATCH
-#define LSR_BWD_ATOM_BATCH 1   // bwd: the group's atomic values and ids read from LDS before any atomic issues
-#endif
 #define LSR_MOM9_STRIDE 12  // reduced moment + colour sums per candidate (16-B aligned rows)
-static_assert(!LSR_BWD_RSCAT || LSR_BWD_ALIAS, "the reduced sums are parked in the aliased aT tile");
 #define LSR_LOG2E 1.4426950408889634f
 #ifdef LSR_MF_NO_ATOMIC   // timing experiment only: keeps the work, drops the atomics
 #define LSR_MF_ATOMIC(ptr, v) do { if ((v) == 1234.5678f) atomicAdd((ptr), (v)); } while (0)
@@ -1694,17 +852,11 @@ __device__ __forceinline__ int stage_candidates_geo_rec(WaveStageG& st, int carr
 template <int NL>
 __device__ __forceinline__ float feature_at(const RenderArgs& a, uint32_t gid, int c)
 {
-#if LSR_BWD_BRFREE
     const bool ok = c < 3 + a.D;
     const float* src = c < 3 ? a.rgb + 3 * (size_t)gid + c
                              : (ok ? a.lang + (size_t)gid * a.D + (c - 3) : a.rgb + 3 * (size_t)gid);
     const float v = *src;
     return ok ? v : 0.f;
-#else
-    if (c < 3) return a.rgb[3 * (size_t)gid + c];
-    if (c - 3 < a.D) return a.lang[(size_t)gid * a.D + (c - 3)];
-    return 0.f;
-#endif
 }
 
 // Channel of the dot product's K-step t in lane group lg.  Default: channel
@@ -1782,27 +934,22 @@ __device__ unsigned long long g_bwd_stamps[16];
 template <int NL, bool LO = false, bool LD = false, bool SP = false>
 __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArgs b)
 {
-    static_assert(!LO || (LSR_BWD_VMOM && NL > 0), "language-only backward needs the VMOM layout and D > 0");
+    static_assert(!LO || NL > 0, "language-only backward needs D > 0");
     static_assert(!SP || LO, "the sparse-input gradient is a language-only backward");
-    static_assert(!LD || (LSR_BWD_VMOM && !LO && NL % 16 == 0), "direct dL/dlang needs VMOM and whole 16-channel lines");
+    static_assert(!LD || (!LO && NL % 16 == 0), "direct dL/dlang needs whole 16-channel lines");
     using FR = BwdFrags<NL>;
     constexpr int KS = FR::KS;
     // LD implies D == NL (launch_render_bwd) and 16-B aligned rows (lsr_api)
-    constexpr bool VEC = LD && LSR_BWD_VEC_FEAT;
+    constexpr bool VEC = LD;
     // RREG (direct dL/dlang): the language lines' atomics take their values
     // straight from the MFMA accumulators, lane (li, lg) adding candidate
     // 4 lg + q's channel li (the C layout), so those rows skip LDS
-    constexpr bool RREG = LD && LSR_BWD_ROWREG && LSR_BWD_ATOM_BATCH && LSR_BWD_VMOM;
-#if LSR_BWD_VMOM
+    constexpr bool RREG = LD;
     // MFMA channel blocks cover the language channels only; RGB (3) and the
     // six geometry moments are summed on the VALU (see phase 3)
     constexpr int NBC = (NL + 15) / 16;
     constexpr int NBA = NBC > 0 ? NBC : 1;
     __shared__ float4 sDrgb[64];      // dL/dout RGB of the block's pixels
-#else
-    constexpr int NBC = FR::NBC;
-    constexpr int NBA = NBC;
-#endif
     constexpr int GS = LSR_GRP_STRIDE;
     __shared__ WaveStageG st;
 #ifdef LSR_BWD_LDS_PAD   // occupancy experiment only: extra LDS per wave
@@ -1814,7 +961,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     constexpr int GCOL0 = LO ? 0 : (LD ? 16 : LSR_GROW_LANG);
     constexpr int GRL = (GCOL0 + NL + 15) / 16;            // 16-float lines per gradient row
     constexpr int GRS = 16 * GRL + 4;                     // staged row stride
-#if LSR_BWD_ALIAS
     // The gradient-row tile and the moments are written only after phase 3
     // has read dot/u and aT into registers (a wave's LDS operations complete
     // in order), so they share those buffers: 2.3-5.4 KB less LDS per wave,
@@ -1825,12 +971,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     static_assert(16 * LSR_MOM9_STRIDE <= 16 * GS, "moment rows must fit the aT tile");
     float* const sGr = sDU;
     float* const sMom = sAT;
-#else
-    __shared__ float sDU[16 * GS];    // dot[k][p], overwritten in place by u[k][p]
-    __shared__ float sAT[16 * GS];    // G[k][p] (phase 1), then aT[k][p] (phase 2)
-    __shared__ float sMom[16 * LSR_MOM_STRIDE];
-    __shared__ float sGr[16 * GRS];   // the group's gradient rows
-#endif
 
     const RenderArgs& a = b.f;
     const Cam& c = a.cam;
@@ -1847,7 +987,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     const int D = a.D;
     const int VP = b.VP;
     const float ddelx_dx = 0.5f * (float)c.W, ddely_dy = 0.5f * (float)c.H;
-#if LSR_BWD_BUF_ATOM
     // gradient rows (and LD: the language output) as raw buffers when every
     // byte offset fits 31 bits (uniform; otherwise 64-bit global atomics)
     const uint64_t nbg = (uint64_t)a.P * (uint64_t)VP * 4u;
@@ -1857,7 +996,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
         __builtin_amdgcn_make_buffer_rsrc(b.grad_acc, 0, (int)min(nbg, (uint64_t)LSR_BUF_OOB), 0x00020000);
     const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
         LD ? b.lang_acc : b.grad_acc, 0, (int)min(LD ? nbl : nbg, (uint64_t)LSR_BUF_OOB), 0x00020000);
-#endif
 
     const float T_final = inside ? a.final_T[pix] : 0.f;
     const int last = inside ? (int)a.n_contrib[pix] : 0;
@@ -1874,26 +1012,15 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     // ahead, so staging never waits on a dependent gather (9 more VGPRs: off
     // for the widest language set, where they would spill)
     constexpr bool SPF = LSR_BWD_SPLAT_PF && NL <= 32;
-#if LSR_BWD_BRFREE
     // tile-list position clamped to the range (wmax >= 1: position 0 exists), result selected
     auto pl_at = [&](int q) -> uint32_t { const uint32_t v = a.point_list[rs + max(q, 0)]; return q >= 0 ? v : 0u; };
-#else
-    auto pl_at = [&](int q) -> uint32_t { return q >= 0 ? a.point_list[rs + q] : 0u; };
-#endif
     uint32_t gid1 = pl_at(wmax - 1 - lane);
     uint32_t gid2 = 0u;
     float4 A1 = make_float4(0.f, 0.f, 0.f, 0.f), B1 = A1;
     if constexpr (SPF) {
         gid2 = pl_at(wmax - 65 - lane);
-#if LSR_BWD_BRFREE
         A1 = a.splatA[gid1];   // gid 0 for positions past the range: a valid record, never staged
         B1 = a.splatB[gid1];
-#else
-        if (wmax - 1 - lane >= 0) {
-            A1 = a.splatA[gid1];
-            B1 = a.splatB[gid1];
-        }
-#endif
     }
     // entries past a group's end are read unconditionally (immediate-offset
     // loads, no index clamps): keep them finite
@@ -1910,7 +1037,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
         dr2 = gd_at<NL>(b, 2, lane, pm.bx, pm.by);
     }
     float dotB[KS][4], chB[NBA][16];
-#if LSR_BWD_GD_BUF
     // VEC: the dL/dout fragments through raw buffer descriptors when every
     // byte offset fits 31 bits (uniform): a fragment's offset is its
     // channel's plane plus the pixel's, and a pixel outside the image gets an
@@ -1947,7 +1073,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #pragma unroll
             for (int t = 0; t < 16; t++) chB[nb][t] = ld(rlng, (uint32_t)(nb * 16 + li) * hw4 + poff(4 * t + lg));
     } else
-#endif
     {
     if constexpr (!LO) {
 #pragma unroll
@@ -1960,7 +1085,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 dotB[t][pb] = gd_at<NL>(b, dot_channel<NL, VEC>(t, lg), pb * 16 + li, pm.bx, pm.by);
 #endif
     }
-#if LSR_BWD_VMOM
 #pragma unroll
     for (int nb = 0; nb < NBC; nb++)
 #pragma unroll
@@ -1970,19 +1094,11 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #else
             chB[nb][t] = gd_at<NL>(b, 3 + nb * 16 + li, 4 * t + lg, pm.bx, pm.by);
 #endif
-#endif
     }
-#if LSR_BWD_VMOM
     // block-centred x of the pixels this lane's fragments cover: columns lg
     // (even K-steps) and 4 + lg (odd K-steps)
     const float lxe = (float)lg - 3.5f, lxo = (float)lg + 0.5f;
     const float lxe2 = lxe * lxe, lxo2 = lxo * lxo;
-#else
-#pragma unroll
-    for (int nb = 0; nb < NBC; nb++)
-#pragma unroll
-        for (int t = 0; t < 16; t++) chB[nb][t] = gd_at<NL>(b, nb * 16 + li, 4 * t + lg, pm.bx, pm.by);
-#endif
     const float bg0 = c.bg[0], bg1 = c.bg[1], bg2 = c.bg[2];
     // dr* are the lane's own pixel's values (0 outside): 0 with a black
     // background, and the term below is then exact 0
@@ -1996,12 +1112,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     // in groups of 16, a partial group carried into the next chunk
     int carry = 0;
     float af[KS];
-#if LSR_BWD_AF_PF
-    bool af_ready = false;
-#endif
-#if LSR_BWD_VMOM
     if constexpr (!LO) sDrgb[lane] = make_float4(dr0, dr1, dr2, 0.f);
-#endif
     BWD_STAMP(0);
     for (int c0 = 0; c0 < wmax; c0 += 64) {
         const int p = wmax - 1 - (c0 + lane);
@@ -2012,17 +1123,8 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             const uint32_t gid = gid1;
             const float4 Ac = A1, Bc = B1;
             gid1 = gid2;
-#if LSR_BWD_BRFREE
             A1 = a.splatA[gid1];
             B1 = a.splatB[gid1];
-#else
-            A1 = make_float4(0.f, 0.f, 0.f, 0.f);
-            B1 = A1;
-            if (p - 64 >= 0) {
-                A1 = a.splatA[gid1];
-                B1 = a.splatB[gid1];
-            }
-#endif
             gid2 = pl_at(p - 128);
             n = carry + stage_candidates_geo_rec(st, carry, valid, gid, p, pm.bx, pm.by, Ac, Bc);
         } else {
@@ -2038,9 +1140,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             BWD_COUNT(9);
             // A fragments of the dot product: feature 4t+lg of candidate g0+li,
             // gathered now, consumed after phase 1
-#if LSR_BWD_AF_PF
-            if (!af_ready)
-#endif
             if constexpr (!LO) {
                 const uint32_t gi = st.gid[g0 + (li < kn ? li : 0)];
 #ifdef LSR_PROBE_NOFEAT   // timing probe only (wrong results): no feature gather
@@ -2058,22 +1157,14 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             // as a lane mask (scalar ORs), not per-lane flags.
             uint64_t near_m = 0u;
             const int kn_u = __builtin_amdgcn_readfirstlane(kn);   // uniform: scalar compares below
-#if LSR_BWD_OPLANE
             // candidate li's opacity in lane li: phase 2 takes candidate k's
             // from lane k (v_readlane) instead of a broadcast LDS read per k
             const int opl = __float_as_int(st.B[g0 + li].y);
 #define BWD_OP(k) __int_as_float(__builtin_amdgcn_readlane(opl, (k)))
-#else
-#define BWD_OP(k) st.B[g0 + (k)].y
-#endif
             // GREG: G stays in registers from phase 1 to phase 2 (no LDS round trip)
             float Gr[16];
             (void)Gr;
-#if LSR_BWD_GREG
 #pragma unroll
-#else
-#pragma unroll LSR_P1_UNROLL
-#endif
             for (int k = 0; k < 16; k++) {
                 const float4 A = st.A[g0 + k];
                 const float4 B = st.B[g0 + k];
@@ -2083,22 +1174,14 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 const float G = cj ? __builtin_amdgcn_exp2f(power * LSR_LOG2E) : 0.f;
                 const float d = fminf(0.99f, B.y * G) - (1.0f / 255.0f);
                 near_m |= lanes_abs_lt(d, 2e-8f);
-#if LSR_BWD_GREG
                 Gr[k] = d >= 0.f ? G : 0.f;
-#else
-                sAT[k * GS + lane] = d >= 0.f ? G : 0.f;
-#endif
             }
             if (near_m != 0u) {
                 // the 1/255 decision must be the forward's: lanes inside the fast
                 // exp's error band re-evaluate with the forward's exp (rare)
-#if LSR_BWD_GREG
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
                     if (k >= kn) break;
-#else
-                for (int k = 0; k < kn; k++) {
-#endif
                     const int j = g0 + k;
                     const float4 A = st.A[j];
                     const float4 B = st.B[j];
@@ -2108,11 +1191,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                     if (cj & (fabsf(af2 - (1.0f / 255.0f)) < 2e-8f)) {
                         const float G = expf_det(power);
                         const float alpha = fminf(0.99f, B.y * G);
-#if LSR_BWD_GREG
                         Gr[k] = !(alpha < 1.0f / 255.0f) ? G : 0.f;
-#else
-                        sAT[k * GS + lane] = !(alpha < 1.0f / 255.0f) ? G : 0.f;
-#endif
                     }
                 }
             }
@@ -2145,15 +1224,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #pragma unroll
                     for (int r = 0; r < 4; r++) sDU[(4 * lg + r) * GS + pb * 16 + li] = acc[pb][r];
             }
-#if LSR_BWD_AF_PF
-            // the next group's feature fragments, when it is staged already
-            af_ready = g0 + 16 < nfull;
-            if (af_ready) {
-                const int kn2 = min(16, nfull - g0 - 16);
-                const uint32_t gi = st.gid[g0 + 16 + (li < kn2 ? li : 0)];
-                dot_features<NL, VEC>(a, gi, lg, af);
-            }
-#endif
             wave_lds_fence();
             BWD_STAMP(3);
             // phase 2: the serial back-to-front recurrence per pixel.  S is the
@@ -2166,7 +1236,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 // transmittance only: aT_k = alpha_k T_k (T_k recovered back to front)
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
-                    const float G = LSR_BWD_GREG ? Gr[k] : sAT[k * GS + lane];
+                    const float G = Gr[k];
                     const float al = fminf(0.99f, BWD_OP(k) * G);
                     T = T * __builtin_amdgcn_rcpf(1.f - al);
                     sAT[k * GS + lane] = al * T;
@@ -2174,7 +1244,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             } else if (has_bg) {
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
-                    const float G = LSR_BWD_GREG ? Gr[k] : sAT[k * GS + lane];
+                    const float G = Gr[k];
                     const float dot = sDU[k * GS + lane];
                     const float al = fminf(0.99f, BWD_OP(k) * G);
                     const float om = 1.f - al;
@@ -2188,7 +1258,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             } else {
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
-                    const float G = LSR_BWD_GREG ? Gr[k] : sAT[k * GS + lane];
+                    const float G = Gr[k];
                     const float dot = sDU[k * GS + lane];
                     const float al = fminf(0.99f, BWD_OP(k) * G);
                     const float om = 1.f - al;
@@ -2200,7 +1270,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             }
             wave_lds_fence();
             BWD_STAMP(4);
-#if LSR_BWD_VMOM
             // phase 3: language gradients on MFMA; RGB gradients and the six
             // pixel moments sum_p u {1, lx, ly, lx^2, lx ly, ly^2} on the VALU.
             // Lane (li, lg) reads candidate li's aT and u at pixel q = 4t + lg
@@ -2246,7 +1315,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                     M5 = fmaf(ly * ly, R0, M5);
                 }
             }
-#if LSR_BWD_RSCAT
             // The nine partial sums over the four lane groups, reduced two at a
             // time: a permlane swap exchanges half of one value for half of
             // another, so swap + add halves two values' lane groups at once
@@ -2273,14 +1341,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 mr[4 + s0] = Y1;
                 if (lg == 0) mr[8] = Y2;
             }
-#else
-            M0 += xor_f32<16>(M0); M1 += xor_f32<16>(M1); M2 += xor_f32<16>(M2);
-            M3 += xor_f32<16>(M3); M4 += xor_f32<16>(M4); M5 += xor_f32<16>(M5);
-            C0 += xor_f32<16>(C0); C1 += xor_f32<16>(C1); C2 += xor_f32<16>(C2);
-            M0 += xor_f32<32>(M0); M1 += xor_f32<32>(M1); M2 += xor_f32<32>(M2);
-            M3 += xor_f32<32>(M3); M4 += xor_f32<32>(M4); M5 += xor_f32<32>(M5);
-            C0 += xor_f32<32>(C0); C1 += xor_f32<32>(C1); C2 += xor_f32<32>(C2);
-#endif
             }
             // Gradient rows of the group staged in LDS (row layout of lsr_device.h:
             // [0..5] geometry, [6..8] colour, [12..) language), then added with
@@ -2294,14 +1354,11 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                     for (int r = 0; r < 4; r++) sGr[(4 * lg + r) * GRS + GCOL0 + chn] = ch[nb][r];
                 }
             }
-#if LSR_BWD_RSCAT
             if constexpr (!LO) wave_lds_fence();
-#endif
             if (!LO && lane < kn) {   // lane = candidate li (lg = 0)
                 const int j = g0 + lane;
                 const float4 A = st.A[j];
                 const float4 B = st.B[j];
-#if LSR_BWD_RSCAT
                 const float* const mr = sMom + lane * LSR_MOM9_STRIDE;
                 const float4 m03 = *reinterpret_cast<const float4*>(mr);
                 const float4 m47 = *reinterpret_cast<const float4*>(mr + 4);
@@ -2309,9 +1366,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 C0 = m47.z;
                 C1 = m47.w;
                 C2 = mr[8];
-#else
-                const float S0 = M0, S1 = M1, S2 = M2, S3 = M3, S4 = M4, S5 = M5;
-#endif
                 const float X = A.x - cx, Y = A.y - cy;
                 const float Sdx = fmaf(X, S0, -S1), Sdy = fmaf(Y, S0, -S2);
                 const float Sdxx = fmaf(X, fmaf(X, S0, -2.f * S1), S3);
@@ -2325,75 +1379,10 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 gr[3] = -o * Sdxy;
                 gr[4] = -0.5f * o * Sdyy;
                 gr[5] = S0;
-#if LSR_BWD_VMOM
                 gr[6] = C0;
                 gr[7] = C1;
                 gr[8] = C2;
-#endif
             }
-#else
-            // phase 3: the group's gradients on MFMA
-            f32x4 mom = {0.f, 0.f, 0.f, 0.f};
-            f32x4 ch[NBC];
-#pragma unroll
-            for (int nb = 0; nb < NBC; nb++) ch[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int t = 0; t < 16; t++) {
-                const float au = sDU[li * GS + 4 * t + lg];
-                const float aa = sAT[li * GS + 4 * t + lg];
-                // moment li of block pixel q = 4t + lg (relative to the block centre)
-                const float lx = (float)(((4 * t) & 7) + lg) - 3.5f, ly = (float)(t >> 1) - 3.5f;
-                float m = li == 0 ? 1.f : 0.f;
-                m = li == 1 ? lx : m;
-                m = li == 2 ? ly : m;
-                m = li == 3 ? lx * lx : m;
-                m = li == 4 ? lx * ly : m;
-                m = li == 5 ? ly * ly : m;
-                mom = BWD_MFMA(au, m, mom);
-#pragma unroll
-                for (int nb = 0; nb < NBC; nb++)
-                    ch[nb] = BWD_MFMA(aa, chB[nb][t], ch[nb]);
-            }
-            // Gradient rows of the group staged in LDS (row layout of lsr_device.h:
-            // [0..5] geometry, [6..8] colour, [12..) language), then added with
-            // line-coalesced atomics: each 16-lane group covers one 64-B line of
-            // one Gaussian's row.
-            // colour / language: lane holds slot 4*lg+r, channel nb*16+li
-#pragma unroll
-            for (int nb = 0; nb < NBC; nb++) {
-                const int chn = nb * 16 + li;
-                if (chn < 3 + NL) {
-                    const int col = chn < 3 ? 6 + chn : LSR_GROW_LANG + chn - 3;
-#pragma unroll
-                    for (int r = 0; r < 4; r++) sGr[(4 * lg + r) * GRS + col] = ch[nb][r];
-                }
-            }
-            if (li < 6) {
-#pragma unroll
-                for (int r = 0; r < 4; r++) sMom[(4 * lg + r) * LSR_MOM_STRIDE + li] = mom[r];
-            }
-            wave_lds_fence();
-            if (lane < kn) {
-                const int j = g0 + lane;
-                const float4 A = st.A[j];
-                const float4 B = st.B[j];
-                const float* M = sMom + lane * LSR_MOM_STRIDE;
-                const float S0 = M[0], S1 = M[1], S2 = M[2], S3 = M[3], S4 = M[4], S5 = M[5];
-                const float X = A.x - cx, Y = A.y - cy;
-                const float Sdx = fmaf(X, S0, -S1), Sdy = fmaf(Y, S0, -S2);
-                const float Sdxx = fmaf(X, fmaf(X, S0, -2.f * S1), S3);
-                const float Sdxy = fmaf(X, fmaf(Y, S0, -S2), fmaf(-Y, S1, S4));
-                const float Sdyy = fmaf(Y, fmaf(Y, S0, -2.f * S2), S5);
-                const float o = B.y;
-                float* gr = sGr + lane * GRS;
-                gr[0] = -o * ddelx_dx * fmaf(A.z, Sdx, A.w * Sdy);
-                gr[1] = -o * ddely_dy * fmaf(B.x, Sdy, A.w * Sdx);
-                gr[2] = -0.5f * o * Sdxx;
-                gr[3] = -o * Sdxy;
-                gr[4] = -0.5f * o * Sdyy;
-                gr[5] = S0;
-            }
-#endif
             wave_lds_fence();
             BWD_STAMP(5);
             if constexpr (SP) {
@@ -2411,7 +1400,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                     }
                 }
             } else {
-#if LSR_BWD_ATOM_BATCH
                 // every value and id the group's atomics need is read from LDS
                 // first (one wait), then the atomics issue back to back
                 uint32_t gq[4];
@@ -2424,14 +1412,11 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 for (int h = 0; h < GRL; h++)
 #pragma unroll
                     for (int q = 0; q < 4; q++) {
-#if LSR_BWD_VMOM
                         if (RREG && h > 0)
                             vq[h][q] = ch[h - 1][q];
                         else
-#endif
                             vq[h][q] = sGr[slot_of(q) * GRS + 16 * h + li];
                     }
-#if LSR_BWD_BUF_ATOM
                 if (buf_atom) {
                     // buffer atomics: 32-bit offsets, and a lane with nothing
                     // to add gets an offset past the buffer (the range check
@@ -2457,7 +1442,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                         }
                     }
                 } else
-#endif
 #pragma unroll
                 for (int h = 0; h < GRL; h++) {
                     const int f = 16 * h + li;
@@ -2475,26 +1459,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                         }
                     }
                 }
-#else
-#pragma unroll
-                for (int h = 0; h < GRL; h++) {
-                    const int f = 16 * h + li;
-                    const bool fcol = LO ? (f < D)
-                                      : LD ? (h == 0 ? (f < 9) : (f - 16 < D))
-                                           : ((f < 9) | ((f >= LSR_GROW_LANG) & (f < LSR_GROW_LANG + D)));
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const int slot = 4 * q + lg;
-                        const float v = sGr[slot * GRS + f];
-                        if (fcol & (slot < kn) & (v != 0.f)) {
-                            if (LD && h > 0)
-                                LSR_MF_ATOMIC(b.lang_acc + (size_t)st.gid[g0 + slot] * D + (f - 16), v);
-                            else
-                                LSR_MF_ATOMIC(b.grad_acc + (size_t)st.gid[g0 + slot] * VP + f, v);
-                        }
-                    }
-                }
-#endif
             }
             wave_lds_fence();
             BWD_STAMP(6);
@@ -2695,405 +1659,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_fwd_mf(RenderArgs a
 }
 
 
-// ------------------------------------------------ MFMA quick (sparse) forward ----
-// Sparse language channels: each Gaussian carries K (weight, code) pairs into
-// Dq output channels.  Per group of 16 candidates the pairs are expanded into
-// a dense 16 x Dq tile in LDS and accumulated out[q][p] += W[k][q] * aT[k][p]
-// on MFMA with the candidates as K in front-to-back order: bit-identical to the
-// sequential per-pixel blend (f32 MFMA == fmaf chain; unused codes add
-// fmaf(0, aT, acc) == acc).  Codes within one Gaussian must be distinct (as
-// utils/vq_utils.py:get_weights_and_indices produces them); a repeated code
-// would be summed before the multiply.  RGB stays on the VALU (phase 2).
-struct WaveStageQ {
-    float4 A[80];
-    float4 B[80];         // .w = 1-based tile-list position (int bits)
-    float4 C[80];         // rgb
-    uint32_t gid[80];
-};
-
-template <int QB>   // one slab of 16 * QB output channels per wave (blockIdx.y = slab)
-__global__ void __launch_bounds__(64) k_render_fwd_quick_mf(RenderArgs a)
-{
-    constexpr int DQ = 16 * QB;
-    const int q0 = (int)blockIdx.y * DQ;
-    const bool slab0 = blockIdx.y == 0;
-    constexpr int FS = LSR_FWD_STRIDE;
-    __shared__ WaveStageQ st;
-    __shared__ float sAT[16 * FS];
-    __shared__ float sWd[16 * DQ];    // dense weights of the group's candidates
-    __shared__ float sT[64];
-
-    const Cam& c = a.cam;
-    const WaveTile wt(c);
-    const int lane = threadIdx.x;
-    const int lg = lane >> 4, li = lane & 15;
-    const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
-    const bool inside = pm.px < c.W && pm.py < c.H;
-    const float pfx = (float)pm.px, pfy = (float)pm.py;
-    const uint32_t rs = a.tile_start[wt.tile], re = a.tile_start[wt.tile + 1];
-    const int K = a.K;
-
-    for (int e = lane; e < 80; e += 64) {
-        st.A[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-        st.B[e] = make_float4(0.f, 0.f, 0.f, __int_as_float(0));
-        st.C[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-        st.gid[e] = 0u;
-    }
-
-    float T = 1.0f, cr = 0.f, cg = 0.f, cbl = 0.f;
-    uint32_t last = 0;
-    bool done = !inside;
-    f32x4 acc[QB][4];
-#pragma unroll
-    for (int qb = 0; qb < QB; qb++)
-#pragma unroll
-        for (int pb = 0; pb < 4; pb++) acc[qb][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    int carry = 0;
-    uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
-    for (uint32_t base = rs; base < re; base += 64) {
-        if (wave_ballot(!done) == 0) break;
-        const uint32_t idx = base + lane;
-        const bool valid = idx < re;
-        const uint32_t gid = next_gid;
-        next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;
-        int nnew;
-        {
-            float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
-            if (valid) {
-                A = a.splatA[gid];
-                B = a.splatB[gid];
-            }
-            const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), pm.bx, pm.by) &&
-                            block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, pm.bx, pm.by);
-            const uint64_t m = wave_ballot(ok);
-            if (ok) {
-                const int r = carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                st.A[r] = A;
-                st.B[r] = make_float4(B.x, B.y, B.z, __int_as_float((int)(idx - rs) + 1));
-                st.C[r] = make_float4(a.rgb[3 * (size_t)gid], a.rgb[3 * (size_t)gid + 1], a.rgb[3 * (size_t)gid + 2], 0.f);
-                st.gid[r] = gid;
-            }
-            wave_lds_fence();
-            nnew = __popcll(m);
-        }
-        const int n = carry + nnew;
-        const int nfull = (base + 64 >= re) ? n : (n & ~15);
-        bool all_done = false;
-        for (int g0 = 0; g0 < nfull; g0 += 16) {
-            if (wave_ballot(!done) == 0) {
-                all_done = true;
-                break;
-            }
-            const int kn = min(16, nfull - g0);
-            // the group's (weight, code) pairs: loads issued now, scattered into
-            // the dense tile after phases 1-2 (which hide their latency)
-            constexpr int PE = (16 * LSR_QUICK_KMAX + 63) / 64;   // pairs per lane
-            float pw[PE];
-            int pq[PE];
-#pragma unroll
-            for (int i = 0; i < PE; i++) {
-                const int e = lane + 64 * i;
-                const int k = e / K, j = e - k * K;
-                pq[i] = -1;
-                pw[i] = 0.f;
-                if (e < 16 * K && k < kn) {
-                    const size_t off = (size_t)st.gid[g0 + k] * K + j;
-                    int q;
-                    if (a.qidx_dtype == LSR_INDEX_F32) q = f2i(((const float*)a.qi)[off] + 0.5f);
-                    else if (a.qidx_dtype == LSR_INDEX_I32) q = ((const int32_t*)a.qi)[off];
-                    else q = (int)((const int64_t*)a.qi)[off];
-                    pw[i] = a.qw[off];
-                    pq[i] = (q >= q0 && q < q0 + DQ && q < a.Dq) ? k * DQ + (q - q0) : -1;
-                }
-            }
-            for (int e = lane; e < 16 * DQ / 4; e += 64) reinterpret_cast<float4*>(sWd)[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-            // phase 1: alpha of the 16 candidates (0 = skipped), independent
-#pragma unroll 4
-            for (int k = 0; k < 16; k++) {
-                const float4 A = st.A[g0 + k];
-                const float4 B = st.B[g0 + k];
-                const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
-                const bool cut = (k < kn) & !(power > 0.0f) & !(power < B.z);
-                const float alpha = fminf(0.99f, B.y * expf_det(power));
-                sAT[k * FS + lane] = (cut & !(alpha < 1.0f / 255.0f)) ? alpha : 0.f;
-            }
-            // phase 2: serial transmittance, termination, RGB per pixel
-#pragma unroll 4
-            for (int k = 0; k < 16; k++) {
-                const float al = sAT[k * FS + lane];
-                const float4 B = st.B[g0 + k];
-                const float4 Cc = st.C[g0 + k];
-                bool ok = (al != 0.f) & !done;
-                const float test_T = T * (1.0f - al);
-                const bool term = ok & (test_T < 0.0001f);
-                done = done | term;
-                ok = ok & !term;
-                const float aT = ok ? al * T : 0.f;
-                if (ok) {
-                    cr = fmaf(Cc.x, aT, cr);
-                    cg = fmaf(Cc.y, aT, cg);
-                    cbl = fmaf(Cc.z, aT, cbl);
-                }
-                sAT[k * FS + lane] = aT;
-                T = ok ? test_T : T;
-                last = ok ? (uint32_t)__float_as_int(B.w) : last;
-            }
-            wave_lds_fence();   // zeroed tile before the scatter
-#pragma unroll
-            for (int i = 0; i < PE; i++)
-                if (pq[i] >= 0) sWd[pq[i]] = pw[i];
-            wave_lds_fence();
-            // phase 3: out[q][p] += W[k][q] * aT[k][p] on MFMA, k in order
-#pragma unroll
-            for (int t = 0; t < 4; t++) {
-                float bv[4];
-#pragma unroll
-                for (int pb = 0; pb < 4; pb++) bv[pb] = sAT[(4 * t + lg) * FS + pb * 16 + li];
-#pragma unroll
-                for (int qb = 0; qb < QB; qb++) {
-                    const float av = sWd[(4 * t + lg) * DQ + qb * 16 + li];
-#pragma unroll
-                    for (int pb = 0; pb < 4; pb++)
-                        acc[qb][pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[pb], acc[qb][pb], 0, 0, 0);
-                }
-            }
-            wave_lds_fence();
-        }
-        if (all_done) break;
-        carry = n - nfull;
-        if (nfull > 0 && lane < carry) {   // source >= 16 > destination: no overlap
-            st.A[lane] = st.A[nfull + lane];
-            st.B[lane] = st.B[nfull + lane];
-            st.C[lane] = st.C[nfull + lane];
-            st.gid[lane] = st.gid[nfull + lane];
-        }
-        wave_lds_fence();
-    }
-    const size_t HW = (size_t)c.H * c.W;
-    if (inside && slab0) {
-        const size_t pix = (size_t)pm.py * c.W + pm.px;
-        a.final_T[pix] = T;
-        a.n_contrib[pix] = last;
-        a.out_color[pix] = fmaf(T, c.bg[0], cr);
-        a.out_color[HW + pix] = fmaf(T, c.bg[1], cg);
-        a.out_color[2 * HW + pix] = fmaf(T, c.bg[2], cbl);
-    }
-    // lane (lg, li) holds channel qb*16 + 4*lg + r of block pixel pb*16 + li
-#pragma unroll
-    for (int pb = 0; pb < 4; pb++) {
-        const int q = pb * 16 + li;
-        const int qx = pm.bx + (q & 7), qy = pm.by + (q >> 3);
-        if (qx < c.W && qy < c.H) {
-            const size_t pix = (size_t)qy * c.W + qx;
-#pragma unroll
-            for (int qb = 0; qb < QB; qb++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int ch = q0 + qb * 16 + 4 * lg + r;
-                    if (ch < a.Dq) a.out_lang[(size_t)ch * HW + pix] = acc[qb][pb][r];
-                }
-        }
-    }
-}
-
-
-// Quick path, one workgroup of NS waves per 8x8 block: wave 0 stages the
-// candidates and runs the blend phases (alpha, serial T, RGB) once; every wave
-// then scatters the (weight, code) pairs of its 16*QB-channel slab into a
-// dense tile and accumulates its slab on MFMA.  Same arithmetic, order and
-// bit-exactness as k_render_fwd_quick_mf, without re-running the blend per slab.
-template <int QB, int NS>
-__global__ void __launch_bounds__(64 * NS) k_render_fwd_quick_wg(RenderArgs a)
-{
-    constexpr int DQ = 16 * QB;
-    constexpr int FS = LSR_FWD_STRIDE;
-    constexpr int PE = (16 * LSR_QUICK_KMAX + 63) / 64;
-    __shared__ WaveStageQ st;
-    __shared__ float sAT[16 * FS];
-    __shared__ float sWd[NS][16 * DQ];
-    __shared__ int sN[2];
-
-    const Cam& c = a.cam;
-    const WaveTile wt(c);
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int lg = lane >> 4, li = lane & 15;
-    const int q0 = w * DQ;
-    const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
-    const bool inside = pm.px < c.W && pm.py < c.H;
-    const float pfx = (float)pm.px, pfy = (float)pm.py;
-    const uint32_t rs = a.tile_start[wt.tile], re = a.tile_start[wt.tile + 1];
-    const int K = a.K;
-
-    if (w == 0) {
-        for (int e = lane; e < 80; e += 64) {
-            st.A[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-            st.B[e] = make_float4(0.f, 0.f, 0.f, __int_as_float(0));
-            st.C[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-            st.gid[e] = 0u;
-        }
-    }
-    float T = 1.0f, cr = 0.f, cg = 0.f, cbl = 0.f;
-    uint32_t last = 0;
-    bool done = !inside;
-    f32x4 acc[QB][4];
-#pragma unroll
-    for (int qb = 0; qb < QB; qb++)
-#pragma unroll
-        for (int pb = 0; pb < 4; pb++) acc[qb][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    int carry = 0;
-    uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
-    for (uint32_t base = rs; base < re; base += 64) {
-        if (w == 0) {
-            const bool stop = wave_ballot(!done) == 0;
-            int nnew = 0;
-            if (!stop) {
-                const uint32_t idx = base + lane;
-                const bool valid = idx < re;
-                const uint32_t gid = next_gid;
-                next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;
-                float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
-                if (valid) {
-                    A = a.splatA[gid];
-                    B = a.splatB[gid];
-                }
-                const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), pm.bx, pm.by) &&
-                                block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, pm.bx, pm.by);
-                const uint64_t m = wave_ballot(ok);
-                if (ok) {
-                    const int r = carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    st.A[r] = A;
-                    st.B[r] = make_float4(B.x, B.y, B.z, __int_as_float((int)(idx - rs) + 1));
-                    st.C[r] = make_float4(a.rgb[3 * (size_t)gid], a.rgb[3 * (size_t)gid + 1],
-                                          a.rgb[3 * (size_t)gid + 2], 0.f);
-                    st.gid[r] = gid;
-                }
-                nnew = __popcll(m);
-            }
-            if (lane == 0) {
-                sN[0] = stop ? -1 : carry + nnew;
-            }
-        }
-        __syncthreads();
-        const int n = sN[0];
-        if (n < 0) break;
-        const int nfull = (base + 64 >= re) ? n : (n & ~15);
-        for (int g0 = 0; g0 < nfull; g0 += 16) {
-            const int kn = min(16, nfull - g0);
-            // this slab's (weight, code) pairs: loads issued now, scattered after the blend
-            float pw[PE];
-            int pq[PE];
-#pragma unroll
-            for (int i = 0; i < PE; i++) {
-                const int e = lane + 64 * i;
-                const int k = e / K, j = e - k * K;
-                pq[i] = -1;
-                pw[i] = 0.f;
-                if (e < 16 * K && k < kn) {
-                    const size_t off = (size_t)st.gid[g0 + k] * K + j;
-                    int q;
-                    if (a.qidx_dtype == LSR_INDEX_F32) q = f2i(((const float*)a.qi)[off] + 0.5f);
-                    else if (a.qidx_dtype == LSR_INDEX_I32) q = ((const int32_t*)a.qi)[off];
-                    else q = (int)((const int64_t*)a.qi)[off];
-                    pw[i] = a.qw[off];
-                    pq[i] = (q >= q0 && q < q0 + DQ && q < a.Dq) ? k * DQ + (q - q0) : -1;
-                }
-            }
-            for (int e = lane; e < 16 * DQ / 4; e += 64) reinterpret_cast<float4*>(sWd[w])[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (w == 0) {
-                // phase 1: alpha of the 16 candidates (0 = skipped), independent
-#pragma unroll 4
-                for (int k = 0; k < 16; k++) {
-                    const float4 A = st.A[g0 + k];
-                    const float4 B = st.B[g0 + k];
-                    const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
-                    const bool cut = (k < kn) & !(power > 0.0f) & !(power < B.z);
-                    const float alpha = fminf(0.99f, B.y * expf_det(power));
-                    sAT[k * FS + lane] = (cut & !(alpha < 1.0f / 255.0f)) ? alpha : 0.f;
-                }
-                // phase 2: serial transmittance, termination, RGB per pixel
-#pragma unroll 4
-                for (int k = 0; k < 16; k++) {
-                    const float al = sAT[k * FS + lane];
-                    const float4 B = st.B[g0 + k];
-                    const float4 Cc = st.C[g0 + k];
-                    bool ok = (al != 0.f) & !done;
-                    const float test_T = T * (1.0f - al);
-                    const bool term = ok & (test_T < 0.0001f);
-                    done = done | term;
-                    ok = ok & !term;
-                    const float aT = ok ? al * T : 0.f;
-                    if (ok) {
-                        cr = fmaf(Cc.x, aT, cr);
-                        cg = fmaf(Cc.y, aT, cg);
-                        cbl = fmaf(Cc.z, aT, cbl);
-                    }
-                    sAT[k * FS + lane] = aT;
-                    T = ok ? test_T : T;
-                    last = ok ? (uint32_t)__float_as_int(B.w) : last;
-                }
-            }
-            wave_lds_fence();   // this wave's zeroed slab tile before its scatter
-#pragma unroll
-            for (int i = 0; i < PE; i++)
-                if (pq[i] >= 0) sWd[w][pq[i]] = pw[i];
-            __syncthreads();    // aT tile (wave 0) and every slab tile complete
-            // phase 3: out[q][p] += W[k][q] * aT[k][p] on MFMA, k in order
-#pragma unroll
-            for (int t = 0; t < 4; t++) {
-                float bv[4];
-#pragma unroll
-                for (int pb = 0; pb < 4; pb++) bv[pb] = sAT[(4 * t + lg) * FS + pb * 16 + li];
-#pragma unroll
-                for (int qb = 0; qb < QB; qb++) {
-                    const float av = sWd[w][(4 * t + lg) * DQ + qb * 16 + li];
-#pragma unroll
-                    for (int pb = 0; pb < 4; pb++)
-                        acc[qb][pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[pb], acc[qb][pb], 0, 0, 0);
-                }
-            }
-            __syncthreads();    // before the next group overwrites the tiles
-        }
-        if (w == 0) {
-            carry = n - nfull;
-            if (nfull > 0 && lane < carry) {   // source >= 16 > destination: no overlap
-                st.A[lane] = st.A[nfull + lane];
-                st.B[lane] = st.B[nfull + lane];
-                st.C[lane] = st.C[nfull + lane];
-                st.gid[lane] = st.gid[nfull + lane];
-            }
-        }
-        __syncthreads();
-    }
-    const size_t HW = (size_t)c.H * c.W;
-    if (inside && w == 0) {
-        const size_t pix = (size_t)pm.py * c.W + pm.px;
-        a.final_T[pix] = T;
-        a.n_contrib[pix] = last;
-        a.out_color[pix] = fmaf(T, c.bg[0], cr);
-        a.out_color[HW + pix] = fmaf(T, c.bg[1], cg);
-        a.out_color[2 * HW + pix] = fmaf(T, c.bg[2], cbl);
-    }
-#pragma unroll
-    for (int pb = 0; pb < 4; pb++) {
-        const int q = pb * 16 + li;
-        const int qx = pm.bx + (q & 7), qy = pm.by + (q >> 3);
-        if (qx < c.W && qy < c.H) {
-            const size_t pix = (size_t)qy * c.W + qx;
-#pragma unroll
-            for (int qb = 0; qb < QB; qb++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int ch = q0 + qb * 16 + 4 * lg + r;
-                    if (ch < a.Dq) a.out_lang[(size_t)ch * HW + pix] = acc[qb][pb][r];
-                }
-        }
-    }
-}
-
 hipError_t launch_render_bwd_lang(const RenderBwdArgs& b, hipStream_t st)
 {
     const int T = b.f.cam.gx * b.f.cam.gy;
@@ -3139,7 +1704,7 @@ namespace lsr {
 
 bool bwd_lang_direct(int D)
 {
-    return LSR_BWD_MF && LSR_BWD_VMOM && LSR_BWD_LANG_DIRECT && (D == 16 || (D == 32 && LSR_BWD_MF_WIDE));
+    return D == 16 || D == 32;
 }
 
 hipError_t launch_render_bwd(const RenderBwdArgs& b, hipStream_t st)
@@ -3148,33 +1713,17 @@ hipError_t launch_render_bwd(const RenderBwdArgs& b, hipStream_t st)
     if (T == 0) return hipSuccess;
     if (b.lang_acc) {
         if (!bwd_lang_direct(b.f.D) || (uintptr_t)b.f.lang % 16 != 0) return hipErrorInvalidValue;
-#if LSR_BWD_MF && LSR_BWD_VMOM
         if (b.f.D == 16) k_render_bwd_mf<16, false, true><<<4 * T, 64, 0, st>>>(b);
-#if LSR_BWD_MF_WIDE
         else k_render_bwd_mf<32, false, true><<<4 * T, 64, 0, st>>>(b);
-#endif
-#endif
         return hipGetLastError();
     }
     switch (lang_set_for(b.f.D)) {
-#if LSR_BWD_MF
         case 0: k_render_bwd_mf<0><<<4 * T, 64, 0, st>>>(b); break;
         case 4: k_render_bwd_mf<4><<<4 * T, 64, 0, st>>>(b); break;
         case 8: k_render_bwd_mf<8><<<4 * T, 64, 0, st>>>(b); break;
         case 16: k_render_bwd_mf<16><<<4 * T, 64, 0, st>>>(b); break;
-#else
-        case 0: k_render_bwd<0><<<4 * T, 64, 0, st>>>(b); break;
-        case 4: k_render_bwd<4><<<4 * T, 64, 0, st>>>(b); break;
-        case 8: k_render_bwd<8><<<4 * T, 64, 0, st>>>(b); break;
-        case 16: k_render_bwd<16><<<4 * T, 64, 0, st>>>(b); break;
-#endif
-#if LSR_BWD_MF_WIDE
         case 32: k_render_bwd_mf<32><<<4 * T, 64, 0, st>>>(b); break;
         case 64: k_render_bwd_mf<64><<<4 * T, 64, 0, st>>>(b); break;
-#else
-        case 32: k_render_bwd<32><<<4 * T, 64, 0, st>>>(b); break;
-        case 64: k_render_bwd<64><<<4 * T, 64, 0, st>>>(b); break;
-#endif
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
