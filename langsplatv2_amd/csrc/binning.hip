@@ -221,9 +221,13 @@ __global__ void __launch_bounds__(256) k_duplicate(Cam c, int P, const uint8_t* 
     int x0, y0, x1, y1;
     get_rect(A.x, A.y, r, c.gx, c.gy, x0, y0, x1, y1);
     const CutEllipse e = tile_cull_prep(A, B);
+    int bx0 = x0, by0 = y0, bx1 = x1, by1 = y1;
+    cull_box(A.x, A.y, A.z, A.w, B.x, B.z, bx0, by0, bx1, by1);
     for (int y = y0; y < y1; y++)
-        for (int x = x0; x < x1; x++, o++)
-            rank[o] = tile_keep(e, x, y) ? atomicAdd(&tile_cnt[y * c.gx + x], 1u) : 0xffffffffu;
+        for (int x = x0; x < x1; x++, o++) {
+            const bool in = x >= bx0 && x < bx1 && y >= by0 && y < by1;
+            rank[o] = (in && tile_keep(e, x, y)) ? atomicAdd(&tile_cnt[y * c.gx + x], 1u) : 0xffffffffu;
+        }
 }
 
 hipError_t launch_duplicate(const Cam& c, int P, const uint8_t* geom, const int32_t* radii, uint32_t* tile_cnt,
@@ -380,21 +384,36 @@ struct RectWalk {
     __device__ __forceinline__ bool keep(int ty0) const { return tile_keep(e, x, y + ty0); }
 };
 
+// One Gaussian's binning inputs (radius, the two splat records, depth),
+// loaded one wave iteration ahead of their use (LSR_BIN_PF): the walk of
+// iteration k runs while iteration k + 1's records are in flight, instead of
+// every iteration waiting for a dependent radius -> record gather.  Lanes
+// past the chunk read Gaussian g1 - 1 (a valid address) and get radius 0.
+struct BinRec {
+    int r;
+    float4 A, B;
+    float depth;
+    __device__ __forceinline__ void load(const uint8_t* geom, int P, int g1, const int32_t* __restrict__ radii, int i,
+                                         bool with_depth)
+    {
+        const GeomLayout L = geom_layout(P);
+        const int q = min(i, g1 - 1);
+        const int rr = radii[q];
+        A = ((const float4*)(geom + L.splatA))[q];
+        B = ((const float4*)(geom + L.splatB))[q];
+        depth = with_depth ? ((const float*)(geom + L.depth))[q] : 0.f;
+        r = i < g1 ? rr : 0;
+    }
+};
+
 // Lane's Gaussian -> its rect clipped to the band (n = 0 if none).
-__device__ __forceinline__ int band_rect(const Cam& c, const Band& bd, const uint8_t* geom, int P, int g1,
-                                         const int32_t* __restrict__ radii, int i, int& x0, int& y0, int& w,
-                                         float4& A, float4& B)
+__device__ __forceinline__ int band_rect(const Cam& c, const Band& bd, const BinRec& g, int& x0, int& y0, int& w)
 {
     x0 = y0 = w = 0;
-    A = B = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i >= g1) return 0;
-    const int r = radii[i];
-    if (r <= 0) return 0;
+    if (g.r <= 0) return 0;
     int x1, y1;
-    const GeomLayout L = geom_layout(P);
-    A = ((const float4*)(geom + L.splatA))[i];
-    B = ((const float4*)(geom + L.splatB))[i];
-    get_rect(A.x, A.y, r, c.gx, c.gy, x0, y0, x1, y1);
+    get_rect(g.A.x, g.A.y, g.r, c.gx, c.gy, x0, y0, x1, y1);
+    cull_box(g.A.x, g.A.y, g.A.z, g.A.w, g.B.x, g.B.z, x0, y0, x1, y1);
     y0 = max(y0, bd.ty0);
     y1 = min(y1, bd.ty1);
     w = x1 - x0;
@@ -425,24 +444,37 @@ __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int r
     WaveRects& wr = wrs[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     const int g0 = blk * chunk, g1 = min(P, g0 + chunk);
+#ifdef LSR_PROBE_CNT
+    uint32_t probe_acc = 0;
+#endif
+    BinRec nx;
+    if (g0 < g1) nx.load(geom, P, g1, radii, g0 + (threadIdx.x & ~63) + lane, false);
     for (int i0 = g0 + (threadIdx.x & ~63); i0 < g1; i0 += BB) {
+        const BinRec cur = nx;
+        nx.load(geom, P, g1, radii, i0 + BB + lane, false);
         int x0, y0, w;
-        float4 A, B;
-        const int n = band_rect(c, bd, geom, P, g1, radii, i0 + lane, x0, y0, w, A, B);
-        const int tot = wave_rects_stage(wr, n, x0, y0 - bd.ty0, w, A, B);
+        const int n = band_rect(c, bd, cur, x0, y0, w);
+        const int tot = wave_rects_stage(wr, n, x0, y0 - bd.ty0, w, cur.A, cur.B);
         const int q = (tot + 63) >> 6;
         int k = lane * q;
         const int kend = min(tot, k + q);
         if (k < kend) {
             RectWalk rw(wr, k);
             for (;;) {
+#ifdef LSR_PROBE_CNT   // timing probe only (wrong counts): 1 = no LDS atomics, 2 = no tile-cull test either
+                if (LSR_PROBE_CNT == 1 ? rw.keep(bd.ty0) : true) probe_acc += (uint32_t)(rw.y * c.gx + rw.x);
+#else
                 if (rw.keep(bd.ty0)) atomicAdd(&hist[rw.y * c.gx + rw.x], 1u);
+#endif
                 if (++k >= kend) break;
                 rw.next(wr);
             }
         }
         wave_lds_fence();
     }
+#ifdef LSR_PROBE_CNT
+    if (probe_acc == 0xdeadbeefu) hist[0] = probe_acc;
+#endif
     __syncthreads();
     uint32_t* row = table + (size_t)blk * T + bd.t0;
     for (int k = threadIdx.x; k < bd.nt; k += BB) row[k] = hist[k];
@@ -516,18 +548,19 @@ __global__ void __launch_bounds__(BB) k_bin_scatter(Cam c, int P, int chunk, int
     const uint32_t* row = table + (size_t)blk * T + bd.t0;
     for (int k = threadIdx.x; k < bd.nt; k += BB) base[k] = tile_start[bd.t0 + k] + row[k];
     __syncthreads();
-    const GeomLayout L = geom_layout(P);
-    const float* depth = (const float*)(geom + L.depth);
     WaveRects& wr = wrs[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     const int g0 = blk * chunk, g1 = min(P, g0 + chunk);
+    BinRec nx;
+    if (g0 < g1) nx.load(geom, P, g1, radii, g0 + (threadIdx.x & ~63) + lane, true);
     for (int i0 = g0 + (threadIdx.x & ~63); i0 < g1; i0 += BB) {
         const int i = i0 + lane;
+        const BinRec cur = nx;
+        nx.load(geom, P, g1, radii, i0 + BB + lane, true);
         int x0, y0, w;
-        float4 A, B;
-        const int n = band_rect(c, bd, geom, P, g1, radii, i, x0, y0, w, A, B);
-        if (n > 0) wr.key[lane] = ((uint64_t)__float_as_uint(depth[i]) << 32) | (uint32_t)i;
-        const int tot = wave_rects_stage(wr, n, x0, y0 - bd.ty0, w, A, B);
+        const int n = band_rect(c, bd, cur, x0, y0, w);
+        if (n > 0) wr.key[lane] = ((uint64_t)__float_as_uint(cur.depth) << 32) | (uint32_t)i;
+        const int tot = wave_rects_stage(wr, n, x0, y0 - bd.ty0, w, cur.A, cur.B);
         const int q = (tot + 63) >> 6;
         int k = lane * q;
         const int kend = min(tot, k + q);

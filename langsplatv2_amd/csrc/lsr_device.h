@@ -396,6 +396,35 @@ __device__ __forceinline__ bool block_overlap_exact(float x, float y, float ca, 
 #ifndef LSR_TILE_CULL
 #define LSR_TILE_CULL 1     // 0: the reference's full rect lists (A/B timing only; the oracle's cull=False)
 #endif
+// The tile cull's box: the tiles whose 16x16 pixel rectangle meets the
+// axis-aligned box of the cut ellipse {q <= thr} (q, thr as in CutEllipse),
+// widened by 1e-4 relative + 0.5 px.  The cull keeps an instance (Gaussian,
+// tile) iff the tile is inside this box AND the exact test meets() passes;
+// the binning walks only the box (fewer instances visited and tested than in
+// the 3-sigma rect), the oracle restates the same rule (lso_cull_box).  A
+// tile outside the box cannot meet the ellipse, so nothing that contributes
+// is dropped (tests/test_oracle.py::test_tile_cull_changes_no_output,
+// tests/test_cull_vs_full.py).  Shrinks [x0, x1) x [y0, y1) in place.
+__device__ __forceinline__ void cull_box(float x, float y, float ca, float cb, float cc, float cut, int& x0, int& y0,
+                                         int& x1, int& y1)
+{
+    if (!LSR_TILE_CULL) return;
+    if (!(ca > 0.f) || !(cc > 0.f) || !(cut > -3.0e38f)) return;
+    const float det = ca * cc - cb * cb;
+    if (!(det > 0.f)) return;
+    const float thr = fmaf(-2.f * cut, 1.001f, 1e-3f);
+    const float ue = fmaf(sqrtf(thr * cc / det), 1.0001f, 0.5f);
+    const float ve = fmaf(sqrtf(thr * ca / det), 1.0001f, 0.5f);
+    if (!(ue < 1.0e7f) || !(ve < 1.0e7f)) return;
+    // tile t meets [x - ue, x + ue] iff 16 t <= x + ue and 16 t + 15 >= x - ue
+    const float tx0 = ceilf((x - ue - 15.f) / 16.f), tx1 = floorf((x + ue) / 16.f) + 1.f;
+    const float ty0 = ceilf((y - ve - 15.f) / 16.f), ty1 = floorf((y + ve) / 16.f) + 1.f;
+    x0 = max(x0, f2i(fmaxf(tx0, -1.f)));
+    y0 = max(y0, f2i(fmaxf(ty0, -1.f)));
+    x1 = min(x1, f2i(fmaxf(tx1, -1.f)));
+    y1 = min(y1, f2i(fmaxf(ty1, -1.f)));
+}
+
 __device__ __forceinline__ CutEllipse tile_cull_prep(const float4& A, const float4& B)
 {
     return CutEllipse(A.x, A.y, A.z, A.w, B.x, B.z);

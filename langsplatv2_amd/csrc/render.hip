@@ -28,6 +28,9 @@
 #ifndef LSR_BWD_SPLAT_PF
 #define LSR_BWD_SPLAT_PF 1  // bwd: chunk records loaded one chunk ahead (ids two ahead), D <= 32
 #endif
+#ifndef LSR_FWD_T0
+#define LSR_FWD_T0 0
+#endif
 #ifndef LSR_MF_WAVES
 #define LSR_MF_WAVES 2      // MFMA render kernels: min waves per SIMD (caps VGPRs at 256)
 #endif
@@ -108,10 +111,10 @@ __device__ __forceinline__ int band_tile(int t, int gx, int gy)
 }
 struct WaveTile {
     int tile, sub;
-    __device__ WaveTile(const Cam& c)
+    __device__ WaveTile(const RenderArgs& a)
     {
         const int o = xcd_remap(blockIdx.x, gridDim.x);
-        tile = band_tile(o >> 2, c.gx, c.gy);
+        tile = band_tile(o >> 2, a.cam.gx, a.cam.gy);
         sub = o & 3;
     }
 };
@@ -216,7 +219,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
     __shared__ WaveStageP<F4, SF> st;
 
     const Cam& c = a.cam;
-    const WaveTile wt(c);
+    const WaveTile wt(a);
     const int lane = threadIdx.x;
     const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
     const bool inside = pm.px < c.W && pm.py < c.H;
@@ -224,12 +227,17 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
     const uint32_t rs = a.tile_start[wt.tile], re = a.tile_start[wt.tile + 1];
     const int D = a.D;
 
+#if LSR_FWD_T0
+    float T = inside ? 1.0f : 0.f;   // 0 = finished (or outside the image)
+    float Tout = 0.f;                // a finished pixel's final T
+#else
     float T = 1.0f;
+    bool done = !inside;
+#endif
     float acc[F4 * 4];
 #pragma unroll
     for (int k = 0; k < F4 * 4; k++) acc[k] = 0.f;
     uint32_t last = 0;
-    bool done = !inside;
 
     uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
     // SPF: a chunk's ids are loaded two chunks ahead and its records one chunk
@@ -246,7 +254,11 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
         B1 = a.splatB[next_gid];
     }
     for (uint32_t base = rs; base < re; base += 64) {
+#if LSR_FWD_T0
+        if (wave_ballot(T > 0.f) == 0) break;
+#else
         if (wave_ballot(!done) == 0) break;
+#endif
         const uint32_t idx = base + lane;
         const bool valid = idx < re;
         const uint32_t gid = next_gid;
@@ -271,6 +283,82 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
         // blends it with weight 0 and keeps T.  The two exp chains are
         // independent (ILP); T carries from the first to the second exactly
         // as in the sequential per-pixel order.
+#if LSR_FWD_T0
+        // T0 form: a finished pixel carries T = 0 (its final T kept in Tout), so
+        // every later candidate is an exact no-op for it (alpha * 0 = 0, and the
+        // termination test stays true) without a per-pixel `done` mask; the
+        // wave's early exit is voted once per 8 candidates.  The exponent-cut
+        // test is dropped: below the cut alpha < e^-0.02 / 255 already fails
+        // the 1/255 test.  Per pixel the blend is the same sequence of
+        // operations, so the outputs are bit-identical.
+        int lastj = -1;
+        for (int j0 = 0; j0 < n; j0 += 2) {
+            if ((j0 & 7) == 0 && wave_ballot(T > 0.f) == 0) break;
+            const bool two = j0 + 1 < n;
+            const int j1 = two ? j0 + 1 : j0;
+            const int e = j0 >> 1;
+            float fr0[F4 * 4], fr1[F4 * 4];
+            if constexpr (SF) {
+                feature_row_uniform<NL, F4>(fr0, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j0]));
+                feature_row_uniform<NL, F4>(fr1, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j1]));
+            }
+            const f32x2 sX = st.X[e], sY = st.Y[e], sCA = st.CA[e], sCB = st.CB[e], sCC = st.CC[e];
+            const f32x2 OP = st.OP[e];
+            const f32x2 dx = sX - f32x2{pfx, pfx}, dy = sY - f32x2{pfy, pfy};
+            const f32x2 P = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f},
+                                                      __builtin_elementwise_fma(sCA * dx, dx, (sCC * dy) * dy),
+                                                      -((sCB * dx) * dy));
+            const f32x2 EX = expf_det2(P);
+            const float al0 = fminf(0.99f, OP.x * EX.x);
+            const float al1 = fminf(0.99f, OP.y * EX.y);
+            const float e0 = (!(P.x > 0.0f) && !(al0 < 1.0f / 255.0f)) ? al0 : 0.f;
+            const float e1 = (two && !(P.y > 0.0f) && !(al1 < 1.0f / 255.0f)) ? al1 : 0.f;
+            {
+                const float test_T = T * (1.0f - e0);
+                const bool term = test_T < 0.0001f;
+                const bool ok = (e0 != 0.f) & !term;
+                Tout = (term & (T > 0.f)) ? T : Tout;
+                const float aT = ok ? e0 * T : 0.f;
+                if constexpr (SF) {
+#pragma unroll
+                    for (int k = 0; k < F4 * 4; k++) acc[k] = fmaf(fr0[k], aT, acc[k]);
+                } else {
+#pragma unroll
+                    for (int f = 0; f < F4; f++) {
+                        const float4 v = st.F[j0 * F4 + f];
+                        acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
+                        acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
+                        acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
+                        acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
+                    }
+                }
+                T = term ? 0.f : test_T;
+                lastj = ok ? j0 : lastj;
+            }
+            {
+                const float test_T = T * (1.0f - e1);
+                const bool term = test_T < 0.0001f;
+                const bool ok = (e1 != 0.f) & !term;
+                Tout = (term & (T > 0.f)) ? T : Tout;
+                const float aT = ok ? e1 * T : 0.f;
+                if constexpr (SF) {
+#pragma unroll
+                    for (int k = 0; k < F4 * 4; k++) acc[k] = fmaf(fr1[k], aT, acc[k]);
+                } else {
+#pragma unroll
+                    for (int f = 0; f < F4; f++) {
+                        const float4 v = st.F[j1 * F4 + f];
+                        acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
+                        acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
+                        acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
+                        acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
+                    }
+                }
+                T = term ? 0.f : test_T;
+                lastj = ok ? j1 : lastj;
+            }
+        }
+#else
         int lastj = -1;   // LASTJ: staged index of the chunk's last contributor
         for (int j0 = 0; j0 < n; j0 += 2) {
             if (wave_ballot(!done) == 0) break;
@@ -285,11 +373,12 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 feature_row_uniform<NL, F4>(fr0, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j0]));
                 feature_row_uniform<NL, F4>(fr1, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j1]));
             }
-            const f32x2 dx = st.X[e] - f32x2{pfx, pfx}, dy = st.Y[e] - f32x2{pfy, pfy};
-            const f32x2 P = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f},
-                                                      __builtin_elementwise_fma(st.CA[e] * dx, dx, (st.CC[e] * dy) * dy),
-                                                      -((st.CB[e] * dx) * dy));
+            const f32x2 sX = st.X[e], sY = st.Y[e], sCA = st.CA[e], sCB = st.CB[e], sCC = st.CC[e];
             const f32x2 CUT = st.CUT[e], OP = st.OP[e];
+            const f32x2 dx = sX - f32x2{pfx, pfx}, dy = sY - f32x2{pfy, pfy};
+            const f32x2 P = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f},
+                                                      __builtin_elementwise_fma(sCA * dx, dx, (sCC * dy) * dy),
+                                                      -((sCB * dx) * dy));
             const float p0 = P.x, p1 = P.y;
             bool ok0 = !done && !(p0 > 0.0f || p0 < CUT.x);
             bool ok1 = two && !done && !(p1 > 0.0f || p1 < CUT.y);
@@ -346,12 +435,16 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 lastj = ok1 ? j1 : lastj;
             }
         }
+#endif
         if (lastj >= 0) last = (uint32_t)st.pos[lastj];
         wave_lds_fence();
     }
     if (inside) {
         const size_t HW = (size_t)c.H * c.W;
         const size_t pix = (size_t)pm.py * c.W + pm.px;
+#if LSR_FWD_T0
+        if (!(T > 0.f)) T = Tout;
+#endif
         a.final_T[pix] = T;
         a.n_contrib[pix] = last;
 #pragma unroll
@@ -526,7 +619,7 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
     static_assert(NP >= 1 && NP <= 6, "up to 192 quick channels");
     __shared__ WaveStageV st;
     const Cam& c = a.cam;
-    const WaveTile wt(c);
+    const WaveTile wt(a);
     const int lane = threadIdx.x;
     const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
     const bool inside = pm.px < c.W && pm.py < c.H;
@@ -780,6 +873,12 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
 #ifndef LSR_GRP_STRIDE
 #define LSR_GRP_STRIDE 66   // dot/u and aT tiles: conflict-free A-fragment reads (li*66 mod 32 = 2 li)
 #endif
+#ifndef LSR_PROBE_ATOM_ON      // timing probe only: (false) every atomic's offset out of range (no memory traffic)
+#define LSR_PROBE_ATOM_ON(on) (on)
+#endif
+#ifndef LSR_PROBE_ATOM_ISSUE   // timing probe only: (0) no atomic instructions at all
+#define LSR_PROBE_ATOM_ISSUE 1
+#endif
 #define LSR_BUF_OOB 0x7ffffffc  // a byte offset past every buffer the backward addresses this way
 #define LSR_MOM9_STRIDE 12  // reduced moment + colour sums per candidate (16-B aligned rows)
 #define LSR_LOG2E 1.4426950408889634f
@@ -900,7 +999,9 @@ __device__ __forceinline__ void dot_features(const RenderArgs& a, uint32_t gid, 
     }
 }
 
-#ifdef LSR_EXP_NOMF   // timing experiment only (wrong results): no matrix-core work
+#if defined(LSR_EXP_NOMF2)   // timing experiment only (wrong results): a lane-wise FMA instead of each MFMA
+#define BWD_MFMA(a, b_, c) ((c) + f32x4{(a) * (b_), (a) + (b_), (a), (b_)})
+#elif defined(LSR_EXP_NOMF)   // timing experiment only (wrong results): no matrix-core work
 #define BWD_MFMA(a, b_, c) (c)
 #else
 #define BWD_MFMA(a, b_, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b_), (c), 0, 0, 0)
@@ -949,7 +1050,8 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     // six geometry moments are summed on the VALU (see phase 3)
     constexpr int NBC = (NL + 15) / 16;
     constexpr int NBA = NBC > 0 ? NBC : 1;
-    __shared__ float4 sDrgb[64];      // dL/dout RGB of the block's pixels
+    __shared__ float2 sRG[64];        // dL/dout R, G of the block's pixels
+    __shared__ float sBc[64];         // dL/dout B
     constexpr int GS = LSR_GRP_STRIDE;
     __shared__ WaveStageG st;
 #ifdef LSR_BWD_LDS_PAD   // occupancy experiment only: extra LDS per wave
@@ -974,7 +1076,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 
     const RenderArgs& a = b.f;
     const Cam& c = a.cam;
-    const WaveTile wt(c);
+    const WaveTile wt(a);
     const int lane = threadIdx.x;
     const int lg = lane >> 4, li = lane & 15;
     const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
@@ -1006,7 +1108,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     // then records) are issued before the block's dL/dout fragments, so
     // waiting for them (vector-memory operations complete in issue order)
     // never waits for the 40 fragment loads; the lane's own RGB dL/dout is
-    // loaded first among those, reaches LDS (sDrgb) just before the chunk
+    // loaded first among those, reaches LDS (sRG, sBc) just before the chunk
     // loop, and gives the background term without reloading it.
     // SPF: chunk c's ids are loaded two chunks ahead and its records one chunk
     // ahead, so staging never waits on a dependent gather (9 more VGPRs: off
@@ -1112,7 +1214,10 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     // in groups of 16, a partial group carried into the next chunk
     int carry = 0;
     float af[KS];
-    if constexpr (!LO) sDrgb[lane] = make_float4(dr0, dr1, dr2, 0.f);
+    if constexpr (!LO) {
+        sRG[lane] = make_float2(dr0, dr1);
+        sBc[lane] = dr2;
+    }
     BWD_STAMP(0);
     for (int c0 = 0; c0 < wmax; c0 += 64) {
         const int p = wmax - 1 - (c0 + lane);
@@ -1296,7 +1401,10 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 const float aa = sAT[li * GS + 4 * t + lg];
 #pragma unroll
                 for (int nb = 0; nb < NBC; nb++) ch[nb] = BWD_MFMA(aa, chB[nb][t], ch[nb]);
-                const float4 d = sDrgb[4 * t + lg];
+                // (R, G) as one 8-B read + B as a 4-B read: 2 + 2 LDS cycles, where
+                // the 12-B read of a float4's three used components (ds_read_b96) costs 8
+                const float2 rg = sRG[4 * t + lg];
+                const float4 d = make_float4(rg.x, rg.y, sBc[4 * t + lg], 0.f);
                 C0 = fmaf(aa, d.x, C0);
                 C1 = fmaf(aa, d.y, C1);
                 C2 = fmaf(aa, d.z, C2);
@@ -1434,10 +1542,10 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                             const bool on = fcol & (slot_of(q) < kn) & (v != 0.f);
                             if (LD && h > 0) {
                                 const int off = (int)(gq[q] * (uint32_t)D + (uint32_t)(f - 16)) * 4;
-                                __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, rl, on ? off : LSR_BUF_OOB, 0, 0);
+                                if (LSR_PROBE_ATOM_ISSUE) __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, rl, LSR_PROBE_ATOM_ON(on) ? off : LSR_BUF_OOB, 0, 0);
                             } else {
                                 const int off = (int)(gq[q] * (uint32_t)VP + (uint32_t)f) * 4;
-                                __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, rg, on ? off : LSR_BUF_OOB, 0, 0);
+                                if (LSR_PROBE_ATOM_ISSUE) __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, rg, LSR_PROBE_ATOM_ON(on) ? off : LSR_BUF_OOB, 0, 0);
                             }
                         }
                     }
@@ -1530,7 +1638,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_fwd_mf(RenderArgs a
     __shared__ float sT[64];
 
     const Cam& c = a.cam;
-    const WaveTile wt(c);
+    const WaveTile wt(a);
     const int lane = threadIdx.x;
     const int lg = lane >> 4, li = lane & 15;
     const PixMap pm(c, wt.tile, lane + (wt.sub << 6));

@@ -355,6 +355,27 @@ int lso_tile_keep(float x, float y, float ca, float cb, float cc, float cut, int
     return !(qmin > thr);
 }
 
+/* The product's cull box (csrc/lsr_device.h cull_box), restated operation for
+ * operation: the tiles meeting the cut ellipse's axis-aligned box, widened by
+ * 1e-4 relative + 0.5 px.  The cull keeps (Gaussian, tile) iff the tile is in
+ * the box AND lso_tile_keep passes. */
+void lso_cull_box(float x, float y, float ca, float cb, float cc, float cut, int* r0, int* r1)
+{
+    if (!(ca > 0.f) || !(cc > 0.f) || !(cut > -3.0e38f)) return;
+    const float det = ca * cc - cb * cb;
+    if (!(det > 0.f)) return;
+    const float thr = fmaf(-2.f * cut, 1.001f, 1e-3f);
+    const float ue = fmaf(sqrtf(thr * cc / det), 1.0001f, 0.5f);
+    const float ve = fmaf(sqrtf(thr * ca / det), 1.0001f, 0.5f);
+    if (!(ue < 1.0e7f) || !(ve < 1.0e7f)) return;
+    const float tx0 = ceilf((x - ue - 15.f) / 16.f), tx1 = floorf((x + ue) / 16.f) + 1.f;
+    const float ty0 = ceilf((y - ve - 15.f) / 16.f), ty1 = floorf((y + ve) / 16.f) + 1.f;
+    r0[0] = imax(r0[0], f2i(fmaxf(tx0, -1.f)));
+    r0[1] = imax(r0[1], f2i(fmaxf(ty0, -1.f)));
+    r1[0] = imin(r1[0], f2i(fmaxf(tx1, -1.f)));
+    r1[1] = imin(r1[1], f2i(fmaxf(ty1, -1.f)));
+}
+
 static inline int keep_instance(const lso_geom* g, int i, float cut, int tx, int ty)
 {
     const float* co = g->conic_opacity + 4 * i;
@@ -371,6 +392,8 @@ int64_t lso_num_rendered_ex(const lso_settings* s, int N, const lso_geom* g, int
         int r0[2], r1[2];
         get_rect(g->xy[2 * i], g->xy[2 * i + 1], g->radii[i], gx, gy, r0, r1);
         const float cut = lso_power_cut(g->conic_opacity[4 * i + 3]);
+        const float* co = g->conic_opacity + 4 * i;
+        lso_cull_box(g->xy[2 * i], g->xy[2 * i + 1], co[0], co[1], co[2], cut, r0, r1);
         for (int y = r0[1]; y < r1[1]; y++)
             for (int x = r0[0]; x < r1[0]; x++) m += keep_instance(g, i, cut, x, y);
     }
@@ -403,6 +426,10 @@ void lso_binning_ex(const lso_settings* s, int N, const lso_geom* g, uint32_t* p
         int r0[2], r1[2];
         get_rect(g->xy[2 * i], g->xy[2 * i + 1], g->radii[i], gx, gy, r0, r1);
         const float cut = lso_power_cut(g->conic_opacity[4 * i + 3]);
+        if (cull) {
+            const float* co = g->conic_opacity + 4 * i;
+            lso_cull_box(g->xy[2 * i], g->xy[2 * i + 1], co[0], co[1], co[2], cut, r0, r1);
+        }
         for (int y = r0[1]; y < r1[1]; y++)
             for (int x = r0[0]; x < r1[0]; x++)
                 if (!cull || keep_instance(g, i, cut, x, y)) cnt[y * gx + x + 1]++;
@@ -418,6 +445,10 @@ void lso_binning_ex(const lso_settings* s, int N, const lso_geom* g, uint32_t* p
         uint32_t db;
         memcpy(&db, &g->depth[i], 4);
         const float cut = lso_power_cut(g->conic_opacity[4 * i + 3]);
+        if (cull) {
+            const float* co = g->conic_opacity + 4 * i;
+            lso_cull_box(g->xy[2 * i], g->xy[2 * i + 1], co[0], co[1], co[2], cut, r0, r1);
+        }
         for (int y = r0[1]; y < r1[1]; y++)
             for (int x = r0[0]; x < r1[0]; x++) {
                 if (cull && !keep_instance(g, i, cut, x, y)) continue;

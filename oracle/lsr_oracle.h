@@ -97,6 +97,9 @@ void lso_binning_ex(const lso_settings* s, int N, const lso_geom* g,
                     uint32_t* point_list, uint32_t* ranges, int cull);
 float lso_power_cut(float opacity);
 int lso_tile_keep(float x, float y, float ca, float cb, float cc, float cut, int tx, int ty);
+/* the cull's box (lsr_device.h cull_box): shrinks the rect [r0, r1) to the
+ * tiles meeting the cut ellipse's bounding box; kept = in box && lso_tile_keep */
+void lso_cull_box(float x, float y, float ca, float cb, float cc, float cut, int* r0, int* r1);
 
 /* A.3 render forward.  out_color 3*H*W; out_lang Dout*H*W (Dout = D dense
  * or quick_dim); final_T, n_contrib H*W.  Tiles are processed in parallel

@@ -4,10 +4,14 @@ CPU: the oracle restatement (oracle.lang_cos_loss) against vectors produced by
 the reference's own cos_loss (tests/golden/make_lang_loss_golden.py).
 GPU: langsplatv2_amd.lang_loss.language_cos_loss (forward + autograd
 backward through the C ABI) against the golden vectors and the oracle.
-Tolerances (fp32 kernel vs float64 references): loss 2e-6 absolute;
-dL/dweight_map per pixel 2e-4 of that pixel's largest |gradient| (the
-|f| = 0 pixel's gradient is ~1e6, the rest ~1e-3); dL/dcodebooks 2e-4 of the
-largest |entry|.
+Tolerances (fp32 kernel vs float64 references): loss 2e-7 absolute;
+dL/dweight_map per pixel 2e-6 of that pixel's largest |gradient| (the
+|f| = 0 pixel's gradient is ~1e6, the rest ~1e-3); dL/dcodebooks 2e-6 of the
+largest |entry|.  Measured (tools/loss_err.py -> profiles/r03_loss_err.json,
+these cases + 270x480): loss <= 2.8e-8, dL/dW <= 6.3e-7, dL/dcodebooks
+<= 6.0e-7; the reference's own fp32 formulation (cos_loss on the materialised
+(512, H, W) maps, torch on the same GPU) is off the float64 truth by up to
+2.3e-6 (dL/dW) and 6.2e-6 (dL/dcodebooks) on the same cases.
 """
 import os
 
@@ -18,8 +22,8 @@ import torch
 from oracle import oracle as O
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_lang_loss.npz")
-LOSS_ATOL = 2e-6
-GRAD_RTOL = 2e-4
+LOSS_ATOL = 2e-7
+GRAD_RTOL = 2e-6
 
 
 def _gold(name):

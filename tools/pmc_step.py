@@ -1,5 +1,6 @@
 """Minimal workload for PMC collection: a few cfg3 fwd+bwd steps, or (LSR_QUICK=1)
-quick-path forwards at 1280x800 with 1M Gaussians (K=12 sparse codes, Dq=192)."""
+quick-path forwards at 1280x800 with 1M Gaussians (K=12 sparse codes, Dq=192), each followed
+by the 3 x 64 x 512 codebook decode + L2 norm."""
 import os
 import sys
 
@@ -23,11 +24,15 @@ if os.environ.get("LSR_QUICK", "0") == "1":
         campos=cam["campos"].to(dev), prefiltered=False, debug=False, include_feature=False, quick_render=True)
     r = GaussianRasterizer(rs)
     z = torch.zeros_like(t["means3D"])
+    from langsplatv2_amd import quick
+    cb = torch.randn(3, 64, 512, generator=torch.Generator().manual_seed(3)).to(dev)
     with torch.no_grad():
         for _ in range(steps):
-            r(means3D=t["means3D"], means2D=z, opacities=t["opacities"], shs=t["shs"],
-              language_feature_weights_quick=t["language_feature_weights_quick"],
-              language_feature_indices=t["language_feature_indices"], scales=t["scales"], rotations=t["rotations"])
+            lm = r(means3D=t["means3D"], means2D=z, opacities=t["opacities"], shs=t["shs"],
+                   language_feature_weights_quick=t["language_feature_weights_quick"],
+                   language_feature_indices=t["language_feature_indices"], scales=t["scales"],
+                   rotations=t["rotations"])[1]
+            quick.decode_language_features(lm, cb)   # eval_lerf.py:214-218
     torch.cuda.synchronize()
     print("ok")
     sys.exit(0)
