@@ -74,7 +74,7 @@ def algorithmic_bytes(g, rs, D, S):
     largest n_contrib, rounded to the 256-batch) for context."""
     N = g["means3D"].shape[0]
     e = torch.empty(0, device=g["means3D"].device)
-    _, _, radii, M, bufs, _, _ = rasterizer._run_forward(
+    _, _, radii, M, bufs, _, _, _ = rasterizer._run_forward(
         g["means3D"], g.get("shs", e), g.get("colors_precomp", e), g.get("language_feature_precomp", e), e, e,
         g["opacities"], g.get("scales", e), g.get("rotations", e), e, rs)
     W, H = rs.image_width, rs.image_height

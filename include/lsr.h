@@ -112,7 +112,19 @@ typedef struct lsr_fwd_out {
     void* binning; size_t binning_bytes;   /* capacity (>= layout for num_rendered) */
     void* image;   size_t image_bytes;
     int64_t num_rendered;
+    /* Optional: the backward's accumulators, prepared by the forward.  In:
+     * grad_ws_request = LSR_GWS_GEOM (the backward will request geometry /
+     * colour gradients) | LSR_GWS_LANG (it will request dL_dlang).  The
+     * forward then allocates them (LSR_BUF_GRAD) and zeroes them inside the
+     * render kernel instead of the backward clearing them with memsets; out:
+     * grad_ws / grad_ws_bytes / grad_ws_kind, and grad_ws_lang_off = byte
+     * offset of an (N,D) dL/dlang accumulator inside grad_ws (SIZE_MAX: none).
+     * Dense language path only (quick_render: nothing prepared). */
+    int grad_ws_request;
+    int grad_ws_kind;
+    void* grad_ws; size_t grad_ws_bytes; size_t grad_ws_lang_off;
 } lsr_fwd_out;
+enum { LSR_GWS_GEOM = 1, LSR_GWS_LANG = 2 };
 
 /* _C.rasterize_gaussians: preprocess → binning (tile buckets + per-tile depth
  * sort) → per-pixel alpha blend of RGB + language channels.  With
@@ -129,6 +141,12 @@ typedef struct lsr_bwd_in {
     const int32_t* radii;           /* (N,) from forward */
     const float* dL_dout_color;     /* (3,H,W) */
     const float* dL_dout_lang;      /* (D,H,W) or NULL */
+    /* Optional: lsr_fwd_out.grad_ws / _bytes / _kind of the same forward
+     * (zeroed accumulators; hand them to ONE backward).  Used when the kind
+     * matches what this call's requested outputs need (otherwise the call
+     * allocates and clears its own); dL_dlang == grad_ws + grad_ws_lang_off
+     * then needs no clearing either. */
+    void* grad_ws; size_t grad_ws_bytes; int grad_ws_kind;
 } lsr_bwd_in;
 
 /* Gradient outputs; NULL = not requested (needs_input_grad False).  Every

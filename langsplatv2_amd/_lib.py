@@ -18,6 +18,7 @@ LSR_ENONFINITE = 6
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_GRAD, LSR_BUF_DECODE, LSR_BUF_KNN, LSR_BUF_LOSS = 0, 1, 2, 3, 4, 5, 6
 LSR_BUF_GUARD, LSR_BUF_SPARSE = 7, 8
 LSR_INDEX_F32, LSR_INDEX_I32, LSR_INDEX_I64 = 0, 1, 2
+LSR_GWS_GEOM, LSR_GWS_LANG = 1, 2
 
 _vp = ctypes.c_void_p
 
@@ -74,6 +75,11 @@ class FwdOut(ctypes.Structure):
         ("image", _vp),
         ("image_bytes", ctypes.c_size_t),
         ("num_rendered", ctypes.c_int64),
+        ("grad_ws_request", ctypes.c_int),
+        ("grad_ws_kind", ctypes.c_int),
+        ("grad_ws", _vp),
+        ("grad_ws_bytes", ctypes.c_size_t),
+        ("grad_ws_lang_off", ctypes.c_size_t),
     ]
 
 
@@ -86,6 +92,9 @@ class BwdIn(ctypes.Structure):
         ("radii", _vp),
         ("dL_dout_color", _vp),
         ("dL_dout_lang", _vp),
+        ("grad_ws", _vp),
+        ("grad_ws_bytes", ctypes.c_size_t),
+        ("grad_ws_kind", ctypes.c_int),
     ]
 
 

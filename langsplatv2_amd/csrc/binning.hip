@@ -45,9 +45,11 @@ namespace lsr {
 
 size_t scan_partials(size_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 1; }
 
-__device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t* sh, uint64_t& total)
+// Block-wide exclusive scan over NB threads (sh: NB / 64 entries).
+template <int NB>
+__device__ __forceinline__ uint64_t block_excl_scan_u64_n(uint64_t v, uint64_t* sh, uint64_t& total)
 {
-    // wave inclusive scan via shuffles, then across the 4 waves through LDS
+    // wave inclusive scan via shuffles, then across the waves through LDS
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint64_t x = v;
 #pragma unroll
@@ -58,13 +60,17 @@ __device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t* sh
     if (lane == 63) sh[w] = x;
     __syncthreads();
     uint64_t wofs = 0, tot = 0;
-    for (int k = 0; k < SCAN_BLOCK / 64; k++) {
+    for (int k = 0; k < NB / 64; k++) {
         if (k < w) wofs += sh[k];
         tot += sh[k];
     }
     __syncthreads();
     total = tot;
     return wofs + x - v;
+}
+__device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t* sh, uint64_t& total)
+{
+    return block_excl_scan_u64_n<SCAN_BLOCK>(v, sh, total);
 }
 
 __global__ void __launch_bounds__(SCAN_BLOCK) k_scan_reduce(const uint32_t* __restrict__ in, size_t n,
@@ -174,23 +180,29 @@ __device__ __forceinline__ int tile_class(int n)
 }
 
 // Wave-aggregated append of tile t (lanes with active) to its class list.
-// Every lane of the wave must call it.
+// Every lane of the wave must call it.  One atomic instruction for the whole
+// wave: lane k adds the wave's class-k count to cls_cnt[k] (the classes'
+// adds are independent, so they share one round trip instead of one each).
 __device__ __forceinline__ void tile_class_append(bool active, int t, int n, int T, uint32_t* __restrict__ cls_cnt,
                                                   uint32_t* __restrict__ cls_list)
 {
     const int c = active ? tile_class(n) : -1;
     const int lane = threadIdx.x & 63;
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint64_t m[SORT_NCLS];
+    uint32_t cnt = 0;
 #pragma unroll
     for (int k = 0; k < SORT_NCLS; k++) {
-        const uint64_t m = __ballot(c == k);
-        if (m == 0) continue;
-        const int leader = __ffsll((unsigned long long)m) - 1;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&cls_cnt[k], (uint32_t)__popcll(m));
-        base = __shfl(base, leader, 64);
-        if (c == k) cls_list[(size_t)k * T + base + __popcll(m & below)] = (uint32_t)t;
+        m[k] = __ballot(c == k);
+        cnt = lane == k ? (uint32_t)__popcll(m[k]) : cnt;
     }
+    uint32_t base = 0;
+    if (cnt) base = atomicAdd(&cls_cnt[lane], cnt);
+    uint64_t mine = 0;
+#pragma unroll
+    for (int k = 0; k < SORT_NCLS; k++) mine = c == k ? m[k] : mine;
+    const uint32_t b = __shfl(base, c < 0 ? 0 : c, 64);
+    if (c >= 0) cls_list[(size_t)c * T + b + __popcll(mine & below)] = (uint32_t)t;
 }
 
 // Classification pass for the global-atomic binning path (the privatised path
@@ -438,7 +450,9 @@ __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int r
     const int blk = blockIdx.x;
     const Band bd(c, rows, blockIdx.y);
 #endif
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < SORT_NCLS) cls_cnt[threadIdx.x] = 0;   // k_bin_table appends after us
+    // k_bin_table appends to the class counts and takes tickets after us
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < SORT_NCLS) cls_cnt[threadIdx.x] = 0;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) cls_cnt[LSR_TICKET_WORD] = 0;
     for (int k = threadIdx.x; k < bd.nt; k += BB) hist[k] = 0;
     __syncthreads();
     WaveRects& wr = wrs[threadIdx.x >> 6];
@@ -476,53 +490,177 @@ __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int r
     if (probe_acc == 0xdeadbeefu) hist[0] = probe_acc;
 #endif
     __syncthreads();
-    uint32_t* row = table + (size_t)blk * T + bd.t0;
+    uint32_t* row = table + (size_t)blk * table_stride(T) + bd.t0;
     for (int k = threadIdx.x; k < bd.nt; k += BB) row[k] = hist[k];
 }
 
 // Column scan: table[b][t] <- sum_{b' < b} table[b'][t]; tile_cnt[t] <- total.
-// A 256-thread block owns 32 tiles x 8 row segments: each thread sums its
-// segment (8 independent loads in flight), the 8 segment sums are scanned in
-// LDS, then each thread rewrites its segment with running bases.
-#define TBL_COLS 32
-#define TBL_SEGS 8
-__global__ void __launch_bounds__(256) k_bin_table(int T, int B, uint32_t* __restrict__ table,
-                                                   uint32_t* __restrict__ tile_cnt, uint32_t* __restrict__ cls_cnt,
-                                                   uint32_t* __restrict__ cls_list)
+// The table's rows have stride Tp = T rounded up to 4 (columns past T are
+// never written by the count and are masked here).  A block owns 64 tiles
+// (one tile group): 16 column groups of 4 tiles (one 16-B load per row) x
+// SEGS row segments of 16 rows, every row held in registers between the sum
+// and the rewrite (the table is read once and written once).
+//
+// The same launch also finishes the tile scan's top level and publishes M:
+// every block stores its group total write-through (sc1) and takes a ticket
+// (agent-scope add after every wave drained its stores, behind a workgroup
+// barrier); the block holding the last ticket scans the group totals (sc1
+// loads, in place), writes tile_start[T] = M and publishes M plus the sort
+// class counts to the pinned host word (what k_publish_total does on the
+// B = 0 path).  k_tile_start_apply then adds each group's base to the
+// in-group scan.  This replaces three scan launches and the publish launch.
+// The ticket is zeroed by k_bin_count (the preceding launch).
+#define TBL_TILES 64   // tiles per k_bin_table block (and per tile group)
+#define TBL_RPT 16     // table rows per thread
+struct BinPublish {
+    uint64_t* gpart;      // per tile group: total, then (last block) exclusive base; [G] = M
+    uint32_t* ticket;     // arrival counter, zero on entry
+    uint32_t* tile_end;   // tile_start + T
+    uint64_t* host_slot;  // pinned host word (+ class counts after it)
+    uint32_t seq;
+};
+__device__ __forceinline__ uint32_t u4_get(const uint4& v, int j) { return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w; }
+__device__ __forceinline__ uint4 u4_add(const uint4& a, const uint4& b)
 {
-    __shared__ uint32_t seg_sum[TBL_SEGS][TBL_COLS];
-    const int col = threadIdx.x % TBL_COLS, seg = threadIdx.x / TBL_COLS;
-    const int t = blockIdx.x * TBL_COLS + col;
-    const int rows = (B + TBL_SEGS - 1) / TBL_SEGS;
-    const int b0 = seg * rows, b1 = min(B, b0 + rows);
-    uint32_t sum = 0;
-    if (t < T) {
-        int b = b0;
-        for (; b + 8 <= b1; b += 8) {
-            uint32_t v[8];
+    return make_uint4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+template <int SEGS>
+__global__ void __launch_bounds__(16 * SEGS) k_bin_table(int T, int Tp, int B, uint32_t* __restrict__ table,
+                                                         uint32_t* __restrict__ tile_cnt,
+                                                         uint32_t* __restrict__ cls_cnt,
+                                                         uint32_t* __restrict__ cls_list, BinPublish pb)
+{
+    constexpr int NT = 16 * SEGS;
+    __shared__ uint4 seg_sum[SEGS][16];
+    __shared__ uint64_t sh[NT / 64];
+    __shared__ int s_last;
+    const int cg = threadIdx.x & 15, seg = threadIdx.x >> 4;
+    const int t4 = blockIdx.x * TBL_TILES + cg * 4;   // this thread's 4 tiles
+    const int b0 = seg * TBL_RPT;
+    // columns past T (the row padding, or past the last tile) count 0
+    const uint4 cmask = make_uint4(t4 < T ? ~0u : 0u, t4 + 1 < T ? ~0u : 0u, t4 + 2 < T ? ~0u : 0u,
+                                   t4 + 3 < T ? ~0u : 0u);
+    const bool colok = t4 < Tp;
+    uint4 v[TBL_RPT];
+    uint4 sum = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
-            for (int k = 0; k < 8; k++) v[k] = table[(size_t)(b + k) * T + t];
-#pragma unroll
-            for (int k = 0; k < 8; k++) sum += v[k];
-        }
-        for (; b < b1; b++) sum += table[(size_t)b * T + t];
+    for (int k = 0; k < TBL_RPT; k++) {
+        const int b = b0 + k;
+        uint4 x = make_uint4(0u, 0u, 0u, 0u);
+        if (colok && b < B) x = *reinterpret_cast<const uint4*>(table + (size_t)b * Tp + t4);
+        v[k] = make_uint4(x.x & cmask.x, x.y & cmask.y, x.z & cmask.z, x.w & cmask.w);
+        sum = u4_add(sum, v[k]);
     }
-    seg_sum[seg][col] = sum;
+    seg_sum[seg][cg] = sum;
     __syncthreads();
-    uint32_t run = 0, tot = 0;
-    for (int k = 0; k < TBL_SEGS; k++) {
-        const uint32_t x = seg_sum[k][col];
-        run += (k < seg) ? x : 0u;
-        tot += x;
+    uint4 run = make_uint4(0u, 0u, 0u, 0u), tot = run;
+    for (int k = 0; k < SEGS; k++) {
+        const uint4 x = seg_sum[k][cg];
+        if (k < seg) run = u4_add(run, x);
+        tot = u4_add(tot, x);
     }
-    if (threadIdx.x < 64) tile_class_append(seg == 0 && t < T, t, (int)tot, T, cls_cnt, cls_list);
-    if (t >= T) return;
-    if (seg == 0) tile_cnt[t] = tot;
-    for (int b = b0; b < b1; b++) {
-        const uint32_t v = table[(size_t)b * T + t];
-        table[(size_t)b * T + t] = run;
-        run += v;
+    if (threadIdx.x < 64) {
+        // segment 0 = lanes 0..15 of wave 0 hold the 64 totals, 4 each: lane
+        // l takes tile l for the class append (one call for the group)
+        const int l = threadIdx.x, src = l >> 2, j = l & 3;
+        const uint32_t n0 = __shfl(tot.x, src, 64), n1 = __shfl(tot.y, src, 64);
+        const uint32_t n2 = __shfl(tot.z, src, 64), n3 = __shfl(tot.w, src, 64);
+        const uint32_t nl = j == 0 ? n0 : j == 1 ? n1 : j == 2 ? n2 : n3;
+        const int tl = blockIdx.x * TBL_TILES + l;
+        tile_class_append(tl < T, tl, (int)nl, T, cls_cnt, cls_list);
+        uint64_t g = seg == 0 ? (uint64_t)tot.x + tot.y + tot.z + tot.w : 0ull;
+#pragma unroll
+        for (int d = 8; d >= 1; d >>= 1) g += __shfl_xor(g, d, 64);
+        if (threadIdx.x == 0) __hip_atomic_store(&pb.gpart[blockIdx.x], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (seg == 0) {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (t4 + j < T) tile_cnt[t4 + j] = u4_get(tot, j);
+        }
     }
+    if (colok) {
+#pragma unroll
+        for (int k = 0; k < TBL_RPT; k++) {
+            const int b = b0 + k;
+            if (b < B) *reinterpret_cast<uint4*>(table + (size_t)b * Tp + t4) = run;
+            run = u4_add(run, v[k]);
+        }
+    }
+    // ticket: every wave drains its stores (the group total's sc1 store, the
+    // class atomics), then one lane arrives for the workgroup
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t prev = __hip_atomic_fetch_add(pb.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = prev == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the sc1 loads below the ticket
+    // the group totals, 8 consecutive ones per thread, all loads in flight at
+    // once (one round trip per 8 NT groups)
+    const int G = (int)gridDim.x;
+    uint64_t carry = 0;
+    for (int base = 0; base < G; base += NT * 8) {
+        const int i0 = base + threadIdx.x * 8;
+        uint64_t gv[8], s = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            gv[k] = i0 + k < G ? __hip_atomic_load(&pb.gpart[i0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+#pragma unroll
+        for (int k = 0; k < 8; k++) s += gv[k];
+        uint64_t gt;
+        uint64_t r = carry + block_excl_scan_u64_n<NT>(s, sh, gt);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            if (i0 + k < G) pb.gpart[i0 + k] = r;
+            r += gv[k];
+        }
+        carry += gt;
+    }
+    if (threadIdx.x < 64) {
+        // the class counts: one load per lane, all in flight; lane 0 stores
+        // them and then the releasing sequence word
+        const int l = threadIdx.x;
+        const uint32_t cnt = l < SORT_NCLS ? __hip_atomic_load(&cls_cnt[l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        uint32_t cv[SORT_NCLS];
+#pragma unroll
+        for (int k = 0; k < SORT_NCLS; k++) cv[k] = __shfl(cnt, k, 64);
+        if (l == 0) {
+            const uint32_t m32 = carry >= 0xffffffffull ? 0xffffffffu : (uint32_t)carry;
+            pb.gpart[G] = carry;
+            *pb.tile_end = m32;
+            uint32_t* h = (uint32_t*)(pb.host_slot + 1);
+#pragma unroll
+            for (int k = 0; k < SORT_NCLS; k++) __hip_atomic_store(&h[k], cv[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // the counts are written through (system scope) and acknowledged
+            // before the sequence word goes out.  No release fence: the host
+            // reads nothing else this kernel wrote, and a system-scope release
+            // writes back this XCD's whole L2 first (the freshly rewritten
+            // table) -- measured ~20 us at cfg5.
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(pb.host_slot, ((uint64_t)pb.seq << 32) | m32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+// tile_start[t] = group base + exclusive scan of tile_cnt inside the 64-tile
+// group (one wave).
+__global__ void __launch_bounds__(256) k_tile_start_apply(int T, const uint32_t* __restrict__ tile_cnt,
+                                                          const uint64_t* __restrict__ gpart,
+                                                          uint32_t* __restrict__ tile_start)
+{
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t v = t < T ? tile_cnt[t] : 0u;
+    uint32_t x = v;
+    const int l = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (l >= d) x += y;
+    }
+    if (t < T) tile_start[t] = (uint32_t)gpart[t / TBL_TILES] + x - v;
 }
 
 // The scatter's bands are its own (rows of its own, not the count's): the
@@ -545,7 +683,7 @@ __global__ void __launch_bounds__(BB) k_bin_scatter(Cam c, int P, int chunk, int
     const int o = xcd_remap(blockIdx.x, gridDim.x);
     const int blk = o / S;
     const Band bd(c, rows, o - blk * S);
-    const uint32_t* row = table + (size_t)blk * T + bd.t0;
+    const uint32_t* row = table + (size_t)blk * table_stride(T) + bd.t0;
     for (int k = threadIdx.x; k < bd.nt; k += BB) base[k] = tile_start[bd.t0 + k] + row[k];
     __syncthreads();
     WaveRects& wr = wrs[threadIdx.x >> 6];
@@ -648,8 +786,8 @@ int bin_blocks(int P, const Cam& c, int& chunk)
 bool bin_privatised_ok(const Cam& c) { return (size_t)c.gx * 4 <= LSR_BAND_LDS && (size_t)c.gx * c.gy <= (1u << 20); }
 
 hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t* geom, const int32_t* radii,
-                            uint32_t* table, uint32_t* tile_cnt, uint32_t* cls_cnt, uint32_t* cls_list,
-                            hipStream_t st)
+                            uint32_t* table, uint32_t* tile_cnt, uint32_t* tile_start, uint64_t* tpart,
+                            uint32_t* cls_cnt, uint32_t* cls_list, uint64_t* host_slot, uint32_t seq, hipStream_t st)
 {
     const int T = c.gx * c.gy;
     const int rows = bin_band_rows(c);
@@ -667,11 +805,29 @@ hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t
             k_bin_count<1024><<<grid, 1024, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt);
         else
             k_bin_count<512><<<grid, 512, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt);
-        k_bin_table<<<(T + TBL_COLS - 1) / TBL_COLS, 256, 0, st>>>(T, B, table, tile_cnt, cls_cnt, cls_list);
+        BinPublish pb{tpart, cls_cnt + LSR_TICKET_WORD, tile_start + T, host_slot, seq};
+        const int G = (T + TBL_TILES - 1) / TBL_TILES, Tp = table_stride(T);
+        if (B <= 16 * TBL_RPT)
+            k_bin_table<16><<<G, 256, 0, st>>>(T, Tp, B, table, tile_cnt, cls_cnt, cls_list, pb);
+        else if (B <= 32 * TBL_RPT)
+            k_bin_table<32><<<G, 512, 0, st>>>(T, Tp, B, table, tile_cnt, cls_cnt, cls_list, pb);
+        else if (B <= 64 * TBL_RPT)
+            k_bin_table<64><<<G, 1024, 0, st>>>(T, Tp, B, table, tile_cnt, cls_cnt, cls_list, pb);
+        else
+            return hipErrorInvalidValue;   // bin_blocks keeps B <= 2 * LSR_BIN_TARGET
     } else {
         (void)hipMemsetAsync(tile_cnt, 0, (size_t)T * 4, st);
         (void)hipMemsetAsync(cls_cnt, 0, SORT_NCLS * 4, st);
+        (void)launch_scan_u32(tile_cnt, tile_start, tpart, (size_t)T, true, st);
+        (void)launch_publish_total(tpart + (scan_partials((size_t)T) - 1), tile_start + T, host_slot, seq, cls_cnt, st);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_start_apply(int T, int B, const uint32_t* tile_cnt, const uint64_t* tpart, uint32_t* tile_start,
+                                   hipStream_t st)
+{
+    if (B > 0 && T > 0) k_tile_start_apply<<<(T + 255) / 256, 256, 0, st>>>(T, tile_cnt, tpart, tile_start);
     return hipGetLastError();
 }
 

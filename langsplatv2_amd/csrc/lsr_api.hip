@@ -550,6 +550,40 @@ static int wait_published(HostSlot& hs, uint32_t seq, hipStream_t st, uint64_t* 
     }
 }
 
+// The dense backward's accumulators (lsr_fwd_out.grad_ws): gradient rows
+// (P x VP, unless only dL/dlang is requested) and, where the render backward
+// adds dL/dlang straight into an (P, D) array (language-only, or D = 16 / 32
+// with aligned rows), that array.  kind encodes the configuration, so a
+// backward uses a forward's workspace only when it needs exactly this one.
+struct GradWs {
+    int kind = 0;          // 0: nothing to prepare
+    int VP = 0;
+    size_t lang_off = SIZE_MAX, total = 0;
+    bool lang_only = false, lang_direct = false;
+};
+static GradWs grad_ws_layout(int P, int Dd, bool geom, bool lang, bool lang_aligned)
+{
+    GradWs w;
+    lang = lang && Dd > 0;
+    if (P <= 0 || (!geom && !lang)) return w;
+    w.lang_only = lang && !geom;
+    w.lang_direct = lang && geom && bwd_lang_direct(Dd) && lang_aligned;
+    const size_t lang_bytes = (size_t)P * Dd * 4;
+    if (w.lang_only) {
+        w.lang_off = 0;
+        w.total = lang_bytes;
+    } else {
+        w.VP = w.lang_direct ? 16 : grad_row_width(Dd);
+        w.total = (size_t)P * w.VP * 4;
+        if (w.lang_direct) {
+            w.lang_off = (w.total + 255) / 256 * 256;
+            w.total = w.lang_off + lang_bytes;
+        }
+    }
+    w.kind = (geom ? 1 : 0) | (lang ? 2 : 0) | (w.lang_direct ? 4 : 0) | (w.VP << 8);
+    return w;
+}
+
 int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, lsr_alloc_fn alloc, void* ctx,
                 void* stream)
 {
@@ -574,7 +608,7 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     const bool priv = P > 0 && bin_privatised_ok(c);
     int chunk = 0;
     const int B = priv ? bin_blocks(P, c, chunk) : 0;
-    const size_t table_bytes = priv ? align256((size_t)B * T * 4) : 0;
+    const size_t table_bytes = priv ? align256((size_t)B * table_stride(T) * 4) : 0;
     uint8_t* geom = (uint8_t*)alloc(ctx, GL.total, LSR_BUF_GEOM);
     uint8_t* img = (uint8_t*)alloc(ctx, IL.total + table_bytes, LSR_BUF_IMAGE);
     if (!geom || !img) return LSR_ENOMEM;
@@ -600,12 +634,12 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
         // 2. per-block tile histograms -> column scan -> tile starts; M = total
         {
             StageScope sc(ST_DUP, st);
-            LSR_HIP(launch_bin_count(c, P, chunk, B, geom, out->radii, table, tile_cnt, cls_cnt, cls_list, st));
+            LSR_HIP(launch_bin_count(c, P, chunk, B, geom, out->radii, table, tile_cnt, tile_start, tpart, cls_cnt,
+                                     cls_list, hs.dev, seq, st));
         }
         {
             StageScope sc(ST_SCAN_T, st);
-            LSR_HIP(launch_scan_u32(tile_cnt, tile_start, tpart, (size_t)T, true, st));
-            LSR_HIP(launch_publish_total(tpart + tnb, tile_start + T, hs.dev, seq, cls_cnt, st));
+            LSR_HIP(launch_tile_start_apply(T, B, tile_cnt, tpart, tile_start, st));
         }
     } else {
         uint64_t* gpart = (uint64_t*)(geom + GL.scan_part);
@@ -679,10 +713,30 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     }
     LSR_DEBUG_SYNC(s, st, "tile_sort");
 
-    // 4. render
+    // 4. render (and the backward's accumulators zeroed alongside it)
     RenderArgs ra = make_render_args(s, in, c, geom, bin, img, (int64_t)M);
     ra.out_color = out->out_color;
     ra.out_lang = out->out_lang;
+    out->grad_ws = nullptr;
+    out->grad_ws_bytes = 0;
+    out->grad_ws_kind = 0;
+    out->grad_ws_lang_off = SIZE_MAX;
+    if (out->grad_ws_request && !s->quick_render) {
+        const GradWs w = grad_ws_layout(P, Dd, (out->grad_ws_request & LSR_GWS_GEOM) != 0,
+                                        (out->grad_ws_request & LSR_GWS_LANG) != 0,
+                                        (uintptr_t)in->language_feature_precomp % 16 == 0);
+        if (w.kind) {
+            const size_t bytes = (w.total + 255) / 256 * 256;
+            void* ws = alloc(ctx, bytes, LSR_BUF_GRAD);
+            if (!ws) return LSR_ENOMEM;
+            out->grad_ws = ws;
+            out->grad_ws_bytes = w.total;
+            out->grad_ws_kind = w.kind;
+            out->grad_ws_lang_off = w.lang_off;
+            ra.zero = (float4*)ws;
+            ra.zero_n16 = bytes / 16;
+        }
+    }
     { StageScope sc(ST_RENDER, st); LSR_HIP(launch_render_fwd(ra, st)); }
     LSR_DEBUG_SYNC(s, st, "render");
     LSR_GUARD(guard, "out_color", out->out_color, 3 * NPIX);
@@ -847,6 +901,11 @@ static int backward_dense(const lsr_settings* s, const lsr_inputs* in, const lsr
     // and no means2D gradient): the language-only render backward writes the
     // output directly; no gradient rows, no preprocess backward.
     const bool lang_only = Dd > 0 && out->dL_dlang && !geometry_requested(out);
+    // the forward's zeroed accumulators, when they are exactly what this call needs
+    const GradWs W = grad_ws_layout(P, Dd, geometry_requested(out), out->dL_dlang != nullptr,
+                                    (uintptr_t)in->language_feature_precomp % 16 == 0);
+    const bool ws_ok = b->grad_ws && W.kind != 0 && b->grad_ws_kind == W.kind && b->grad_ws_bytes >= W.total;
+    const bool ws_lang = ws_ok && W.lang_off != SIZE_MAX && out->dL_dlang == (float*)((uint8_t*)b->grad_ws + W.lang_off);
     if (lang_only) {
         RenderBwdArgs rb;
         rb.f = make_render_args(s, in, c, (const uint8_t*)b->geom, (const uint8_t*)b->binning,
@@ -858,7 +917,7 @@ static int backward_dense(const lsr_settings* s, const lsr_inputs* in, const lsr
         rb.dout_lang = b->dL_dout_lang;
         rb.grad_acc = out->dL_dlang;
         rb.VP = Dd;
-        { StageScope sc(ST_GZERO, st); LSR_HIP(hipMemsetAsync(out->dL_dlang, 0, (size_t)P * Dd * 4, st)); }
+        if (!ws_lang) { StageScope sc(ST_GZERO, st); LSR_HIP(hipMemsetAsync(out->dL_dlang, 0, (size_t)P * Dd * 4, st)); }
         { StageScope sc(ST_RENDER_BWD, st); LSR_HIP(launch_render_bwd_lang(rb, st)); }
         LSR_DEBUG_SYNC(s, st, "render_bwd_lang");
         rc = record_lang_ready(out, st);
@@ -872,12 +931,12 @@ static int backward_dense(const lsr_settings* s, const lsr_inputs* in, const lsr
     const bool lang_direct = Dd > 0 && out->dL_dlang && bwd_lang_direct(Dd) &&
                              (uintptr_t)in->language_feature_precomp % 16 == 0;
     const int VP = lang_direct ? 16 : grad_row_width(Dd);
-    float* gacc = (float*)alloc(ctx, (size_t)P * VP * 4, LSR_BUF_GRAD);
+    float* gacc = ws_ok ? (float*)b->grad_ws : (float*)alloc(ctx, (size_t)P * VP * 4, LSR_BUF_GRAD);
     if (!gacc) return LSR_ENOMEM;
-    {
+    if (!ws_ok || (lang_direct && !ws_lang)) {
         StageScope sc(ST_GZERO, st);
-        LSR_HIP(hipMemsetAsync(gacc, 0, (size_t)P * VP * 4, st));
-        if (lang_direct) LSR_HIP(hipMemsetAsync(out->dL_dlang, 0, (size_t)P * Dd * 4, st));
+        if (!ws_ok) LSR_HIP(hipMemsetAsync(gacc, 0, (size_t)P * VP * 4, st));
+        if (lang_direct && !ws_lang) LSR_HIP(hipMemsetAsync(out->dL_dlang, 0, (size_t)P * Dd * 4, st));
     }
 
     RenderBwdArgs rb;

@@ -464,6 +464,9 @@ __host__ __device__ inline GeomLayout geom_layout(size_t N)
     return L;
 }
 
+// Row stride of the privatised binning's B x T count table (16-B rows).
+__host__ __device__ inline int table_stride(int T) { return (T + 3) & ~3; }
+
 // Image workspace (per pixel + per tile).
 struct ImageLayout {
     size_t final_T, n_contrib, tile_cnt, tile_start, tile_part, cls_cnt, cls_list, total;
@@ -477,8 +480,8 @@ __host__ __device__ inline ImageLayout image_layout(size_t P, size_t T)
     L.n_contrib = o;  o += align256(P * 4);
     L.tile_cnt = o;   o += align256(T * 4);
     L.tile_start = o; o += align256((T + 1) * 4);   // exclusive scan, [T] = num_rendered
-    L.tile_part = o;  o += align256(((T + 4095) / 4096 + 1) * 8);
-    L.cls_cnt = o;    o += 256;                        // per-class tile counts (tile-sort classes)
+    L.tile_part = o;  o += align256(((T + 63) / 64 + 1) * 8);   // scan partials / 64-tile group bases
+    L.cls_cnt = o;    o += 256;                        // per-class tile counts (tile-sort classes); word 32: ticket
     L.cls_list = o;   o += align256(T * 6 * 4);        // per-class tile lists, T slots each
     L.total = o;
     return L;

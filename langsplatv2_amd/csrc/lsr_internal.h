@@ -34,6 +34,7 @@ hipError_t launch_scan_u32(const uint32_t* in, uint32_t* out, uint64_t* part, si
 // Tile-sort size classes (binning.hip tile_class); their per-class tile counts
 // and lists live in the image workspace (cls_cnt, cls_list).
 #define SORT_NCLS 6
+#define LSR_TICKET_WORD 32   // cls_cnt word k_bin_table counts arrivals in (own 128-B line)
 hipError_t launch_publish_total(const uint64_t* total, uint32_t* tile_end, uint64_t* host_slot, uint32_t seq,
                                 const uint32_t* cls_cnt, hipStream_t st);
 hipError_t launch_duplicate(const Cam& c, int P, const uint8_t* geom, const int32_t* radii, uint32_t* tile_cnt,
@@ -42,9 +43,14 @@ hipError_t launch_scatter(const Cam& c, int P, const uint8_t* geom, const int32_
                           const uint32_t* rank, uint64_t* keys, hipStream_t st);
 int bin_blocks(int P, const Cam& c, int& chunk);
 bool bin_privatised_ok(const Cam& c);
+// count + column scan + group-level tile scan; publishes M (and the sort
+// class counts) to host_slot like launch_publish_total
 hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t* geom, const int32_t* radii,
-                            uint32_t* table, uint32_t* tile_cnt, uint32_t* cls_cnt, uint32_t* cls_list,
-                            hipStream_t st);
+                            uint32_t* table, uint32_t* tile_cnt, uint32_t* tile_start, uint64_t* tpart,
+                            uint32_t* cls_cnt, uint32_t* cls_list, uint64_t* host_slot, uint32_t seq, hipStream_t st);
+// tile_start[0..T) from tile_cnt and the group bases launch_bin_count left in tpart
+hipError_t launch_tile_start_apply(int T, int B, const uint32_t* tile_cnt, const uint64_t* tpart, uint32_t* tile_start,
+                                   hipStream_t st);
 hipError_t launch_bin_scatter(const Cam& c, int P, int chunk, int B, const uint8_t* geom, const int32_t* radii,
                               const uint32_t* table, const uint32_t* tile_start, uint64_t* keys, hipStream_t st);
 hipError_t launch_tile_sort(int T, const uint32_t* tile_start, uint64_t* keys, uint32_t* point_list,
@@ -68,6 +74,9 @@ struct RenderArgs {
     uint32_t* n_contrib;
     float* out_color;
     float* out_lang;
+    // the backward's accumulators, zeroed by the dense forward render (NULL: none)
+    float4* zero = nullptr;
+    size_t zero_n16 = 0;
 };
 hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st);
 

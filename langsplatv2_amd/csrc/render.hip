@@ -28,9 +28,6 @@
 #ifndef LSR_BWD_SPLAT_PF
 #define LSR_BWD_SPLAT_PF 1  // bwd: chunk records loaded one chunk ahead (ids two ahead), D <= 32
 #endif
-#ifndef LSR_FWD_T0
-#define LSR_FWD_T0 0
-#endif
 #ifndef LSR_MF_WAVES
 #define LSR_MF_WAVES 2      // MFMA render kernels: min waves per SIMD (caps VGPRs at 256)
 #endif
@@ -210,9 +207,27 @@ __device__ __forceinline__ int stage_candidates_p(WaveStageP<F4, fwd_sfeat<NL>()
     return stage_candidates_p_rec<NL, F4>(st, valid, gid, pos, bx, by, A, B, rgb, lang, D);
 }
 
-template <int NL>
+// The backward's accumulators (RenderArgs::zero; lsr_fwd_out.grad_ws): a
+// grid-strided share per wave, non-temporal 16-B stores, issued first so no
+// early exit skips them.  The render is VALU / LDS bound; these writes replace
+// the backward's two memset launches.
+__device__ __forceinline__ void zero_backward_accumulators(const RenderArgs& a)
+{
+    if (!a.zero) return;
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    v4f* const z = reinterpret_cast<v4f*>(a.zero);
+    const size_t stride = (size_t)gridDim.x * 64;
+    for (size_t i = (size_t)blockIdx.x * 64 + threadIdx.x; i < a.zero_n16; i += stride)
+        __builtin_nontemporal_store(v4f{0.f, 0.f, 0.f, 0.f}, z + i);
+}
+
+// ZERO: this launch also clears the backward's accumulators (a.zero set);
+// a separate instantiation, so a forward without a pending backward runs the
+// unchanged kernel (the clearing loop alone moved cfg5's D = 32 render by +2 %)
+template <int NL, bool ZERO = false>
 __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
 {
+    if constexpr (ZERO) zero_backward_accumulators(a);
     constexpr int C = 3 + NL;
     constexpr int F4 = (C + 3) / 4;  // float4 per feature row
     constexpr bool SF = fwd_sfeat<NL>();
@@ -227,13 +242,8 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
     const uint32_t rs = a.tile_start[wt.tile], re = a.tile_start[wt.tile + 1];
     const int D = a.D;
 
-#if LSR_FWD_T0
-    float T = inside ? 1.0f : 0.f;   // 0 = finished (or outside the image)
-    float Tout = 0.f;                // a finished pixel's final T
-#else
     float T = 1.0f;
     bool done = !inside;
-#endif
     float acc[F4 * 4];
 #pragma unroll
     for (int k = 0; k < F4 * 4; k++) acc[k] = 0.f;
@@ -254,11 +264,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
         B1 = a.splatB[next_gid];
     }
     for (uint32_t base = rs; base < re; base += 64) {
-#if LSR_FWD_T0
-        if (wave_ballot(T > 0.f) == 0) break;
-#else
         if (wave_ballot(!done) == 0) break;
-#endif
         const uint32_t idx = base + lane;
         const bool valid = idx < re;
         const uint32_t gid = next_gid;
@@ -283,82 +289,6 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
         // blends it with weight 0 and keeps T.  The two exp chains are
         // independent (ILP); T carries from the first to the second exactly
         // as in the sequential per-pixel order.
-#if LSR_FWD_T0
-        // T0 form: a finished pixel carries T = 0 (its final T kept in Tout), so
-        // every later candidate is an exact no-op for it (alpha * 0 = 0, and the
-        // termination test stays true) without a per-pixel `done` mask; the
-        // wave's early exit is voted once per 8 candidates.  The exponent-cut
-        // test is dropped: below the cut alpha < e^-0.02 / 255 already fails
-        // the 1/255 test.  Per pixel the blend is the same sequence of
-        // operations, so the outputs are bit-identical.
-        int lastj = -1;
-        for (int j0 = 0; j0 < n; j0 += 2) {
-            if ((j0 & 7) == 0 && wave_ballot(T > 0.f) == 0) break;
-            const bool two = j0 + 1 < n;
-            const int j1 = two ? j0 + 1 : j0;
-            const int e = j0 >> 1;
-            float fr0[F4 * 4], fr1[F4 * 4];
-            if constexpr (SF) {
-                feature_row_uniform<NL, F4>(fr0, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j0]));
-                feature_row_uniform<NL, F4>(fr1, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j1]));
-            }
-            const f32x2 sX = st.X[e], sY = st.Y[e], sCA = st.CA[e], sCB = st.CB[e], sCC = st.CC[e];
-            const f32x2 OP = st.OP[e];
-            const f32x2 dx = sX - f32x2{pfx, pfx}, dy = sY - f32x2{pfy, pfy};
-            const f32x2 P = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f},
-                                                      __builtin_elementwise_fma(sCA * dx, dx, (sCC * dy) * dy),
-                                                      -((sCB * dx) * dy));
-            const f32x2 EX = expf_det2(P);
-            const float al0 = fminf(0.99f, OP.x * EX.x);
-            const float al1 = fminf(0.99f, OP.y * EX.y);
-            const float e0 = (!(P.x > 0.0f) && !(al0 < 1.0f / 255.0f)) ? al0 : 0.f;
-            const float e1 = (two && !(P.y > 0.0f) && !(al1 < 1.0f / 255.0f)) ? al1 : 0.f;
-            {
-                const float test_T = T * (1.0f - e0);
-                const bool term = test_T < 0.0001f;
-                const bool ok = (e0 != 0.f) & !term;
-                Tout = (term & (T > 0.f)) ? T : Tout;
-                const float aT = ok ? e0 * T : 0.f;
-                if constexpr (SF) {
-#pragma unroll
-                    for (int k = 0; k < F4 * 4; k++) acc[k] = fmaf(fr0[k], aT, acc[k]);
-                } else {
-#pragma unroll
-                    for (int f = 0; f < F4; f++) {
-                        const float4 v = st.F[j0 * F4 + f];
-                        acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
-                        acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
-                        acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
-                        acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
-                    }
-                }
-                T = term ? 0.f : test_T;
-                lastj = ok ? j0 : lastj;
-            }
-            {
-                const float test_T = T * (1.0f - e1);
-                const bool term = test_T < 0.0001f;
-                const bool ok = (e1 != 0.f) & !term;
-                Tout = (term & (T > 0.f)) ? T : Tout;
-                const float aT = ok ? e1 * T : 0.f;
-                if constexpr (SF) {
-#pragma unroll
-                    for (int k = 0; k < F4 * 4; k++) acc[k] = fmaf(fr1[k], aT, acc[k]);
-                } else {
-#pragma unroll
-                    for (int f = 0; f < F4; f++) {
-                        const float4 v = st.F[j1 * F4 + f];
-                        acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
-                        acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
-                        acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
-                        acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
-                    }
-                }
-                T = term ? 0.f : test_T;
-                lastj = ok ? j1 : lastj;
-            }
-        }
-#else
         int lastj = -1;   // LASTJ: staged index of the chunk's last contributor
         for (int j0 = 0; j0 < n; j0 += 2) {
             if (wave_ballot(!done) == 0) break;
@@ -435,16 +365,12 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 lastj = ok1 ? j1 : lastj;
             }
         }
-#endif
         if (lastj >= 0) last = (uint32_t)st.pos[lastj];
         wave_lds_fence();
     }
     if (inside) {
         const size_t HW = (size_t)c.H * c.W;
         const size_t pix = (size_t)pm.py * c.W + pm.px;
-#if LSR_FWD_T0
-        if (!(T > 0.f)) T = Tout;
-#endif
         a.final_T[pix] = T;
         a.n_contrib[pix] = last;
 #pragma unroll
@@ -785,7 +711,7 @@ int lang_set_for(int D)
 
 // (declarations carry the definitions' launch bounds: without them the
 // kernels would default to 1024-thread workgroups and a 128-register cap)
-template <int NL>
+template <int NL, bool ZERO = false>
 __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_fwd_mf(RenderArgs a);
 
 hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
@@ -809,13 +735,15 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
         return hipGetLastError();
     }
     switch (lang_set_for(a.D)) {
-        case 0: k_render_fwd<0><<<4 * T, 64, 0, st>>>(a); break;
-        case 4: k_render_fwd<4><<<4 * T, 64, 0, st>>>(a); break;
-        case 8: k_render_fwd<8><<<4 * T, 64, 0, st>>>(a); break;
-        case 16: k_render_fwd<16><<<4 * T, 64, 0, st>>>(a); break;
+#define LSR_FWD_LAUNCH(K, NL) (a.zero ? K<NL, true><<<4 * T, 64, 0, st>>>(a) : K<NL, false><<<4 * T, 64, 0, st>>>(a))
+        case 0: LSR_FWD_LAUNCH(k_render_fwd, 0); break;
+        case 4: LSR_FWD_LAUNCH(k_render_fwd, 4); break;
+        case 8: LSR_FWD_LAUNCH(k_render_fwd, 8); break;
+        case 16: LSR_FWD_LAUNCH(k_render_fwd, 16); break;
         // measured (cfg3 geometry): D = 32 legacy 0.78 vs MFMA 0.81 ms; D = 64 legacy 1.38 vs MFMA 1.13 ms
-        case 32: k_render_fwd<32><<<4 * T, 64, 0, st>>>(a); break;
-        case 64: k_render_fwd_mf<64><<<4 * T, 64, 0, st>>>(a); break;
+        case 32: LSR_FWD_LAUNCH(k_render_fwd, 32); break;
+        case 64: LSR_FWD_LAUNCH(k_render_fwd_mf, 64); break;
+#undef LSR_FWD_LAUNCH
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1625,7 +1553,7 @@ __device__ __forceinline__ int stage_candidates_f(WaveStageF& st, int carry, boo
 
 #define LSR_FWD_STRIDE 80   // aT tile row stride: conflict-free B-fragment reads
 
-template <int NL>
+template <int NL, bool ZERO>
 __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_fwd_mf(RenderArgs a)
 {
     constexpr int C = 3 + NL;
@@ -1636,6 +1564,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_fwd_mf(RenderArgs a
     __shared__ WaveStageF st;
     __shared__ float sAT[16 * FS];
     __shared__ float sT[64];
+    if constexpr (ZERO) zero_backward_accumulators(a);
 
     const Cam& c = a.cam;
     const WaveTile wt(a);

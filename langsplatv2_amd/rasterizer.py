@@ -215,9 +215,11 @@ def _dump(path, tensors):
 
 
 def _run_forward(means3D, sh, colors_precomp, language_feature_precomp, language_feature_weights_quick,
-                 language_feature_indices, opacities, scales, rotations, cov3Ds_precomp, rs):
-    """One lsr_forward call.  Returns (color, lang, radii, num_rendered, bufs, saved) where
-    bufs = {LSR_BUF_*: uint8 workspace tensor} and saved = contiguous inputs."""
+                 language_feature_indices, opacities, scales, rotations, cov3Ds_precomp, rs, grad_request=0):
+    """One lsr_forward call.  Returns (color, lang, radii, num_rendered, bufs, saved, dims, grad_ws) where
+    bufs = {LSR_BUF_*: uint8 workspace tensor}, saved = contiguous inputs and grad_ws = None or
+    (uint8 tensor, bytes, kind, lang_off): the backward's accumulators, zeroed by the forward render
+    when grad_request (LSR_GWS_*) asked for them (lsr_fwd_out.grad_ws)."""
     dev = means3D.device
     lib = _lib.load()
     N = means3D.shape[0]
@@ -254,6 +256,7 @@ def _run_forward(means3D, sh, colors_precomp, language_feature_precomp, language
     lang_out = torch.empty((Dout, H, W), dtype=torch.float32, device=dev)
     radii = torch.empty((N,), dtype=torch.int32, device=dev)
     out = _lib.FwdOut(color.data_ptr(), lang_out.data_ptr() if Dout else None, radii.data_ptr())
+    out.grad_ws_request = int(grad_request)
     alloc = _Alloc(dev)
     rc = lib.lsr_forward(ctypes.byref(s), ctypes.byref(ins), ctypes.byref(out), alloc.fn, None, _stream(dev))
     if rc != _lib.LSR_OK:
@@ -262,7 +265,28 @@ def _run_forward(means3D, sh, colors_precomp, language_feature_precomp, language
                                        cov3Ds_precomp, language_feature_precomp, rs.viewmatrix, rs.projmatrix])
         _lib.check(rc, "rasterize_gaussians (forward)")
     saved = (means3D_c, opac_c, sh_c, col_c, sc_c, rot_c, cov_c, lang_c, qw_c, qi_c)
-    return color, lang_out, radii, int(out.num_rendered), alloc.bufs, saved, (N, M, D, K)
+    grad_ws = None
+    if out.grad_ws:
+        grad_ws = (alloc.bufs[_lib.LSR_BUF_GRAD], int(out.grad_ws_bytes), int(out.grad_ws_kind),
+                   int(out.grad_ws_lang_off))
+    return color, lang_out, radii, int(out.num_rendered), alloc.bufs, saved, (N, M, D, K), grad_ws
+
+
+_SIZE_MAX = ctypes.c_size_t(-1).value
+_CALL = threading.local()   # grad mode at the rasterize_gaussians call (see _grad_request)
+
+
+def _grad_request(need, sh, colors_precomp, language_feature_precomp, scales, rotations, cov3Ds_precomp, rs) -> int:
+    """LSR_GWS_* bits for the gradients the backward will request (the same rule as backward's outputs)."""
+    # (called inside Function.forward, where grad mode is always off: whether
+    # the caller had it on is recorded by rasterize_gaussians before apply)
+    if bool(rs.quick_render) or not getattr(_CALL, "grad_enabled", False):
+        return 0
+    geom = (need[0] or need[1] or (need[2] and _present(sh)) or (need[3] and _present(colors_precomp)) or need[7]
+            or (need[8] and _present(scales)) or (need[9] and _present(rotations))
+            or (need[10] and _present(cov3Ds_precomp)))
+    lang = need[4] and bool(rs.include_feature) and _present(language_feature_precomp)
+    return (_lib.LSR_GWS_GEOM if geom else 0) | (_lib.LSR_GWS_LANG if lang else 0)
 
 
 class _RasterizeGaussians(torch.autograd.Function):
@@ -270,9 +294,13 @@ class _RasterizeGaussians(torch.autograd.Function):
     def forward(ctx, means3D, means2D, sh, colors_precomp, language_feature_precomp,
                 language_feature_weights_quick, language_feature_indices, opacities, scales, rotations,
                 cov3Ds_precomp, raster_settings):
-        color, lang_out, radii, num_rendered, bufs, saved, dims = _run_forward(
+        req = _grad_request(ctx.needs_input_grad, sh, colors_precomp, language_feature_precomp, scales, rotations,
+                            cov3Ds_precomp, raster_settings)
+        color, lang_out, radii, num_rendered, bufs, saved, dims, grad_ws = _run_forward(
             means3D, sh, colors_precomp, language_feature_precomp, language_feature_weights_quick,
-            language_feature_indices, opacities, scales, rotations, cov3Ds_precomp, raster_settings)
+            language_feature_indices, opacities, scales, rotations, cov3Ds_precomp, raster_settings, req)
+        # zeroed accumulators for ONE backward (taken there)
+        ctx.grad_ws = grad_ws
         ctx.raster_settings = raster_settings
         ctx.num_rendered = num_rendered
         # identities of the inputs (GradSink.params: a sink buffer is used only for its own leaf)
@@ -315,6 +343,10 @@ class _RasterizeGaussians(torch.autograd.Function):
                           _ptr(qw) if quick else None, _ptr(qi) if quick else None)
         bin_ = _lib.BwdIn(geom.data_ptr(), binning.data_ptr(), image.data_ptr(), ctx.num_rendered, radii.data_ptr(),
                           grad_color.data_ptr(), _ptr(gl))
+        ws = ctx.grad_ws
+        ctx.grad_ws = None   # a second backward (retain_graph) clears its own
+        if ws is not None:
+            bin_.grad_ws, bin_.grad_ws_bytes, bin_.grad_ws_kind = ws[0].data_ptr(), ws[1], ws[2]
         sink = _sink()
 
         def mk(name, shape, flag):
@@ -333,7 +365,15 @@ class _RasterizeGaussians(torch.autograd.Function):
         g_means3D = mk("means3D", (N, 3), need[0])
         g_sh = mk("shs", tuple(sh.shape), need[2]) if sh is not None else None
         g_col = mk("colors_precomp", (N, 3), need[3]) if col is not None else None
-        g_lang = mk("language_feature_precomp", (N, D), need[4]) if lang is not None else None
+        g_lang = None
+        if lang is not None and need[4]:
+            if sink is not None:
+                g_lang = sink.take("language_feature_precomp", (N, D), dev, ctx.input_ids["language_feature_precomp"])
+            if g_lang is None and ws is not None and ws[3] != _SIZE_MAX:
+                # the forward's zeroed (N, D) accumulator: the library adds into it in place
+                g_lang = ws[0][ws[3]:ws[3] + N * D * 4].view(torch.float32).view(N, D)
+            if g_lang is None:
+                g_lang = torch.empty((N, D), dtype=torch.float32, device=dev)
         g_qw = mk("language_feature_weights_quick", (N, K), need[5]) if (quick and qw is not None) else None
         g_opac = mk("opacities", (N, 1), need[7])
         g_sc = mk("scales", (N, 3), need[8]) if sc is not None else None
@@ -369,9 +409,13 @@ class _RasterizeGaussians(torch.autograd.Function):
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, language_feature_precomp,
                         language_feature_weights_quick, language_feature_indices, opacities, scales, rotations,
                         cov3Ds_precomp, raster_settings):
-    return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, language_feature_precomp,
-                                     language_feature_weights_quick, language_feature_indices, opacities, scales,
-                                     rotations, cov3Ds_precomp, raster_settings)
+    _CALL.grad_enabled = torch.is_grad_enabled()
+    try:
+        return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, language_feature_precomp,
+                                         language_feature_weights_quick, language_feature_indices, opacities, scales,
+                                         rotations, cov3Ds_precomp, raster_settings)
+    finally:
+        _CALL.grad_enabled = False
 
 
 class GaussianRasterizer(nn.Module):

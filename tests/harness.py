@@ -67,7 +67,7 @@ def run_gpu_forward(case, device):
     rs = settings_for(case, device)
     t = gpu_inputs(case, device, requires_grad=False)
     e = torch.empty(0, device=device)
-    color, lang, radii, M, bufs, _, _ = rasterizer._run_forward(
+    color, lang, radii, M, bufs, _, _, _ = rasterizer._run_forward(
         t["means3D"], t.get("shs", e), t.get("colors_precomp", e), t.get("language_feature_precomp", e),
         t.get("language_feature_weights_quick", e), t.get("language_feature_indices", e), t["opacities"],
         t.get("scales", e), t.get("rotations", e), t.get("cov3D_precomp", e), rs)

@@ -160,7 +160,7 @@ def test_cfg5_binning_and_image_properties(gpu):
     rs = settings_for(case, gpu)
     t = gpu_inputs(case, gpu, requires_grad=False)
     e = torch.empty(0, device=gpu)
-    color, lang, radii, M, bufs, _, _ = rasterizer._run_forward(
+    color, lang, radii, M, bufs, _, _, _ = rasterizer._run_forward(
         t["means3D"], t["shs"], e, t["language_feature_precomp"], e, e, t["opacities"], t["scales"],
         t["rotations"], e, rs)
     N, W, H = t["means3D"].shape[0], rs.image_width, rs.image_height

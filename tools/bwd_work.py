@@ -30,7 +30,7 @@ g = {k: v.to(dev) for k, v in g0.items() if isinstance(v, torch.Tensor)}
 rs = bench.settings(cam, dev, 3, True)
 e = torch.empty(0, device=dev)
 with torch.no_grad():
-    _, _, radii, M, bufs, _, _ = rasterizer._run_forward(
+    _, _, radii, M, bufs, _, _, _ = rasterizer._run_forward(
         g["means3D"], g["shs"], e, g["language_feature_precomp"], e, e, g["opacities"], g["scales"],
         g["rotations"], e, rs)
 dec = layout.decode(bufs, N, W, H, M)
