@@ -232,14 +232,15 @@ __global__ void __launch_bounds__(256) k_duplicate(Cam c, int P, const uint8_t* 
     uint32_t o = offs[i] - tiles[i];
     int x0, y0, x1, y1;
     get_rect(A.x, A.y, r, c.gx, c.gy, x0, y0, x1, y1);
-    const CutEllipse e = tile_cull_prep(A, B);
+    const SpanPrep sp = span_prep(A, B);
     int bx0 = x0, by0 = y0, bx1 = x1, by1 = y1;
     cull_box(A.x, A.y, A.z, A.w, B.x, B.z, bx0, by0, bx1, by1);
-    for (int y = y0; y < y1; y++)
-        for (int x = x0; x < x1; x++, o++) {
-            const bool in = x >= bx0 && x < bx1 && y >= by0 && y < by1;
-            rank[o] = (in && tile_keep(e, x, y)) ? atomicAdd(&tile_cnt[y * c.gx + x], 1u) : 0xffffffffu;
-        }
+    for (int y = y0; y < y1; y++) {
+        int sx0 = 0, sx1 = 0;
+        if (y >= by0 && y < by1) row_span(sp, y, bx0, bx1, sx0, sx1);
+        for (int x = x0; x < x1; x++, o++)
+            rank[o] = (x >= sx0 && x < sx1) ? atomicAdd(&tile_cnt[y * c.gx + x], 1u) : 0xffffffffu;
+    }
 }
 
 hipError_t launch_duplicate(const Cam& c, int P, const uint8_t* geom, const int32_t* radii, uint32_t* tile_cnt,
@@ -312,88 +313,112 @@ struct Band {
     }
 };
 
-// Load-balanced rect expansion.  Lane l of a wave owns Gaussian i0 + l with
-// n_l instances (its tile rect clipped to the band); the wave's instances are
-// numbered by an exclusive scan of n_l and handed out 64 at a time, each lane
-// finding its owner by binary search over the scan in LDS.  Every lane does
-// one instance per step however unequal the rects are (a per-lane rect loop
-// runs as long as the wave's largest rect: ~10x the mean here).
-struct WaveRects {
-    int pre[65];   // exclusive scan; pre[64] = total
-    int x0[64], y0[64], w[64];
-    uint64_t key[64];
-    float4 E0[64], E1[64];   // the owners' prepared cut ellipses (tile cull, CutEllipse::pack)
+// Load-balanced expansion of the kept instances.  Lane l of a wave owns
+// Gaussian i0 + l: its cull box clipped to the band, h_l rows.  The wave's
+// rows are numbered by an exclusive scan of h_l and taken 64 at a time
+// (a round): lane j computes row entry r0 + j's kept tile range (row_span,
+// owner found by binary search over the row scan), the round's entries are
+// scanned by width, and each lane walks a contiguous slice of the round's
+// kept instances (one entry search, then along the entries).  Every lane
+// does one kept instance per step however unequal the Gaussians are, and no
+// instance outside the cull is visited or tested.
+struct WaveSpans {
+    int rpre[65];      // exclusive scan of the owners' band rows; [64] = total
+    int epre[65];      // the round's entries: exclusive scan of kept widths; [64] = total
+    float4 P0[64];     // owner's SpanPrep: x, y, vm, vr
+    float4 P1[64];     //                   cb, det, tca, ica
+    float me[64];      //                   me
+    int box[64];       // owner's box columns: bx0 | bx1 << 16
+    int y0[64];        // owner's first band row (band-relative)
+    int ent[64];       // entry: first kept column | band row << 16 | owner << 24
 };
 
-// Wave-uniform: stage the lanes' rects, return the wave's instance total.
-__device__ __forceinline__ int wave_rects_stage(WaveRects& wr, int n, int x0, int y0, int w, float4 A, float4 B)
+// Wave-uniform: stage the lanes' Gaussians, return the wave's row total.
+__device__ __forceinline__ int wave_spans_stage(WaveSpans& ws, int h, int bx0, int bx1, int y0, const SpanPrep& sp)
 {
     const int lane = threadIdx.x & 63;
-    tile_cull_prep(A, B).pack(wr.E0[lane], wr.E1[lane]);
-    int s = n;
+    ws.P0[lane] = make_float4(sp.x, sp.y, sp.vm, sp.vr);
+    ws.P1[lane] = make_float4(sp.cb, sp.det, sp.tca, sp.ica);
+    ws.me[lane] = sp.me;
+    ws.box[lane] = bx0 | (bx1 << 16);
+    ws.y0[lane] = y0;
+    int s = h;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
         const int t = __shfl_up(s, d, 64);
         if (lane >= d) s += t;
     }
-    wr.pre[lane] = s - n;
-    if (lane == 63) wr.pre[64] = s;
-    wr.x0[lane] = x0;
-    wr.y0[lane] = y0;
-    wr.w[lane] = w;
+    ws.rpre[lane] = s - h;
+    if (lane == 63) ws.rpre[64] = s;
     wave_lds_fence();
     return __shfl(s, 63, 64);
 }
 
-// Instance k of the staged wave -> (owner lane, tile x, tile y).
-__device__ __forceinline__ int wave_rects_item(const WaveRects& wr, int k, int& x, int& y)
+// largest o in [0, 64) with pre[o] <= k (pre non-decreasing, pre[64] > k)
+__device__ __forceinline__ int wave_search(const int* pre, int k)
 {
     int o = 0;
 #pragma unroll
     for (int step = 32; step >= 1; step >>= 1)
-        if (wr.pre[o + step] <= k) o += step;
-    const int local = k - wr.pre[o], w = wr.w[o];
-    // exact: (local + 0.5) / w is >= 0.5/w away from an integer, far more
-    // than the approximate reciprocal's error for w, local < 2^16
-    const int dy = (int)__fdividef((float)local + 0.5f, (float)w);
-    y = wr.y0[o] + dy;
-    x = wr.x0[o] + (local - dy * w);
+        if (pre[o + step] <= k) o += step;
     return o;
 }
 
-// Contiguous split of the staged instances: lane l takes [l*q, l*q + q),
-// q = ceil(total / 64); one owner search, then a walk along the rects (LDS
-// reads only when the walk crosses into the next owner).
-struct RectWalk {
-    int o, x, y, xs, xe, left;
-    CutEllipse e;   // owner's cut ellipse, prepared once per owner
-    __device__ __forceinline__ RectWalk(const WaveRects& wr, int k)
+// Wave-uniform: one round's entries (rows r0 .. r0 + 63 of the wave), return
+// the round's kept-instance total.
+__device__ __forceinline__ int wave_spans_round(WaveSpans& ws, int r0, int R, int ty0)
+{
+    const int lane = threadIdx.x & 63;
+    const int e = r0 + lane;
+    int wd = 0, packed = 0;
+    if (e < R) {
+        const int o = wave_search(ws.rpre, e);
+        const int yr = ws.y0[o] + (e - ws.rpre[o]);
+        const float4 p0 = ws.P0[o], p1 = ws.P1[o];
+        const SpanPrep sp{p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w, ws.me[o]};
+        const int bx = ws.box[o];
+        int sx0, sx1;
+        row_span(sp, yr + ty0, bx & 0xffff, bx >> 16, sx0, sx1);
+        wd = sx1 - sx0;
+        packed = sx0 | (yr << 16) | (o << 24);
+    }
+    int s = wd;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(s, d, 64);
+        if (lane >= d) s += t;
+    }
+    ws.epre[lane] = s - wd;
+    if (lane == 63) ws.epre[64] = s;
+    ws.ent[lane] = packed;
+    wave_lds_fence();
+    return __shfl(s, 63, 64);
+}
+
+// A lane's contiguous slice of a round's kept instances: one entry search,
+// then along the entries (LDS reads only when the walk enters the next one).
+struct SpanWalk {
+    int j, x, xe, y, o;
+    __device__ __forceinline__ void enter(const WaveSpans& ws, int k0)
     {
-        o = wave_rects_item(wr, k, x, y);
-        xs = wr.x0[o];
-        xe = xs + wr.w[o];
-        left = wr.pre[o + 1] - k;
-        e = CutEllipse(wr.E0[o], wr.E1[o]);
+        const int p = ws.ent[j];
+        x = (p & 0xffff) + k0;
+        xe = (p & 0xffff) + (ws.epre[j + 1] - ws.epre[j]);
+        y = (p >> 16) & 0xff;
+        o = p >> 24;
+    }
+    __device__ __forceinline__ SpanWalk(const WaveSpans& ws, int k)
+    {
+        j = wave_search(ws.epre, k);
+        enter(ws, k - ws.epre[j]);
     }
     // advance to the next instance (the caller guarantees there is one)
-    __device__ __forceinline__ void next(const WaveRects& wr)
+    __device__ __forceinline__ void next(const WaveSpans& ws)
     {
-        if (--left > 0) {
-            if (++x == xe) {
-                x = xs;
-                ++y;
-            }
-            return;
-        }
-        do { ++o; } while (wr.pre[o + 1] == wr.pre[o]);
-        xs = x = wr.x0[o];
-        xe = xs + wr.w[o];
-        y = wr.y0[o];
-        left = wr.pre[o + 1] - wr.pre[o];
-        e = CutEllipse(wr.E0[o], wr.E1[o]);
+        if (++x < xe) return;
+        do { ++j; } while (ws.epre[j + 1] == ws.epre[j]);
+        enter(ws, 0);
     }
-    // the instance survives the tile cull (y is band-relative)
-    __device__ __forceinline__ bool keep(int ty0) const { return tile_keep(e, x, y + ty0); }
 };
 
 // One Gaussian's binning inputs (radius, the two splat records, depth),
@@ -418,18 +443,28 @@ struct BinRec {
     }
 };
 
-// Lane's Gaussian -> its rect clipped to the band (n = 0 if none).
-__device__ __forceinline__ int band_rect(const Cam& c, const Band& bd, const BinRec& g, int& x0, int& y0, int& w)
+// Lane's Gaussian -> its cull box clipped to the band: columns [x0, x1),
+// first row y0 (band-relative); returns the row count (0 if none).
+__device__ __forceinline__ int band_box(const Cam& c, const Band& bd, const BinRec& g, int& x0, int& x1, int& y0)
 {
-    x0 = y0 = w = 0;
+    x0 = x1 = y0 = 0;
     if (g.r <= 0) return 0;
-    int x1, y1;
+    int y1;
     get_rect(g.A.x, g.A.y, g.r, c.gx, c.gy, x0, y0, x1, y1);
     cull_box(g.A.x, g.A.y, g.A.z, g.A.w, g.B.x, g.B.z, x0, y0, x1, y1);
     y0 = max(y0, bd.ty0);
     y1 = min(y1, bd.ty1);
-    w = x1 - x0;
-    return (y1 > y0 && w > 0) ? w * (y1 - y0) : 0;
+    const int h = (y1 > y0 && x1 > x0) ? y1 - y0 : 0;
+    y0 -= bd.ty0;
+    return h;
+}
+
+// Stage the lane's Gaussian for the span walk; returns the wave's row total.
+__device__ __forceinline__ int stage_gaussian(WaveSpans& ws, const Cam& c, const Band& bd, const BinRec& g)
+{
+    int x0, x1, y0;
+    const int h = band_box(c, bd, g, x0, x1, y0);
+    return wave_spans_stage(ws, h, x0, x1, y0, span_prep(g.A, g.B));
 }
 
 template <int BB>
@@ -439,7 +474,7 @@ __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int r
                                                          uint32_t* __restrict__ cls_cnt)
 {
     extern __shared__ uint32_t hist[];
-    __shared__ WaveRects wrs[BB / 64];
+    __shared__ WaveSpans wss[BB / 64];
     const int T = c.gx * c.gy;
 #if LSR_COUNT_XCD
     // chunk-major, XCD-aware (as k_bin_scatter): a chunk's bands share an L2
@@ -455,7 +490,7 @@ __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int r
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) cls_cnt[LSR_TICKET_WORD] = 0;
     for (int k = threadIdx.x; k < bd.nt; k += BB) hist[k] = 0;
     __syncthreads();
-    WaveRects& wr = wrs[threadIdx.x >> 6];
+    WaveSpans& ws = wss[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     const int g0 = blk * chunk, g1 = min(P, g0 + chunk);
 #ifdef LSR_PROBE_CNT
@@ -466,25 +501,26 @@ __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int r
     for (int i0 = g0 + (threadIdx.x & ~63); i0 < g1; i0 += BB) {
         const BinRec cur = nx;
         nx.load(geom, P, g1, radii, i0 + BB + lane, false);
-        int x0, y0, w;
-        const int n = band_rect(c, bd, cur, x0, y0, w);
-        const int tot = wave_rects_stage(wr, n, x0, y0 - bd.ty0, w, cur.A, cur.B);
-        const int q = (tot + 63) >> 6;
-        int k = lane * q;
-        const int kend = min(tot, k + q);
-        if (k < kend) {
-            RectWalk rw(wr, k);
-            for (;;) {
-#ifdef LSR_PROBE_CNT   // timing probe only (wrong counts): 1 = no LDS atomics, 2 = no tile-cull test either
-                if (LSR_PROBE_CNT == 1 ? rw.keep(bd.ty0) : true) probe_acc += (uint32_t)(rw.y * c.gx + rw.x);
+        const int R = stage_gaussian(ws, c, bd, cur);
+        for (int r0 = 0; r0 < R; r0 += 64) {
+            const int K = wave_spans_round(ws, r0, R, bd.ty0);
+            const int q = (K + 63) >> 6;
+            int k = lane * q;
+            const int kend = min(K, k + q);
+            if (k < kend) {
+                SpanWalk sw(ws, k);
+                for (;;) {
+#ifdef LSR_PROBE_CNT   // timing probe only (wrong counts): no LDS atomics
+                    probe_acc += (uint32_t)(sw.y * c.gx + sw.x);
 #else
-                if (rw.keep(bd.ty0)) atomicAdd(&hist[rw.y * c.gx + rw.x], 1u);
+                    atomicAdd(&hist[sw.y * c.gx + sw.x], 1u);
 #endif
-                if (++k >= kend) break;
-                rw.next(wr);
+                    if (++k >= kend) break;
+                    sw.next(ws);
+                }
             }
+            wave_lds_fence();
         }
-        wave_lds_fence();
     }
 #ifdef LSR_PROBE_CNT
     if (probe_acc == 0xdeadbeefu) hist[0] = probe_acc;
@@ -678,7 +714,8 @@ __global__ void __launch_bounds__(BB) k_bin_scatter(Cam c, int P, int chunk, int
                                                            uint64_t* __restrict__ keys)
 {
     extern __shared__ uint32_t base[];
-    __shared__ WaveRects wrs[BB / 64];
+    __shared__ WaveSpans wss[BB / 64];
+    __shared__ uint64_t wkey[BB];   // the lanes' (depth, id) keys
     const int T = c.gx * c.gy;
     const int o = xcd_remap(blockIdx.x, gridDim.x);
     const int blk = o / S;
@@ -686,7 +723,8 @@ __global__ void __launch_bounds__(BB) k_bin_scatter(Cam c, int P, int chunk, int
     const uint32_t* row = table + (size_t)blk * table_stride(T) + bd.t0;
     for (int k = threadIdx.x; k < bd.nt; k += BB) base[k] = tile_start[bd.t0 + k] + row[k];
     __syncthreads();
-    WaveRects& wr = wrs[threadIdx.x >> 6];
+    WaveSpans& ws = wss[threadIdx.x >> 6];
+    uint64_t* const key = wkey + (threadIdx.x & ~63);
     const int lane = threadIdx.x & 63;
     const int g0 = blk * chunk, g1 = min(P, g0 + chunk);
     BinRec nx;
@@ -695,43 +733,41 @@ __global__ void __launch_bounds__(BB) k_bin_scatter(Cam c, int P, int chunk, int
         const int i = i0 + lane;
         const BinRec cur = nx;
         nx.load(geom, P, g1, radii, i0 + BB + lane, true);
-        int x0, y0, w;
-        const int n = band_rect(c, bd, cur, x0, y0, w);
-        if (n > 0) wr.key[lane] = ((uint64_t)__float_as_uint(cur.depth) << 32) | (uint32_t)i;
-        const int tot = wave_rects_stage(wr, n, x0, y0 - bd.ty0, w, cur.A, cur.B);
-        const int q = (tot + 63) >> 6;
-        int k = lane * q;
-        const int kend = min(tot, k + q);
-        if (k < kend) {
-            RectWalk rw(wr, k);
-            // two instances per step: both LDS-atomic returns in flight
-            for (;;) {
-                const bool oka = rw.keep(bd.ty0);
-                const uint32_t sa = oka ? atomicAdd(&base[rw.y * c.gx + rw.x], 1u) : 0u;
-                const uint64_t ka = wr.key[rw.o];
-                const bool two = k + 1 < kend;
-                bool okb = false;
-                uint32_t sb = 0;
-                uint64_t kb = 0;
-                if (two) {
-                    rw.next(wr);
-                    okb = rw.keep(bd.ty0);
-                    sb = okb ? atomicAdd(&base[rw.y * c.gx + rw.x], 1u) : 0u;
-                    kb = wr.key[rw.o];
-                }
+        key[lane] = ((uint64_t)__float_as_uint(cur.depth) << 32) | (uint32_t)i;
+        const int R = stage_gaussian(ws, c, bd, cur);
+        for (int r0 = 0; r0 < R; r0 += 64) {
+            const int K = wave_spans_round(ws, r0, R, bd.ty0);
+            const int q = (K + 63) >> 6;
+            int k = lane * q;
+            const int kend = min(K, k + q);
+            if (k < kend) {
+                SpanWalk sw(ws, k);
+                // two instances per step: both LDS-atomic returns in flight
+                for (;;) {
+                    const uint32_t sa = atomicAdd(&base[sw.y * c.gx + sw.x], 1u);
+                    const uint64_t ka = key[sw.o];
+                    const bool two = k + 1 < kend;
+                    uint32_t sb = 0;
+                    uint64_t kb = 0;
+                    if (two) {
+                        sw.next(ws);
+                        sb = atomicAdd(&base[sw.y * c.gx + sw.x], 1u);
+                        kb = key[sw.o];
+                    }
 #if LSR_SCATTER_PROBE
-                if (oka && sa == 0xffffffffu) keys[0] = ka;
-                if (okb && sb == 0xffffffffu) keys[0] = kb;
+                    if (sa == 0xffffffffu) keys[0] = ka;
+                    if (two && sb == 0xffffffffu) keys[0] = kb;
 #else
-                if (oka) keys[sa] = ka;
-                if (okb) keys[sb] = kb;
+                    keys[sa] = ka;
+                    if (two) keys[sb] = kb;
 #endif
-                k += 2;
-                if (k >= kend) break;
-                rw.next(wr);
+                    k += 2;
+                    if (k >= kend) break;
+                    sw.next(ws);
+                }
             }
+            wave_lds_fence();
         }
-        wave_lds_fence();
     }
 }
 

@@ -321,50 +321,9 @@ __device__ __forceinline__ bool block_overlap(float x, float y, uint32_t ext, in
 // every pair the blend would accept survives (results stay bit-identical);
 // the bounding-box test (block_overlap) keeps far more false candidates for
 // thin, rotated splats.
-// The test with its per-Gaussian part (threshold, reciprocals) prepared once,
-// for loops that test one Gaussian against many rectangles (the binning's
-// tile cull); rect_overlap_exact below is the same sequence of operations.
-struct CutEllipse {
-    float x, y, ca, cb, cc, thr, ica, icc;
-    bool all;   // degenerate / no cut: every rectangle is kept
-    __device__ __forceinline__ CutEllipse() {}
-    // packed form for LDS staging: {x, y, ca, cb}, {cc, thr, ica, icc}; `all`
-    // travels as thr = +inf (then every path of meets() returns true)
-    __device__ __forceinline__ void pack(float4& p0, float4& p1) const
-    {
-        p0 = make_float4(x, y, ca, cb);
-        p1 = make_float4(cc, all ? INFINITY : thr, ica, icc);
-    }
-    __device__ __forceinline__ CutEllipse(const float4& p0, const float4& p1)
-        : x(p0.x), y(p0.y), ca(p0.z), cb(p0.w), cc(p1.x), thr(p1.y), ica(p1.z), icc(p1.w), all(p1.y == INFINITY) {}
-    __device__ __forceinline__ CutEllipse(float x_, float y_, float ca_, float cb_, float cc_, float cut)
-        : x(x_), y(y_), ca(ca_), cb(cb_), cc(cc_)
-    {
-        all = !(ca > 0.f) || !(cc > 0.f) || !(cut > -3.0e38f);
-        thr = fmaf(-2.f * cut, 1.001f, 1e-3f);
-        ica = 1.f / ca;
-        icc = 1.f / cc;
-    }
-    // does the ellipse meet the (EX+1) x (EY+1) rectangle at (bx, by)?
-    __device__ __forceinline__ bool meets(int bx, int by, float EX, float EY) const
-    {
-        if (all) return true;
-        const float u1 = x - (float)bx, u0 = u1 - EX;   // dx over the rectangle's columns
-        const float v1 = y - (float)by, v0 = v1 - EY;   // dy over its rows
-        if (u0 <= 0.f && u1 >= 0.f && v0 <= 0.f && v1 >= 0.f) return true;
-        auto q = [&](float u, float v) { return fmaf(ca * u, u, fmaf(2.f * cb * u, v, cc * v * v)); };
-        const float va = fminf(fmaxf(-cb * u0 * icc, v0), v1);
-        const float vb = fminf(fmaxf(-cb * u1 * icc, v0), v1);
-        const float ua = fminf(fmaxf(-cb * v0 * ica, u0), u1);
-        const float ub = fminf(fmaxf(-cb * v1 * ica, u0), u1);
-        const float qmin = fminf(fminf(q(u0, va), q(u1, vb)), fminf(q(ua, v0), q(ub, v1)));
-        return !(qmin > thr);
-    }
-};
-
-// rect_overlap_exact: the same test for the (EX+1) x (EY+1) rectangle at
-// (bx, by), in one piece (the reciprocals only past the early exits: the
-// render's staging mostly exits early).
+// rect_overlap_exact: the test for the (EX+1) x (EY+1) rectangle at (bx, by)
+// (the reciprocals only past the early exits: the render's staging mostly
+// exits early).
 __device__ __forceinline__ bool rect_overlap_exact(float x, float y, float ca, float cb, float cc, float cut,
                                                    int bx, int by, float EX, float EY)
 {
@@ -397,13 +356,13 @@ __device__ __forceinline__ bool block_overlap_exact(float x, float y, float ca, 
 #define LSR_TILE_CULL 1     // 0: the reference's full rect lists (A/B timing only; the oracle's cull=False)
 #endif
 // The tile cull's box: the tiles whose 16x16 pixel rectangle meets the
-// axis-aligned box of the cut ellipse {q <= thr} (q, thr as in CutEllipse),
-// widened by 1e-4 relative + 0.5 px.  The cull keeps an instance (Gaussian,
-// tile) iff the tile is inside this box AND the exact test meets() passes;
-// the binning walks only the box (fewer instances visited and tested than in
-// the 3-sigma rect), the oracle restates the same rule (lso_cull_box).  A
-// tile outside the box cannot meet the ellipse, so nothing that contributes
-// is dropped (tests/test_oracle.py::test_tile_cull_changes_no_output,
+// axis-aligned box of the cut ellipse {q <= thr}, q(d) = ca dx^2 + 2 cb dx dy
+// + cc dy^2, thr = -2 cut (1.001) + 1e-3, widened by 1e-4 relative + 0.5 px.
+// The cull keeps an instance (Gaussian, tile) iff the tile is inside this box
+// AND inside its row's span (row_span below); the oracle restates the same
+// rule (lso_cull_box, lso_row_span).  A tile outside both cannot meet the
+// ellipse, so nothing that contributes is dropped
+// (tests/test_oracle.py::test_tile_cull_changes_no_output,
 // tests/test_cull_vs_full.py).  Shrinks [x0, x1) x [y0, y1) in place.
 __device__ __forceinline__ void cull_box(float x, float y, float ca, float cb, float cc, float cut, int& x0, int& y0,
                                          int& x1, int& y1)
@@ -425,18 +384,63 @@ __device__ __forceinline__ void cull_box(float x, float y, float ca, float cb, f
     y1 = min(y1, f2i(fmaxf(ty1, -1.f)));
 }
 
-__device__ __forceinline__ CutEllipse tile_cull_prep(const float4& A, const float4& B)
+// Row-span tile cull.  Per Gaussian, the cut ellipse {q <= thr} (cull_box)
+// is intersected with each tile row's pixel band [16 ty,
+// 16 ty + 15]; the x-extent of that piece, widened by 1e-3 of the ellipse's
+// half width + 0.05 px, is a contiguous tile range.  The cull keeps (Gaussian,
+// tile) iff the tile is in cull_box and in its row's range, so the binning
+// walks exactly the kept instances, with no per-tile test.  Over a row the
+// right edge u(v) = (-cb v + sqrt(thr ca - det v^2)) / ca is concave in v, so
+// its maximum is at the row's v nearest v_r = -cb sqrt(thr / (det cc)) (the
+// ellipse's rightmost point), the left edge's minimum at -v_r.  Rows outside
+// |v| <= the (widened) vertical half extent are empty.  Restated operation
+// for operation by the oracle (lso_span_prep / lso_row_span).
+struct SpanPrep {
+    float x, y, vm, vr, cb, det, tca, ica, me;
+};
+__device__ __forceinline__ SpanPrep span_prep(float x, float y, float ca, float cb, float cc, float cut)
 {
-    return CutEllipse(A.x, A.y, A.z, A.w, B.x, B.z);
+    SpanPrep s;
+    s.x = x;
+    s.y = y;
+    const float det = ca * cc - cb * cb;
+    const float thr = fmaf(-2.f * cut, 1.001f, 1e-3f);
+    const float tcd = thr / det;
+    const bool all = !LSR_TILE_CULL || !(ca > 0.f) || !(cc > 0.f) || !(cut > -3.0e38f) || !(det > 0.f) ||
+                     !(tcd < 1.0e30f);
+    if (all) {   // degenerate / no cut: every tile of the box row
+        s.vm = INFINITY; s.vr = 0.f; s.cb = 0.f; s.det = 1.f; s.tca = 1.f; s.ica = 1.f; s.me = INFINITY;
+        return s;
+    }
+    s.vm = fmaf(sqrtf(tcd * ca), 1.0001f, 0.01f);
+    s.vr = -cb * sqrtf(tcd / cc);
+    s.cb = cb;
+    s.det = det;
+    s.tca = thr * ca;
+    s.ica = 1.f / ca;
+    s.me = fmaf(sqrtf(tcd * cc), 1e-3f, 0.05f);
+    return s;
 }
-__device__ __forceinline__ bool tile_keep(const CutEllipse& e, int tx, int ty)
+// Kept tiles [sx0, sx1) of tile row ty inside the box columns [bx0, bx1).
+__device__ __forceinline__ void row_span(const SpanPrep& s, int ty, int bx0, int bx1, int& sx0, int& sx1)
 {
-    if (!LSR_TILE_CULL) return true;
-    return e.meets(tx * LSR_TILE, ty * LSR_TILE, 15.f, 15.f);
+    const float v1 = s.y - (float)(ty * LSR_TILE), v0 = v1 - 15.f;
+    const float w0 = fmaxf(v0, -s.vm), w1 = fminf(v1, s.vm);
+    const float a = fminf(fmaxf(s.vr, w0), w1), b = fminf(fmaxf(-s.vr, w0), w1);
+    const float ra = sqrtf(fmaxf(fmaf(-s.det * a, a, s.tca), 0.f));
+    const float rb = sqrtf(fmaxf(fmaf(-s.det * b, b, s.tca), 0.f));
+    const float umax = fmaf(ra - s.cb * a, s.ica, s.me);
+    const float umin = fmaf(-rb - s.cb * b, s.ica, -s.me);
+    // tile t meets [x - umax, x - umin] iff 16 t <= x - umin and 16 t + 15 >= x - umax
+    const float fx0 = ceilf((s.x - umax - 15.f) / 16.f);
+    const float fx1 = floorf((s.x - umin) / 16.f) + 1.f;
+    sx0 = f2i(fminf(fmaxf(fx0, (float)bx0), (float)bx1));
+    sx1 = f2i(fminf(fmaxf(fx1, (float)bx0), (float)bx1));
+    if (!(w0 <= w1) || sx1 < sx0) sx1 = sx0;
 }
-__device__ __forceinline__ bool tile_keep(const float4& A, const float4& B, int tx, int ty)
+__device__ __forceinline__ SpanPrep span_prep(const float4& A, const float4& B)
 {
-    return tile_keep(tile_cull_prep(A, B), tx, ty);
+    return span_prep(A.x, A.y, A.z, A.w, B.x, B.z);
 }
 
 // ------------------------------------------------------------- layouts --

@@ -332,33 +332,10 @@ float lso_power_cut(float o)
     return (float)(-log((double)(255.0f * o))) - 0.02f;
 }
 
-/* Does the cut ellipse {d : Q(d) <= -2 cut} of the Gaussian at (x, y) with
- * conic (ca, cb, cc) meet the 16x16 tile (tx, ty)?  Q is convex: its minimum
- * over the tile is 0 with the centre inside, else on an edge at a clamped
- * stationary point; relative + absolute margin.  Operation for operation
- * lsr_device.h rect_overlap_exact with a 15 x 15 extent. */
-int lso_tile_keep(float x, float y, float ca, float cb, float cc, float cut, int tx, int ty)
-{
-    if (!(ca > 0.f) || !(cc > 0.f) || !(cut > -3.0e38f)) return 1;
-    const float thr = fmaf(-2.f * cut, 1.001f, 1e-3f);
-    const float u1 = x - (float)(tx * TILE), u0 = u1 - 15.f;
-    const float v1 = y - (float)(ty * TILE), v0 = v1 - 15.f;
-    if (u0 <= 0.f && u1 >= 0.f && v0 <= 0.f && v1 >= 0.f) return 1;
-    const float ica = 1.f / ca, icc = 1.f / cc;
-#define LSO_Q(u, v) fmaf(ca * (u), (u), fmaf(2.f * cb * (u), (v), cc * (v) * (v)))
-    const float va = fminf(fmaxf(-cb * u0 * icc, v0), v1);
-    const float vb = fminf(fmaxf(-cb * u1 * icc, v0), v1);
-    const float ua = fminf(fmaxf(-cb * v0 * ica, u0), u1);
-    const float ub = fminf(fmaxf(-cb * v1 * ica, u0), u1);
-    const float qmin = fminf(fminf(LSO_Q(u0, va), LSO_Q(u1, vb)), fminf(LSO_Q(ua, v0), LSO_Q(ub, v1)));
-#undef LSO_Q
-    return !(qmin > thr);
-}
-
 /* The product's cull box (csrc/lsr_device.h cull_box), restated operation for
  * operation: the tiles meeting the cut ellipse's axis-aligned box, widened by
  * 1e-4 relative + 0.5 px.  The cull keeps (Gaussian, tile) iff the tile is in
- * the box AND lso_tile_keep passes. */
+ * the box AND in its row's span (lso_row_span). */
 void lso_cull_box(float x, float y, float ca, float cb, float cc, float cut, int* r0, int* r1)
 {
     if (!(ca > 0.f) || !(cc > 0.f) || !(cut > -3.0e38f)) return;
@@ -376,10 +353,67 @@ void lso_cull_box(float x, float y, float ca, float cb, float cc, float cut, int
     r1[1] = imin(r1[1], f2i(fmaxf(ty1, -1.f)));
 }
 
-static inline int keep_instance(const lso_geom* g, int i, float cut, int tx, int ty)
+/* The product's row-span cull (csrc/lsr_device.h span_prep / row_span),
+ * restated operation for operation: per tile row ty, the cut ellipse's
+ * x-extent over the row's pixel band [16 ty, 16 ty + 15], widened by 1e-3 of
+ * its half width + 0.05 px, as the tile range [sx0, sx1) inside the box
+ * columns [bx0, bx1).  The right edge (-cb v + sqrt(thr ca - det v^2)) / ca
+ * is concave in v: its maximum over the row is at the row's v nearest the
+ * ellipse's rightmost point v_r = -cb sqrt(thr / (det cc)); the left edge's
+ * minimum at -v_r; rows beyond the widened vertical half extent are empty. */
+void lso_span_prep(float x, float y, float ca, float cb, float cc, float cut, lso_span* s)
 {
+    s->x = x;
+    s->y = y;
+    const float det = ca * cc - cb * cb;
+    const float thr = fmaf(-2.f * cut, 1.001f, 1e-3f);
+    const float tcd = thr / det;
+    if (!(ca > 0.f) || !(cc > 0.f) || !(cut > -3.0e38f) || !(det > 0.f) || !(tcd < 1.0e30f)) {
+        s->vm = INFINITY; s->vr = 0.f; s->cb = 0.f; s->det = 1.f; s->tca = 1.f; s->ica = 1.f; s->me = INFINITY;
+        return;
+    }
+    s->vm = fmaf(sqrtf(tcd * ca), 1.0001f, 0.01f);
+    s->vr = -cb * sqrtf(tcd / cc);
+    s->cb = cb;
+    s->det = det;
+    s->tca = thr * ca;
+    s->ica = 1.f / ca;
+    s->me = fmaf(sqrtf(tcd * cc), 1e-3f, 0.05f);
+}
+
+void lso_row_span(const lso_span* s, int ty, int bx0, int bx1, int* sx0, int* sx1)
+{
+    const float v1 = s->y - (float)(ty * TILE), v0 = v1 - 15.f;
+    const float w0 = fmaxf(v0, -s->vm), w1 = fminf(v1, s->vm);
+    const float a = fminf(fmaxf(s->vr, w0), w1), b = fminf(fmaxf(-s->vr, w0), w1);
+    const float ra = sqrtf(fmaxf(fmaf(-s->det * a, a, s->tca), 0.f));
+    const float rb = sqrtf(fmaxf(fmaf(-s->det * b, b, s->tca), 0.f));
+    const float umax = fmaf(ra - s->cb * a, s->ica, s->me);
+    const float umin = fmaf(-rb - s->cb * b, s->ica, -s->me);
+    const float fx0 = ceilf((s->x - umax - 15.f) / 16.f);
+    const float fx1 = floorf((s->x - umin) / 16.f) + 1.f;
+    *sx0 = f2i(fminf(fmaxf(fx0, (float)bx0), (float)bx1));
+    *sx1 = f2i(fminf(fmaxf(fx1, (float)bx0), (float)bx1));
+    if (!(w0 <= w1) || *sx1 < *sx0) *sx1 = *sx0;
+}
+
+/* The culled instances of Gaussian i: rows [r0[1], r1[1]) of the box, each
+ * with its kept column range (cull) or the whole rect row (no cull). */
+static inline void gaussian_prep(const lso_geom* g, int i, float cut, int cull, int* r0, int* r1, lso_span* sp)
+{
+    if (!cull) return;
     const float* co = g->conic_opacity + 4 * i;
-    return lso_tile_keep(g->xy[2 * i], g->xy[2 * i + 1], co[0], co[1], co[2], cut, tx, ty);
+    lso_cull_box(g->xy[2 * i], g->xy[2 * i + 1], co[0], co[1], co[2], cut, r0, r1);
+    lso_span_prep(g->xy[2 * i], g->xy[2 * i + 1], co[0], co[1], co[2], cut, sp);
+}
+static inline void row_range(const lso_span* sp, int cull, int y, const int* r0, const int* r1, int* x0, int* x1)
+{
+    if (!cull) {
+        *x0 = r0[0];
+        *x1 = r1[0];
+        return;
+    }
+    lso_row_span(sp, y, r0[0], r1[0], x0, x1);
 }
 
 int64_t lso_num_rendered_ex(const lso_settings* s, int N, const lso_geom* g, int cull)
@@ -392,10 +426,14 @@ int64_t lso_num_rendered_ex(const lso_settings* s, int N, const lso_geom* g, int
         int r0[2], r1[2];
         get_rect(g->xy[2 * i], g->xy[2 * i + 1], g->radii[i], gx, gy, r0, r1);
         const float cut = lso_power_cut(g->conic_opacity[4 * i + 3]);
-        const float* co = g->conic_opacity + 4 * i;
-        lso_cull_box(g->xy[2 * i], g->xy[2 * i + 1], co[0], co[1], co[2], cut, r0, r1);
-        for (int y = r0[1]; y < r1[1]; y++)
-            for (int x = r0[0]; x < r1[0]; x++) m += keep_instance(g, i, cut, x, y);
+        lso_span sp;
+        gaussian_prep(g, i, cut, 1, r0, r1, &sp);
+        if (r1[0] <= r0[0]) continue;
+        for (int y = r0[1]; y < r1[1]; y++) {
+            int x0, x1;
+            row_range(&sp, 1, y, r0, r1, &x0, &x1);
+            m += x1 - x0;
+        }
     }
     return m;
 }
@@ -426,13 +464,14 @@ void lso_binning_ex(const lso_settings* s, int N, const lso_geom* g, uint32_t* p
         int r0[2], r1[2];
         get_rect(g->xy[2 * i], g->xy[2 * i + 1], g->radii[i], gx, gy, r0, r1);
         const float cut = lso_power_cut(g->conic_opacity[4 * i + 3]);
-        if (cull) {
-            const float* co = g->conic_opacity + 4 * i;
-            lso_cull_box(g->xy[2 * i], g->xy[2 * i + 1], co[0], co[1], co[2], cut, r0, r1);
+        lso_span sp;
+        gaussian_prep(g, i, cut, cull, r0, r1, &sp);
+        if (r1[0] <= r0[0]) continue;
+        for (int y = r0[1]; y < r1[1]; y++) {
+            int x0, x1;
+            row_range(&sp, cull, y, r0, r1, &x0, &x1);
+            for (int x = x0; x < x1; x++) cnt[y * gx + x + 1]++;
         }
-        for (int y = r0[1]; y < r1[1]; y++)
-            for (int x = r0[0]; x < r1[0]; x++)
-                if (!cull || keep_instance(g, i, cut, x, y)) cnt[y * gx + x + 1]++;
     }
     for (int t = 0; t < T; t++) cnt[t + 1] += cnt[t];
     uint64_t* keys = (uint64_t*)malloc((size_t)(M > 0 ? M : 1) * sizeof(uint64_t));
@@ -445,16 +484,17 @@ void lso_binning_ex(const lso_settings* s, int N, const lso_geom* g, uint32_t* p
         uint32_t db;
         memcpy(&db, &g->depth[i], 4);
         const float cut = lso_power_cut(g->conic_opacity[4 * i + 3]);
-        if (cull) {
-            const float* co = g->conic_opacity + 4 * i;
-            lso_cull_box(g->xy[2 * i], g->xy[2 * i + 1], co[0], co[1], co[2], cut, r0, r1);
-        }
-        for (int y = r0[1]; y < r1[1]; y++)
-            for (int x = r0[0]; x < r1[0]; x++) {
-                if (cull && !keep_instance(g, i, cut, x, y)) continue;
+        lso_span sp;
+        gaussian_prep(g, i, cut, cull, r0, r1, &sp);
+        if (r1[0] <= r0[0]) continue;
+        for (int y = r0[1]; y < r1[1]; y++) {
+            int x0, x1;
+            row_range(&sp, cull, y, r0, r1, &x0, &x1);
+            for (int x = x0; x < x1; x++) {
                 int t = y * gx + x;
                 keys[cur[t]++] = ((uint64_t)db << 32) | (uint32_t)i;
             }
+        }
     }
     for (int t = 0; t < T; t++) {
         uint32_t a = cnt[t], b = cnt[t + 1];

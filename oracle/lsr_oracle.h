@@ -87,8 +87,9 @@ void lso_binning(const lso_settings* s, int N, const lso_geom* g,
                  uint32_t* point_list, uint32_t* ranges);
 
 /* The same with the product's tile cull (cull != 0): an instance (Gaussian,
- * tile) of the rect is kept only if the Gaussian's cut ellipse meets the
- * 16x16 tile (lso_tile_keep, the restatement of lsr_device.h tile_keep).
+ * tile) of the rect is kept only if the tile lies in the Gaussian's cull box
+ * and in its row's span of the widened cut ellipse (lso_cull_box,
+ * lso_row_span: the restatements of lsr_device.h cull_box / row_span).
  * Dropped instances have alpha < 1/255 at every pixel of their tile, so the
  * rendered outputs equal lso_binning's; the lists shrink.  cull = 0 is
  * lso_num_rendered / lso_binning. */
@@ -96,10 +97,14 @@ int64_t lso_num_rendered_ex(const lso_settings* s, int N, const lso_geom* g, int
 void lso_binning_ex(const lso_settings* s, int N, const lso_geom* g,
                     uint32_t* point_list, uint32_t* ranges, int cull);
 float lso_power_cut(float opacity);
-int lso_tile_keep(float x, float y, float ca, float cb, float cc, float cut, int tx, int ty);
 /* the cull's box (lsr_device.h cull_box): shrinks the rect [r0, r1) to the
- * tiles meeting the cut ellipse's bounding box; kept = in box && lso_tile_keep */
+ * tiles meeting the cut ellipse's bounding box */
 void lso_cull_box(float x, float y, float ca, float cb, float cc, float cut, int* r0, int* r1);
+/* the per-Gaussian part of the row-span cull and one row's kept tile range
+ * [sx0, sx1) inside the box columns [bx0, bx1) (lsr_device.h span_prep / row_span) */
+typedef struct { float x, y, vm, vr, cb, det, tca, ica, me; } lso_span;
+void lso_span_prep(float x, float y, float ca, float cb, float cc, float cut, lso_span* s);
+void lso_row_span(const lso_span* s, int ty, int bx0, int bx1, int* sx0, int* sx1);
 
 /* A.3 render forward.  out_color 3*H*W; out_lang Dout*H*W (Dout = D dense
  * or quick_dim); final_T, n_contrib H*W.  Tiles are processed in parallel
