@@ -364,6 +364,19 @@ __device__ __forceinline__ int wave_search(const int* pre, int k)
     return o;
 }
 
+// Row entry e of the staged wave: its owner (returned), band row yr and kept
+// columns [sx0, sx1).
+__device__ __forceinline__ int row_entry(const WaveSpans& ws, int e, int ty0, int& sx0, int& sx1, int& yr)
+{
+    const int o = wave_search(ws.rpre, e);
+    yr = ws.y0[o] + (e - ws.rpre[o]);
+    const float4 p0 = ws.P0[o], p1 = ws.P1[o];
+    const SpanPrep sp{p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w, ws.me[o]};
+    const int bx = ws.box[o];
+    row_span(sp, yr + ty0, bx & 0xffff, bx >> 16, sx0, sx1);
+    return o;
+}
+
 // Wave-uniform: one round's entries (rows r0 .. r0 + 63 of the wave), return
 // the round's kept-instance total.
 __device__ __forceinline__ int wave_spans_round(WaveSpans& ws, int r0, int R, int ty0)
@@ -372,13 +385,8 @@ __device__ __forceinline__ int wave_spans_round(WaveSpans& ws, int r0, int R, in
     const int e = r0 + lane;
     int wd = 0, packed = 0;
     if (e < R) {
-        const int o = wave_search(ws.rpre, e);
-        const int yr = ws.y0[o] + (e - ws.rpre[o]);
-        const float4 p0 = ws.P0[o], p1 = ws.P1[o];
-        const SpanPrep sp{p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w, ws.me[o]};
-        const int bx = ws.box[o];
-        int sx0, sx1;
-        row_span(sp, yr + ty0, bx & 0xffff, bx >> 16, sx0, sx1);
+        int sx0, sx1, yr;
+        const int o = row_entry(ws, e, ty0, sx0, sx1, yr);
         wd = sx1 - sx0;
         packed = sx0 | (yr << 16) | (o << 24);
     }
@@ -502,32 +510,45 @@ __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int r
         const BinRec cur = nx;
         nx.load(geom, P, g1, radii, i0 + BB + lane, false);
         const int R = stage_gaussian(ws, c, bd, cur);
-        for (int r0 = 0; r0 < R; r0 += 64) {
-            const int K = wave_spans_round(ws, r0, R, bd.ty0);
-            const int q = (K + 63) >> 6;
-            int k = lane * q;
-            const int kend = min(K, k + q);
-            if (k < kend) {
-                SpanWalk sw(ws, k);
-                for (;;) {
+        // every row entry adds its kept range [sx0, sx1) to the histogram as
+        // a difference (+1 at sx0, -1 at sx1 inside the row): two LDS atomics
+        // per (Gaussian, row) instead of one per instance
+        for (int e = lane; e < R; e += 64) {
+            int sx0, sx1, yr;
+            row_entry(ws, e, bd.ty0, sx0, sx1, yr);
+            if (sx1 > sx0) {
 #ifdef LSR_PROBE_CNT   // timing probe only (wrong counts): no LDS atomics
-                    probe_acc += (uint32_t)(sw.y * c.gx + sw.x);
+                probe_acc += (uint32_t)(yr * c.gx + sx0 + sx1);
 #else
-                    atomicAdd(&hist[sw.y * c.gx + sw.x], 1u);
+                atomicAdd(&hist[yr * c.gx + sx0], 1u);
+                if (sx1 < c.gx) atomicAdd(&hist[yr * c.gx + sx1], 0xffffffffu);
 #endif
-                    if (++k >= kend) break;
-                    sw.next(ws);
-                }
             }
-            wave_lds_fence();
         }
+        wave_lds_fence();
     }
 #ifdef LSR_PROBE_CNT
     if (probe_acc == 0xdeadbeefu) hist[0] = probe_acc;
 #endif
     __syncthreads();
+    // per band row: counts = running sum of the differences (mod 2^32), written
+    // straight into the block's table row; one wave per row, 64 columns a step
     uint32_t* row = table + (size_t)blk * table_stride(T) + bd.t0;
-    for (int k = threadIdx.x; k < bd.nt; k += BB) row[k] = hist[k];
+    const int nrows = bd.ty1 - bd.ty0;
+    for (int r = threadIdx.x >> 6; r < nrows; r += BB / 64) {
+        uint32_t carry = 0;
+        for (int x0 = 0; x0 < c.gx; x0 += 64) {
+            const int x = x0 + lane;
+            uint32_t v = x < c.gx ? hist[r * c.gx + x] : 0u;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t t = __shfl_up(v, d, 64);
+                if (lane >= d) v += t;
+            }
+            if (x < c.gx) row[r * c.gx + x] = carry + v;
+            carry += __shfl(v, 63, 64);
+        }
+    }
 }
 
 // Column scan: table[b][t] <- sum_{b' < b} table[b'][t]; tile_cnt[t] <- total.
