@@ -727,7 +727,7 @@ __global__ void __launch_bounds__(256) k_tile_start_apply(int T, const uint32_t*
 // L2 and the partial key lines the XCD has open at once span ~one chunk's
 // tiles instead of one per resident block.
 template <int BB>
-__global__ void __launch_bounds__(BB) k_bin_scatter(Cam c, int P, int chunk, int rows, int S,
+__global__ void __launch_bounds__(BB) k_bin_scatter(Cam c, int P, int chunk, int km, int rows, int S,
                                                            const uint8_t* __restrict__ geom,
                                                            const int32_t* __restrict__ radii,
                                                            const uint32_t* __restrict__ table,
@@ -739,15 +739,15 @@ __global__ void __launch_bounds__(BB) k_bin_scatter(Cam c, int P, int chunk, int
     __shared__ uint64_t wkey[BB];   // the lanes' (depth, id) keys
     const int T = c.gx * c.gy;
     const int o = xcd_remap(blockIdx.x, gridDim.x);
-    const int blk = o / S;
-    const Band bd(c, rows, o - blk * S);
+    const int blk = (o / S) * km;   // first of the km count chunks this block places
+    const Band bd(c, rows, o - (o / S) * S);
     const uint32_t* row = table + (size_t)blk * table_stride(T) + bd.t0;
     for (int k = threadIdx.x; k < bd.nt; k += BB) base[k] = tile_start[bd.t0 + k] + row[k];
     __syncthreads();
     WaveSpans& ws = wss[threadIdx.x >> 6];
     uint64_t* const key = wkey + (threadIdx.x & ~63);
     const int lane = threadIdx.x & 63;
-    const int g0 = blk * chunk, g1 = min(P, g0 + chunk);
+    const int g0 = blk * chunk, g1 = min(P, g0 + km * chunk);
     BinRec nx;
     if (g0 < g1) nx.load(geom, P, g1, radii, g0 + (threadIdx.x & ~63) + lane, true);
     for (int i0 = g0 + (threadIdx.x & ~63); i0 < g1; i0 += BB) {
@@ -811,8 +811,21 @@ static int bin_band_rows(const Cam& c)
 #ifndef LSR_SCATTER_LDS
 #define LSR_SCATTER_LDS LSR_BAND_LDS
 #endif
+#ifndef LSR_SCATTER_ROWS
+#define LSR_SCATTER_ROWS 0   // > 0: tile rows per scatter band (A/B)
+#endif
+// Count chunks per scatter block: their table rows are consecutive, so the
+// block's run per tile is the concatenation of theirs (longer runs, fewer
+// partially written lines).  From 4M Gaussians up 4 (cfg5 bin_scatter 0.900 ->
+// 0.839 ms; 2 measured 1.08), below 1 (cfg3: 2 / 4 slower, 4 with 17-row
+// bands equal; r03q A/B).  LSR_SCATTER_MERGE > 0 forces a factor (A/B).
+#ifndef LSR_SCATTER_MERGE
+#define LSR_SCATTER_MERGE 0
+#endif
+static int scatter_merge(int P) { return LSR_SCATTER_MERGE > 0 ? LSR_SCATTER_MERGE : (P >= (4 << 20) ? 4 : 1); }
 static int bin_scatter_rows(const Cam& c)
 {
+    if (LSR_SCATTER_ROWS > 0) return std::max(1, std::min(c.gy, LSR_SCATTER_ROWS));
     return std::max(1, std::min(c.gy, LSR_SCATTER_LDS / (4 * c.gx)));
 }
 
@@ -898,10 +911,11 @@ hipError_t launch_bin_scatter(const Cam& c, int P, int chunk, int B, const uint8
         (void)hipFuncSetAttribute((const void*)k_bin_scatter<512>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         (void)hipFuncSetAttribute((const void*)k_bin_scatter<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
+    const int km = scatter_merge(P), Bs = (B + km - 1) / km;
     if (B > 0 && bin_block(P) == 1024)
-        k_bin_scatter<1024><<<B * S, 1024, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, tile_start, keys);
+        k_bin_scatter<1024><<<Bs * S, 1024, lds, st>>>(c, P, chunk, km, rows, S, geom, radii, table, tile_start, keys);
     else if (B > 0)
-        k_bin_scatter<512><<<B * S, 512, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, tile_start, keys);
+        k_bin_scatter<512><<<Bs * S, 512, lds, st>>>(c, P, chunk, km, rows, S, geom, radii, table, tile_start, keys);
     return hipGetLastError();
 }
 
