@@ -1052,6 +1052,9 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m)
     return ((uint64_t)hi << 32) | lo;
 }
 
+#ifndef LSR_SORT_XBATCH
+#define LSR_SORT_XBATCH 1
+#endif
 // Partner value across lanes l <-> l ^ M without the LDS crossbar where the
 // ISA has a register path: v_permlane32_swap (M = 32), v_permlane16_swap
 // (M = 16), DPP row_ror:8 (M = 8), DPP quad_perm (M = 2, 1); ds_bpermute
@@ -1097,11 +1100,22 @@ __device__ __forceinline__ void wave_sort_xstep(uint64_t (&v)[KPL])
     // K >= 2J >= 2 KPL: the direction bit of element lane*KPL + r is the
     // lane's alone, so one flag serves all KPL elements
     const bool take_min = ((lane & M) == 0) == (((lane * KPL) & K) == 0);
+#if LSR_SORT_XBATCH
+    // every partner first, then every select: the lane exchanges (DPP /
+    // permlane) read registers the previous step wrote long before, so no
+    // hazard wait states sit between a select and the exchange that needs it
+    uint64_t o[KPL];
+#pragma unroll
+    for (int r = 0; r < KPL; r++) o[r] = xor_lane_u64<M>(v[r]);
+#pragma unroll
+    for (int r = 0; r < KPL; r++) v[r] = ((v[r] < o[r]) == take_min) ? v[r] : o[r];
+#else
 #pragma unroll
     for (int r = 0; r < KPL; r++) {
         const uint64_t o = xor_lane_u64<M>(v[r]);
         v[r] = ((v[r] < o) == take_min) ? v[r] : o;   // keep own value iff it is the wanted one
     }
+#endif
 }
 
 template <int KPL, int K, int J>
@@ -1110,13 +1124,17 @@ __device__ __forceinline__ void wave_sort_steps(uint64_t (&v)[KPL])
     if constexpr (J >= 1) {
         if constexpr (J < KPL) {
             const int lane = threadIdx.x & 63;
+            // direction of element lane*KPL + r: from r alone while K < KPL
+            // (compile time), from the lane alone once K >= KPL (r < KPL <= K
+            // never reaches bit K): one compare + one mask XOR per pair
+            const bool desc_lane = ((lane * KPL) & K) != 0;
 #pragma unroll
             for (int r = 0; r < KPL; r++) {
                 if (r & J) continue;
-                const int e = lane * KPL + r;
-                const bool asc = (e & K) == 0;
                 const uint64_t a = v[r], b = v[r | J];
-                const bool sw = asc ? (a > b) : (a < b);
+                bool sw;
+                if constexpr (K < KPL) sw = (r & K) ? (a < b) : (a > b);
+                else sw = (a > b) != desc_lane;
                 v[r] = sw ? b : a;
                 v[r | J] = sw ? a : b;
             }
