@@ -1055,10 +1055,10 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m)
 #ifndef LSR_SORT_XBATCH
 #define LSR_SORT_XBATCH 1
 #endif
-// Partner value across lanes l <-> l ^ M without the LDS crossbar where the
-// ISA has a register path: v_permlane32_swap (M = 32), v_permlane16_swap
-// (M = 16), DPP row_ror:8 (M = 8), DPP quad_perm (M = 2, 1); ds_bpermute
-// only for M = 4.
+// Partner value across lanes l <-> l ^ M without the LDS crossbar: the ISA
+// has a register path for every distance: v_permlane32_swap (M = 32),
+// v_permlane16_swap (M = 16), DPP row_ror:8 (M = 8), two DPP row rotations
+// and a select (M = 4), DPP quad_perm (M = 2, 1).
 template <int M>
 __device__ __forceinline__ uint32_t xor_lane_u32(uint32_t x)
 {
@@ -1070,11 +1070,18 @@ __device__ __forceinline__ uint32_t xor_lane_u32(uint32_t x)
         auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
         return (lane & 16) ? r[0] : r[1];
     } else if constexpr (M == 8) {
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false);   // row_ror:8
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, false);   // row_ror:8
+    } else if constexpr (M == 4) {
+        // l ^ 4 inside a row of 16.  row_ror:N makes lane l read lane (l - N) mod 16
+        // (as row_shr:N reads l - N), so row_ror:4 gives x[l - 4] (the partner
+        // where bit 2 of l is set) and row_ror:12 gives x[l + 4] (bit 2 clear).
+        const uint32_t from_below = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x124, 0xF, 0xF, false);
+        const uint32_t from_above = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x12C, 0xF, 0xF, false);
+        return (lane & 4) ? from_below : from_above;
     } else if constexpr (M == 2) {
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
     } else if constexpr (M == 1) {
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
     } else {
         return (uint32_t)__shfl_xor((int)x, M, 64);
     }
