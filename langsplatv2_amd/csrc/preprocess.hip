@@ -15,6 +15,9 @@
 #define LSR_SCALE_GRAD_EXACT 0
 #endif
 #define LSR_SCALE_GRAD_MOD(mod) (LSR_SCALE_GRAD_EXACT ? (mod) : 1.0f)
+#ifndef LSR_PRE_SH_EARLY
+#define LSR_PRE_SH_EARLY 1   // SH row loads before the visibility tests: cfg3 preprocess 77.9 -> 71.7 us, cfg5 311 -> 289 us
+#endif
 
 namespace lsr {
 
@@ -29,12 +32,22 @@ namespace lsr {
 __device__ __forceinline__ void stage_sh_rows(float* shl, const float* shs, int b0, int cnt, int lane)
 {
     const float4* src = reinterpret_cast<const float4*>(shs) + (size_t)b0 * 12;
-    for (int f = lane; f < cnt * 12; f += 64) {
-        const float4 v = src[f];
+    auto put = [&](int f, const float4 v) {
         const int row = f / 12, c4 = f - row * 12;
         float* d = shl + row * LSR_SH_ROW + c4 * 4;
         d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    };
+    if (cnt == 64) {
+        // full wave: all 12 loads in flight before the first LDS write (a
+        // rolled loop waits for each load in turn: 12 serial round trips)
+        float4 v[12];
+#pragma unroll
+        for (int k = 0; k < 12; k++) v[k] = src[lane + 64 * k];
+#pragma unroll
+        for (int k = 0; k < 12; k++) put(lane + 64 * k, v[k]);
+        return;
     }
+    for (int f = lane; f < cnt * 12; f += 64) put(f, src[f]);
 }
 
 template <bool SH16>
@@ -67,6 +80,16 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
     };
 
     const float mx = in.means3D[3 * i], my = in.means3D[3 * i + 1], mz = in.means3D[3 * i + 2];
+#if LSR_PRE_SH_EARLY
+    // the SH row's loads issued before the visibility tests (latency hidden
+    // behind the projection; culled Gaussians read their row for nothing)
+    float4 shv[SH16 ? 12 : 1];
+    if (SH16 && !in.colors_precomp) {
+        const float4* src = reinterpret_cast<const float4*>(in.shs) + (size_t)i * 12;
+#pragma unroll
+        for (int k = 0; k < 12; k++) shv[k] = src[k];
+    }
+#endif
     const float3 pv = xform43(c.view, mx, my, mz);
     if (pv.z <= 0.2f) {
         invisible();
@@ -115,12 +138,20 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
             // visible Gaussians only: direct float4 loads (staging every row
             // through LDS also reads the culled ones and measured slower here)
             float sh[48];
+#if LSR_PRE_SH_EARLY
+#pragma unroll
+            for (int k = 0; k < 12; k++) {
+                const float4 v = shv[k];
+                sh[4 * k] = v.x; sh[4 * k + 1] = v.y; sh[4 * k + 2] = v.z; sh[4 * k + 3] = v.w;
+            }
+#else
             const float4* src = reinterpret_cast<const float4*>(in.shs) + (size_t)i * 12;
 #pragma unroll
             for (int k = 0; k < 12; k++) {
                 const float4 v = src[k];
                 sh[4 * k] = v.x; sh[4 * k + 1] = v.y; sh[4 * k + 2] = v.z; sh[4 * k + 3] = v.w;
             }
+#endif
 #pragma unroll
             for (int ch = 0; ch < 3; ch++) out[ch] = sh_channel(c.sh_degree, sh, ch, dir[0], dir[1], dir[2]);
         } else {
@@ -173,23 +204,61 @@ hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, 
 // float4 when D % 4 == 0.
 // SH16: `shrow` holds this Gaussian's 48 SH values on entry and receives its
 // 48 SH gradients (written back by the caller with coalesced stores).
-template <bool SH16>
-__device__ __forceinline__ void preprocess_bwd_one(const Cam& c, const lsr_inputs& in, const uint8_t* __restrict__ geom,
-                                                   const int32_t* __restrict__ radii, const float* __restrict__ gacc,
-                                                   int VP, const lsr_bwd_out& out, int i, float* shrow)
-{
-    const int N = in.P;
-    const GeomLayout L = geom_layout(N);
-    const bool vis = radii[i] > 0;
-    const int M = in.max_coeffs;
-    const int D = in.lang_dim;
-    const float4* g4 = reinterpret_cast<const float4*>(gacc + (size_t)i * VP);
-    float4 g0 = make_float4(0.f, 0.f, 0.f, 0.f), g1 = g0, g2 = g0;
-    if (vis) {
+// One Gaussian's backward inputs.  Every row is loaded up front, whether or
+// not the Gaussian is visible (all are valid addresses): one round trip
+// instead of a chain radius -> gradient row -> means / scales / rotation, and
+// (SH16) issued before the SH rows are staged, so both are in flight at once.
+struct BwdRow {
+    int rad;
+    float4 g0, g1, g2;
+    float mx, my, mz;
+    float4 q;
+    float sc0, sc1, sc2;
+    float cov[6];
+    // COV: cov3D_precomp given (a kernel-wide choice, a template parameter so
+    // no branch merges the two cases' loaded values: such merges cost a copy
+    // each, and every copy waits for its load)
+    template <bool COV>
+    __device__ __forceinline__ void load(const lsr_inputs& in, const int32_t* __restrict__ radii,
+                                         const float* __restrict__ gacc, int VP, int i)
+    {
+        const float4* g4 = reinterpret_cast<const float4*>(gacc + (size_t)i * VP);
+        rad = radii[i];
         g0 = g4[0];
         g1 = g4[1];
         g2 = g4[2];
+        mx = in.means3D[3 * i]; my = in.means3D[3 * i + 1]; mz = in.means3D[3 * i + 2];
+        q = make_float4(1.f, 0.f, 0.f, 0.f);
+        sc0 = sc1 = sc2 = 0.f;
+        if constexpr (COV) {
+#pragma unroll
+            for (int k = 0; k < 6; k++) cov[k] = in.cov3D_precomp[6 * i + k];
+        } else {
+            q = reinterpret_cast<const float4*>(in.rotations)[i];
+            sc0 = in.scales[3 * i]; sc1 = in.scales[3 * i + 1]; sc2 = in.scales[3 * i + 2];
+        }
     }
+};
+
+template <bool SH16>
+__device__ __forceinline__ void preprocess_bwd_one(const Cam& c, const lsr_inputs& in, const uint8_t* __restrict__ geom,
+                                                   const BwdRow& row, const float* __restrict__ gacc, int VP,
+                                                   const lsr_bwd_out& out, int i, float* shrow)
+{
+    const int N = in.P;
+    const GeomLayout L = geom_layout(N);
+    const int M = in.max_coeffs;
+    const int D = in.lang_dim;
+    const float4* g4 = reinterpret_cast<const float4*>(gacc + (size_t)i * VP);
+    const float mx = row.mx, my = row.my, mz = row.mz;
+    const float4 q = row.q;
+    const float sc0 = row.sc0, sc1 = row.sc1, sc2 = row.sc2;
+    float cov[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) cov[k] = row.cov[k];
+    const bool vis = row.rad > 0;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 g0 = vis ? row.g0 : z4, g1 = vis ? row.g1 : z4, g2 = vis ? row.g2 : z4;
     const float gm2x = g0.x, gm2y = g0.y, dA = g0.z, dB = g0.w;
     const float dC = g1.x, gop = g1.y;
     const float gcol[3] = {g1.z, g1.w, g2.x};
@@ -203,7 +272,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const Cam& c, const lsr_input
     if (out.dL_dlang) {
         if ((D & 3) == 0) {
             float4* dl = reinterpret_cast<float4*>(out.dL_dlang + (size_t)i * D);
-            for (int q = 0; q < D / 4; q++) dl[q] = vis ? g4[LSR_GROW_LANG / 4 + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int w = 0; w < D / 4; w++) dl[w] = vis ? g4[LSR_GROW_LANG / 4 + w] : make_float4(0.f, 0.f, 0.f, 0.f);
         } else {
             const float* g = gacc + (size_t)i * VP + LSR_GROW_LANG;
             for (int k = 0; k < D; k++) out.dL_dlang[(size_t)i * D + k] = vis ? g[k] : 0.f;
@@ -233,17 +302,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const Cam& c, const lsr_input
     (void)L;
     const float* V = c.view;
     const float* P = c.proj;
-    const float mx = in.means3D[3 * i], my = in.means3D[3 * i + 1], mz = in.means3D[3 * i + 2];
-    float cov[6];
-    float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
-    float sc0 = 0.f, sc1 = 0.f, sc2 = 0.f;
-    if (in.cov3D_precomp) {
-        for (int k = 0; k < 6; k++) cov[k] = in.cov3D_precomp[6 * i + k];
-    } else {
-        q = reinterpret_cast<const float4*>(in.rotations)[i];
-        sc0 = in.scales[3 * i]; sc1 = in.scales[3 * i + 1]; sc2 = in.scales[3 * i + 2];
-        compute_cov3D(sc0, sc1, sc2, c.scale_modifier, q, cov);
-    }
+    if (!in.cov3D_precomp) compute_cov3D(sc0, sc1, sc2, c.scale_modifier, q, cov);
     const float3 pv = xform43(V, mx, my, mz);
     Ewa e;
     ewa_setup(V, pv, c.fx, c.fy, c.tanfovx, c.tanfovy, e);
@@ -440,15 +499,19 @@ __device__ __forceinline__ void preprocess_bwd_one(const Cam& c, const lsr_input
     }
 }
 
+template <bool COV>
 __global__ void __launch_bounds__(256) k_preprocess_bwd(Cam c, lsr_inputs in, const uint8_t* __restrict__ geom,
                                                         const int32_t* __restrict__ radii,
                                                         const float* __restrict__ gacc, int VP, lsr_bwd_out out)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= in.P) return;
-    preprocess_bwd_one<false>(c, in, geom, radii, gacc, VP, out, i, nullptr);
+    BwdRow row;
+    row.load<COV>(in, radii, gacc, VP, i);
+    preprocess_bwd_one<false>(c, in, geom, row, gacc, VP, out, i, nullptr);
 }
 
+template <bool COV>
 __global__ void __launch_bounds__(64) k_preprocess_bwd_sh16(Cam c, lsr_inputs in, const uint8_t* __restrict__ geom,
                                                             const int32_t* __restrict__ radii,
                                                             const float* __restrict__ gacc, int VP, lsr_bwd_out out)
@@ -457,11 +520,13 @@ __global__ void __launch_bounds__(64) k_preprocess_bwd_sh16(Cam c, lsr_inputs in
     const int b0 = blockIdx.x * 64, lane = threadIdx.x;
     const int cnt = min(64, in.P - b0);
     const bool sh = !in.colors_precomp;
+    BwdRow row;
+    row.load<COV>(in, radii, gacc, VP, b0 + min(lane, cnt - 1));
     if (sh) {
         stage_sh_rows(shl, in.shs, b0, cnt, lane);
         __syncthreads();
     }
-    if (lane < cnt) preprocess_bwd_one<true>(c, in, geom, radii, gacc, VP, out, b0 + lane, shl + lane * LSR_SH_ROW);
+    if (lane < cnt) preprocess_bwd_one<true>(c, in, geom, row, gacc, VP, out, b0 + lane, shl + lane * LSR_SH_ROW);
     if (sh && out.dL_dsh) {
         __syncthreads();
         float4* dst = reinterpret_cast<float4*>(out.dL_dsh) + (size_t)b0 * 12;
@@ -479,10 +544,15 @@ hipError_t launch_preprocess_bwd(const Cam& c, const lsr_inputs& in, const uint8
     if (in.P == 0) return hipSuccess;
     const bool sh16 = in.shs && in.max_coeffs == 16 && ((uintptr_t)in.shs % 16 == 0) &&
                       (!out.dL_dsh || (uintptr_t)out.dL_dsh % 16 == 0);
-    if (sh16)
-        k_preprocess_bwd_sh16<<<(in.P + 63) / 64, 64, 0, st>>>(c, in, geom, radii, grad_acc, VP, out);
+    const bool cov = in.cov3D_precomp != nullptr;
+    if (sh16 && cov)
+        k_preprocess_bwd_sh16<true><<<(in.P + 63) / 64, 64, 0, st>>>(c, in, geom, radii, grad_acc, VP, out);
+    else if (sh16)
+        k_preprocess_bwd_sh16<false><<<(in.P + 63) / 64, 64, 0, st>>>(c, in, geom, radii, grad_acc, VP, out);
+    else if (cov)
+        k_preprocess_bwd<true><<<(in.P + 255) / 256, 256, 0, st>>>(c, in, geom, radii, grad_acc, VP, out);
     else
-        k_preprocess_bwd<<<(in.P + 255) / 256, 256, 0, st>>>(c, in, geom, radii, grad_acc, VP, out);
+        k_preprocess_bwd<false><<<(in.P + 255) / 256, 256, 0, st>>>(c, in, geom, radii, grad_acc, VP, out);
     return hipGetLastError();
 }
 
