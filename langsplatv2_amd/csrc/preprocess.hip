@@ -50,7 +50,7 @@ __device__ __forceinline__ void stage_sh_rows(float* shl, const float* shs, int 
     for (int f = lane; f < cnt * 12; f += 64) put(f, src[f]);
 }
 
-template <bool SH16>
+template <bool SH16, bool COV>
 __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& in, uint8_t* __restrict__ geom,
                                                int32_t* __restrict__ radii, int i, const float* shrow)
 {
@@ -79,17 +79,47 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
         }
     };
 
+    // Every input of the Gaussian is loaded up front (LSR_PRE_SH_EARLY), before
+    // the visibility tests: one round trip instead of a chain means -> (tests)
+    // -> covariance inputs -> SH row -> opacity; culled Gaussians read their
+    // rows for nothing.  SH16 implies shs (and no colors_precomp).
     const float mx = in.means3D[3 * i], my = in.means3D[3 * i + 1], mz = in.means3D[3 * i + 2];
-#if LSR_PRE_SH_EARLY
-    // the SH row's loads issued before the visibility tests (latency hidden
-    // behind the projection; culled Gaussians read their row for nothing)
-    float4 shv[SH16 ? 12 : 1];
-    if (SH16 && !in.colors_precomp) {
-        const float4* src = reinterpret_cast<const float4*>(in.shs) + (size_t)i * 12;
+    float cov[6];
+    float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    float o = 0.f;
+    float sh[SH16 ? 48 : 1];
+    if (LSR_PRE_SH_EARLY) {
+        if constexpr (COV) {
 #pragma unroll
-        for (int k = 0; k < 12; k++) shv[k] = src[k];
+            for (int k = 0; k < 6; k++) cov[k] = in.cov3D_precomp[6 * i + k];
+        } else {
+            q = reinterpret_cast<const float4*>(in.rotations)[i];
+            s0 = in.scales[3 * i]; s1 = in.scales[3 * i + 1]; s2 = in.scales[3 * i + 2];
+        }
+        o = in.opacities[i];
+        if constexpr (SH16) {
+            const float4* src = reinterpret_cast<const float4*>(in.shs) + (size_t)i * 12;
+#pragma unroll
+            for (int k = 0; k < 12; k++) {
+                const float4 v = src[k];
+                sh[4 * k] = v.x; sh[4 * k + 1] = v.y; sh[4 * k + 2] = v.z; sh[4 * k + 3] = v.w;
+            }
+        }
+        // keep the loads here: the compiler otherwise sinks them past the
+        // visibility tests into the blocks that use them (empty asm: no code)
+        if constexpr (SH16) {
+#pragma unroll
+            for (int k = 0; k < 48; k++) asm volatile("" : "+v"(sh[k]));
+        }
+        asm volatile("" : "+v"(o));
+        if constexpr (COV) {
+#pragma unroll
+            for (int k = 0; k < 6; k++) asm volatile("" : "+v"(cov[k]));
+        } else {
+            asm volatile("" : "+v"(q.x), "+v"(q.y), "+v"(q.z), "+v"(q.w), "+v"(s0), "+v"(s1), "+v"(s2));
+        }
     }
-#endif
     const float3 pv = xform43(c.view, mx, my, mz);
     if (pv.z <= 0.2f) {
         invisible();
@@ -99,14 +129,16 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
     const float pw = 1.0f / (ph.w + 0.0000001f);
     const float ppx = ph.x * pw, ppy = ph.y * pw;
 
-    float cov[6];
-    if (in.cov3D_precomp) {
+    if (!LSR_PRE_SH_EARLY) {
+        if constexpr (COV) {
 #pragma unroll
-        for (int k = 0; k < 6; k++) cov[k] = in.cov3D_precomp[6 * i + k];
-    } else {
-        const float4 q = reinterpret_cast<const float4*>(in.rotations)[i];
-        compute_cov3D(in.scales[3 * i], in.scales[3 * i + 1], in.scales[3 * i + 2], c.scale_modifier, q, cov);
+            for (int k = 0; k < 6; k++) cov[k] = in.cov3D_precomp[6 * i + k];
+        } else {
+            q = reinterpret_cast<const float4*>(in.rotations)[i];
+            s0 = in.scales[3 * i]; s1 = in.scales[3 * i + 1]; s2 = in.scales[3 * i + 2];
+        }
     }
+    if constexpr (!COV) compute_cov3D(s0, s1, s2, c.scale_modifier, q, cov);
     Ewa e;
     ewa_setup(c.view, pv, c.fx, c.fy, c.tanfovx, c.tanfovy, e);
     float a, b, cc;
@@ -134,29 +166,21 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
         float dir[3], dor[3];
         sh_dir(mx, my, mz, c.campos, dir, dor);
         float out[3];
-        if (SH16) {
-            // visible Gaussians only: direct float4 loads (staging every row
-            // through LDS also reads the culled ones and measured slower here)
-            float sh[48];
-#if LSR_PRE_SH_EARLY
+        if constexpr (SH16) {
+            // direct float4 loads (staging every row through LDS measured slower)
+            if (!LSR_PRE_SH_EARLY) {
+                const float4* src = reinterpret_cast<const float4*>(in.shs) + (size_t)i * 12;
 #pragma unroll
-            for (int k = 0; k < 12; k++) {
-                const float4 v = shv[k];
-                sh[4 * k] = v.x; sh[4 * k + 1] = v.y; sh[4 * k + 2] = v.z; sh[4 * k + 3] = v.w;
+                for (int k = 0; k < 12; k++) {
+                    const float4 v = src[k];
+                    sh[4 * k] = v.x; sh[4 * k + 1] = v.y; sh[4 * k + 2] = v.z; sh[4 * k + 3] = v.w;
+                }
             }
-#else
-            const float4* src = reinterpret_cast<const float4*>(in.shs) + (size_t)i * 12;
-#pragma unroll
-            for (int k = 0; k < 12; k++) {
-                const float4 v = src[k];
-                sh[4 * k] = v.x; sh[4 * k + 1] = v.y; sh[4 * k + 2] = v.z; sh[4 * k + 3] = v.w;
-            }
-#endif
 #pragma unroll
             for (int ch = 0; ch < 3; ch++) out[ch] = sh_channel(c.sh_degree, sh, ch, dir[0], dir[1], dir[2]);
         } else {
-            const float* sh = in.shs + (size_t)i * in.max_coeffs * 3;
-            for (int ch = 0; ch < 3; ch++) out[ch] = sh_channel(c.sh_degree, sh, ch, dir[0], dir[1], dir[2]);
+            const float* shg = in.shs + (size_t)i * in.max_coeffs * 3;
+            for (int ch = 0; ch < 3; ch++) out[ch] = sh_channel(c.sh_degree, shg, ch, dir[0], dir[1], dir[2]);
         }
         uint32_t m = 0;
 #pragma unroll
@@ -168,7 +192,7 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
     } else {
         clampm[i] = 0;
     }
-    const float o = in.opacities[i];
+    if (!LSR_PRE_SH_EARLY) o = in.opacities[i];
     depth[i] = pv.z;
     radii[i] = r;
     splatA[i] = make_float4(px, py, cc * det_inv, -b * det_inv);
@@ -177,23 +201,25 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
     tiles[i] = (uint32_t)area;
 }
 
-template <bool SH16>
+template <bool SH16, bool COV>
 __global__ void __launch_bounds__(256) k_preprocess(Cam c, lsr_inputs in, uint8_t* __restrict__ geom,
                                                     int32_t* __restrict__ radii)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= in.P) return;
-    preprocess_one<SH16>(c, in, geom, radii, i, nullptr);
+    preprocess_one<SH16, COV>(c, in, geom, radii, i, nullptr);
 }
 
 hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, int32_t* radii, hipStream_t st)
 {
     if (in.P == 0) return hipSuccess;
     const bool sh16 = in.shs && in.max_coeffs == 16 && ((uintptr_t)in.shs % 16 == 0);
-    if (sh16)
-        k_preprocess<true><<<(in.P + 255) / 256, 256, 0, st>>>(c, in, geom, radii);
-    else
-        k_preprocess<false><<<(in.P + 255) / 256, 256, 0, st>>>(c, in, geom, radii);
+    const bool cov = in.cov3D_precomp != nullptr;
+    const dim3 g((in.P + 255) / 256);
+    if (sh16 && cov) k_preprocess<true, true><<<g, 256, 0, st>>>(c, in, geom, radii);
+    else if (sh16) k_preprocess<true, false><<<g, 256, 0, st>>>(c, in, geom, radii);
+    else if (cov) k_preprocess<false, true><<<g, 256, 0, st>>>(c, in, geom, radii);
+    else k_preprocess<false, false><<<g, 256, 0, st>>>(c, in, geom, radii);
     return hipGetLastError();
 }
 
