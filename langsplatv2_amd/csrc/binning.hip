@@ -792,126 +792,6 @@ __global__ void __launch_bounds__(BB) k_bin_scatter(Cam c, int P, int chunk, int
     }
 }
 
-// LDS-staged scatter (LSR_SCATTER_STAGE): the block's keys are collected in
-// LDS grouped by tile (tile t's slots start at the exclusive scan of the
-// block's own per-tile counts, table row b+km minus row b), then written out
-// in one burst at the end of the block, each tile's run at tile_start[t] +
-// table[b][t].  The direct scatter writes each 8-B key the moment it is
-// ranked, so every key line is written back many times half-filled (PMC at
-// cfg3: 204.7 MB written for 37.9 MB of keys); here the blocks that share a
-// tile's lines flush close together in time, while those lines are still in
-// their XCD's L2.  A block whose keys exceed `cap` uses the direct stores.
-template <int BB>
-__global__ void __launch_bounds__(BB) k_bin_scatter_lds(Cam c, int P, int chunk, int km, int B, int rows, int S,
-                                                        int cap, const uint8_t* __restrict__ geom,
-                                                        const int32_t* __restrict__ radii,
-                                                        const uint32_t* __restrict__ table,
-                                                        const uint32_t* __restrict__ tile_start,
-                                                        uint64_t* __restrict__ keys)
-{
-    extern __shared__ uint32_t dyn[];
-    __shared__ WaveSpans wss[BB / 64];
-    __shared__ uint64_t wkey[BB];
-    __shared__ uint64_t sh[BB / 64];
-    __shared__ uint32_t s_total;
-    const int T = c.gx * c.gy;
-    const int o = xcd_remap(blockIdx.x, gridDim.x);
-    const int blk = (o / S) * km;
-    const Band bd(c, rows, o - (o / S) * S);
-    const int nt = bd.nt;
-    uint32_t* const gbase = dyn;        // global start of this block's run, per band tile
-    uint32_t* const lcur = dyn + nt;    // LDS slot cursor; after the walk, the run's end
-    uint64_t* const kbuf = reinterpret_cast<uint64_t*>(dyn + 2 * ((nt + 1) & ~1));
-    uint16_t* const tidx = reinterpret_cast<uint16_t*>(kbuf + cap);   // band tile of each staged key
-    const size_t Tp = (size_t)table_stride(T);
-    const uint32_t* row = table + (size_t)blk * Tp + bd.t0;
-    const bool lastb = blk + km >= B;
-    const uint32_t* rown = table + (size_t)(lastb ? blk : blk + km) * Tp + bd.t0;
-    // per-tile counts of this block and their exclusive scan (8 tiles a thread)
-    constexpr int TPT = 8;
-    uint64_t carry = 0;
-    for (int base = 0; base < nt; base += BB * TPT) {
-        const int k0 = base + threadIdx.x * TPT;
-        uint32_t cnt[TPT];
-        uint64_t sum = 0;
-#pragma unroll
-        for (int j = 0; j < TPT; j++) {
-            const int k = k0 + j;
-            uint32_t v = 0;
-            if (k < nt) {
-                const uint32_t r0 = row[k];
-                const uint32_t ts = tile_start[bd.t0 + k];
-                const uint32_t r1 = lastb ? tile_start[bd.t0 + k + 1] - ts : rown[k];
-                v = r1 - r0;
-                gbase[k] = ts + r0;
-            }
-            cnt[j] = v;
-            sum += v;
-        }
-        uint64_t tot;
-        uint64_t run = carry + block_excl_scan_u64_n<BB>(sum, sh, tot);
-#pragma unroll
-        for (int j = 0; j < TPT; j++) {
-            if (k0 + j < nt) lcur[k0 + j] = (uint32_t)run;
-            run += cnt[j];
-        }
-        carry += tot;
-    }
-    if (threadIdx.x == 0) s_total = (uint32_t)carry;
-    __syncthreads();
-    const uint32_t total = s_total;
-    const bool staged = total <= (uint32_t)cap;
-    if (!staged) {   // direct stores: the cursors count ranks inside each tile's run
-        for (int k = threadIdx.x; k < nt; k += BB) lcur[k] = 0u;
-        __syncthreads();
-    }
-    WaveSpans& ws = wss[threadIdx.x >> 6];
-    uint64_t* const key = wkey + (threadIdx.x & ~63);
-    const int lane = threadIdx.x & 63;
-    const int g0 = blk * chunk, g1 = min(P, g0 + km * chunk);
-    BinRec nx;
-    if (g0 < g1) nx.load(geom, P, g1, radii, g0 + (threadIdx.x & ~63) + lane, true);
-    for (int i0 = g0 + (threadIdx.x & ~63); i0 < g1; i0 += BB) {
-        const int i = i0 + lane;
-        const BinRec cur = nx;
-        nx.load(geom, P, g1, radii, i0 + BB + lane, true);
-        key[lane] = ((uint64_t)__float_as_uint(cur.depth) << 32) | (uint32_t)i;
-        const int R = stage_gaussian(ws, c, bd, cur);
-        for (int r0 = 0; r0 < R; r0 += 64) {
-            const int K = wave_spans_round(ws, r0, R, bd.ty0);
-            const int q = (K + 63) >> 6;
-            int k = lane * q;
-            const int kend = min(K, k + q);
-            if (k < kend) {
-                SpanWalk sw(ws, k);
-                for (;;) {
-                    const int t = sw.y * c.gx + sw.x;
-                    const uint32_t sl = atomicAdd(&lcur[t], 1u);
-                    const uint64_t kv = key[sw.o];
-                    if (staged) {
-                        kbuf[sl] = kv;
-                        tidx[sl] = (uint16_t)t;
-                    } else {
-                        keys[gbase[t] + sl] = kv;
-                    }
-                    if (++k >= kend) break;
-                    sw.next(ws);
-                }
-            }
-            wave_lds_fence();
-        }
-    }
-    if (!staged) return;
-    __syncthreads();
-    // flush: entry e of tile t = tidx[e] sits at e - (start of t's slots), the
-    // start being the previous tile's end cursor
-    for (uint32_t e = threadIdx.x; e < total; e += BB) {
-        const int t = tidx[e];
-        const uint32_t st0 = t ? lcur[t - 1] : 0u;
-        keys[gbase[t] + (e - st0)] = kbuf[e];
-    }
-}
-
 // Tile rows per band: the largest band whose histogram fits LSR_BAND_LDS.
 // At most LSR_BAND_ROWS rows: at cfg3 (68 tile rows) two bands of 34 halve
 // the chunk count for the same ~512 blocks — a smaller B x T table and longer
@@ -1021,36 +901,9 @@ hipError_t launch_tile_start_apply(int T, int B, const uint32_t* tile_cnt, const
     return hipGetLastError();
 }
 
-#ifndef LSR_SCATTER_STAGE
-#define LSR_SCATTER_STAGE 0       // LDS-staged scatter (k_bin_scatter_lds) below 4M Gaussians
-#endif
-#ifndef LSR_SCATTER_STAGE_ROWS
-#define LSR_SCATTER_STAGE_ROWS 34
-#endif
-#ifndef LSR_SCATTER_STAGE_BB
-#define LSR_SCATTER_STAGE_BB 512
-#endif
 hipError_t launch_bin_scatter(const Cam& c, int P, int chunk, int B, const uint8_t* geom, const int32_t* radii,
                               const uint32_t* table, const uint32_t* tile_start, uint64_t* keys, hipStream_t st)
 {
-    if (LSR_SCATTER_STAGE && P < (4 << 20) && B > 0 && c.gx * LSR_SCATTER_STAGE_ROWS < 65536) {
-        constexpr int BBS = LSR_SCATTER_STAGE_BB;
-        const int rows = std::max(1, std::min(c.gy, LSR_SCATTER_STAGE_ROWS));
-        const int S = (c.gy + rows - 1) / rows;
-        const int nt = rows * c.gx;
-        const size_t fixed = (size_t)2 * ((nt + 1) & ~1) * 4;
-        const size_t stat = (size_t)(BBS / 64) * sizeof(WaveSpans) + BBS * 8 + (BBS / 64) * 8 + 64;
-        const size_t budget = 160 * 1024 - stat - 1024;
-        if (fixed + 10 * 1024 <= budget) {
-            const int cap = (int)((budget - fixed) / 10) & ~3;
-            const size_t lds = fixed + (size_t)cap * 10;
-            (void)hipFuncSetAttribute((const void*)k_bin_scatter_lds<BBS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)lds);
-            k_bin_scatter_lds<BBS><<<B * S, BBS, lds, st>>>(c, P, chunk, 1, B, rows, S, cap, geom, radii, table,
-                                                           tile_start, keys);
-            return hipGetLastError();
-        }
-    }
     const int rows = bin_scatter_rows(c);
     const int S = (c.gy + rows - 1) / rows;
     const size_t lds = (size_t)rows * c.gx * 4;
