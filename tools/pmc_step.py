@@ -48,8 +48,11 @@ r = GaussianRasterizer(bench.settings(cam, dev, 3, True))
 dc = torch.randn(3, cfg["H"], cfg["W"], device=dev)
 dl = torch.randn(D, cfg["H"], cfg["W"], device=dev)
 for _ in range(steps):
-    c, l, _ = r(means3D=g["means3D"], means2D=g["means2D"], opacities=g["opacities"], shs=g["shs"],
-                language_feature_precomp=g["language_feature_precomp"], scales=g["scales"], rotations=g["rotations"])
-    torch.autograd.backward([c, l], [dc, dl])
+    with torch.set_grad_enabled(cfg["backward"]):   # cfg5 is forward-only
+        c, l, _ = r(means3D=g["means3D"], means2D=g["means2D"], opacities=g["opacities"], shs=g["shs"],
+                    language_feature_precomp=g["language_feature_precomp"], scales=g["scales"],
+                    rotations=g["rotations"])
+    if cfg["backward"]:
+        torch.autograd.backward([c, l], [dc, dl])
 torch.cuda.synchronize()
 print("ok")
