@@ -132,53 +132,13 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 #endif
 template <int NL>
 constexpr bool fwd_sfeat() { return LSR_FWD_SFEAT > 0 && NL >= LSR_FWD_SFEAT; }
-#ifndef LSR_FWD_GEO4
-#define LSR_FWD_GEO4 1      // fwd: a candidate pair's geometry as 16-B lines (ds_read_b128) instead of field arrays
-#endif
 template <int F4, bool SF>
 struct WaveStageP {
-#if LSR_FWD_GEO4
-    // pair e = candidates (2e, 2e+1): {X, Y}, {CA, CB}, {CC, OP}, {CUT, -} lines,
-    // component j & 1 of each field; one broadcast ds_read_b128 reads two
-    // fields of both candidates (4 LDS cycles, where a ds_read2_b64 of two
-    // field arrays costs 8)
-    float4 G[32][4];
-#else
     f32x2 X[32], Y[32], CA[32], CB[32], CC[32], OP[32], CUT[32];
-#endif
     float4 F[SF ? 1 : 64 * F4];
     uint32_t gid[SF ? 64 : 1];
     int pos[64];
 };
-// The staged geometry of candidate pair e.
-struct PairGeo {
-    f32x2 X, Y, CA, CB, CC, OP, CUT;
-};
-template <class ST>
-__device__ __forceinline__ PairGeo pair_geo(const ST& st, int e)
-{
-    PairGeo g;
-#if LSR_FWD_GEO4
-    const float4 q0 = st.G[e][0], q1 = st.G[e][1], q2 = st.G[e][2];
-    const float2 q3 = *reinterpret_cast<const float2*>(&st.G[e][3]);
-    g.X = f32x2{q0.x, q0.y};
-    g.Y = f32x2{q0.z, q0.w};
-    g.CA = f32x2{q1.x, q1.y};
-    g.CB = f32x2{q1.z, q1.w};
-    g.CC = f32x2{q2.x, q2.y};
-    g.OP = f32x2{q2.z, q2.w};
-    g.CUT = f32x2{q3.x, q3.y};
-#else
-    g.X = st.X[e];
-    g.Y = st.Y[e];
-    g.CA = st.CA[e];
-    g.CB = st.CB[e];
-    g.CC = st.CC[e];
-    g.OP = st.OP[e];
-    g.CUT = st.CUT[e];
-#endif
-    return g;
-}
 
 // Feature row (rgb + dense language, zero-padded) of a wave-uniform Gaussian:
 // the address is uniform, so these are scalar loads through the constant
@@ -217,16 +177,6 @@ __device__ __forceinline__ int stage_candidates_p_rec(WaveStageP<F4, fwd_sfeat<N
     const int cnt = __popcll(m);
     if (ok) {
         const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-#if LSR_FWD_GEO4
-        float* g = reinterpret_cast<float*>(&st.G[r >> 1][0]) + (r & 1);
-        g[0] = A.x;
-        g[2] = A.y;
-        g[4] = A.z;
-        g[6] = A.w;
-        g[8] = B.x;
-        g[10] = B.y;
-        g[12] = B.z;
-#else
         float* base = reinterpret_cast<float*>(&st) + (r & 1);
         const int e = (r >> 1) * 2;
         base[0 * 64 + e] = A.x;
@@ -236,7 +186,6 @@ __device__ __forceinline__ int stage_candidates_p_rec(WaveStageP<F4, fwd_sfeat<N
         base[4 * 64 + e] = B.x;
         base[5 * 64 + e] = B.y;
         base[6 * 64 + e] = B.z;
-#endif
         st.pos[r] = pos;
         if constexpr (fwd_sfeat<NL>())
             st.gid[r] = gid;
@@ -366,9 +315,8 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 float fr0[F4 * 4], fr1[F4 * 4];
                 feature_row_uniform<NL, F4>(fr0, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j0]));
                 feature_row_uniform<NL, F4>(fr1, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j1]));
-                const PairGeo pg = pair_geo(st, e);
-                const f32x2 sX = pg.X, sY = pg.Y, sCA = pg.CA, sCB = pg.CB, sCC = pg.CC;
-                const f32x2 OP = pg.OP;
+                const f32x2 sX = st.X[e], sY = st.Y[e], sCA = st.CA[e], sCB = st.CB[e], sCC = st.CC[e];
+                const f32x2 OP = st.OP[e];
                 const f32x2 dx = sX - f32x2{pfx, pfx}, dy = sY - f32x2{pfy, pfy};
                 const f32x2 P = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f},
                                                           __builtin_elementwise_fma(sCA * dx, dx, (sCC * dy) * dy),
@@ -406,9 +354,8 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 feature_row_uniform<NL, F4>(fr0, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j0]));
                 feature_row_uniform<NL, F4>(fr1, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j1]));
             }
-            const PairGeo pg = pair_geo(st, e);
-            const f32x2 sX = pg.X, sY = pg.Y, sCA = pg.CA, sCB = pg.CB, sCC = pg.CC;
-            const f32x2 CUT = pg.CUT, OP = pg.OP;
+            const f32x2 sX = st.X[e], sY = st.Y[e], sCA = st.CA[e], sCB = st.CB[e], sCC = st.CC[e];
+            const f32x2 CUT = st.CUT[e], OP = st.OP[e];
             const f32x2 dx = sX - f32x2{pfx, pfx}, dy = sY - f32x2{pfy, pfy};
             const f32x2 P = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f},
                                                       __builtin_elementwise_fma(sCA * dx, dx, (sCC * dy) * dy),
@@ -1186,13 +1133,9 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             const int qx = pm.bx + (q & 7), qy = pm.by + (q >> 3);
             return (qx < c.W && qy < c.H) ? (uint32_t)(qy * c.W + qx) * 4u : 0x80000000u;
         };
-#ifdef LSR_PROBE_NOPRO   // timing probe only (wrong results): no prologue dL/dout loads
-        auto ld = [&](__amdgpu_buffer_rsrc_t r, uint32_t off) { return __uint_as_float(off) * 1e-30f; };
-#else
         auto ld = [&](__amdgpu_buffer_rsrc_t r, uint32_t off) {
             return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
         };
-#endif
         uint32_t pa[4];
 #pragma unroll
         for (int pb = 0; pb < 4; pb++) pa[pb] = poff(pb * 16 + li);
