@@ -335,7 +335,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                     Tout = (term & (T > 0.f)) ? T : Tout;
                     const float aT = ok ? ev * T : 0.f;
 #pragma unroll
-                    for (int k = 0; k < F4 * 4; k++) acc[k] = fmaf(h ? fr1[k] : fr0[k], aT, acc[k]);
+                    for (int k = 0; k < C; k++) acc[k] = fmaf(h ? fr1[k] : fr0[k], aT, acc[k]);
                     T = term ? 0.f : test_T;
                     lastj = ok ? (h ? j1 : j0) : lastj;
                 }
@@ -377,16 +377,17 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 const float aT = ok0 ? al0 * T : 0.f;
                 if constexpr (SF) {
 #pragma unroll
-                    for (int k = 0; k < F4 * 4; k++) acc[k] = fmaf(fr0[k], aT, acc[k]);
+                    for (int k = 0; k < C; k++) acc[k] = fmaf(fr0[k], aT, acc[k]);
                 } else
                 {
 #pragma unroll
                     for (int f = 0; f < F4; f++) {
                         const float4 v = st.F[j0 * F4 + f];
-                        acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
-                        acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
-                        acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
-                        acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
+                        // the row's zero padding past channel C is not accumulated
+                        if (4 * f + 0 < C) acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
+                        if (4 * f + 1 < C) acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
+                        if (4 * f + 2 < C) acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
+                        if (4 * f + 3 < C) acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
                     }
                 }
                 T = ok0 ? test_T : T;
@@ -400,16 +401,17 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 const float aT = ok1 ? al1 * T : 0.f;
                 if constexpr (SF) {
 #pragma unroll
-                    for (int k = 0; k < F4 * 4; k++) acc[k] = fmaf(fr1[k], aT, acc[k]);
+                    for (int k = 0; k < C; k++) acc[k] = fmaf(fr1[k], aT, acc[k]);
                 } else
                 {
 #pragma unroll
                     for (int f = 0; f < F4; f++) {
                         const float4 v = st.F[j1 * F4 + f];
-                        acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
-                        acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
-                        acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
-                        acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
+                        // the row's zero padding past channel C is not accumulated
+                        if (4 * f + 0 < C) acc[4 * f + 0] = fmaf(v.x, aT, acc[4 * f + 0]);
+                        if (4 * f + 1 < C) acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
+                        if (4 * f + 2 < C) acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
+                        if (4 * f + 3 < C) acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
                     }
                 }
                 T = ok1 ? test_T : T;
