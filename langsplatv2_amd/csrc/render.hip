@@ -28,6 +28,9 @@
 #ifndef LSR_BWD_SPLAT_PF
 #define LSR_BWD_SPLAT_PF 1  // bwd: chunk records loaded one chunk ahead (ids two ahead), D <= 32
 #endif
+#ifndef LSR_FWD_MF16
+#define LSR_FWD_MF16 0      // A/B: D = 16 forward on the MFMA-accumulated kernel
+#endif
 #ifndef LSR_FWD_T0_SF
 #define LSR_FWD_T0_SF 1     // fwd, scalar feature rows (D >= LSR_FWD_SFEAT): the T0 blend loop (see k_render_fwd)
 #endif
@@ -134,7 +137,7 @@ template <int NL>
 constexpr bool fwd_sfeat() { return LSR_FWD_SFEAT > 0 && NL >= LSR_FWD_SFEAT; }
 template <int F4, bool SF>
 struct WaveStageP {
-    f32x2 X[32], Y[32], CA[32], CB[32], CC[32], OP[32], CUT[32];
+    f32x2 X[32], Y[32], CA[32], CB[32], CC[32], OP[32];
     float4 F[SF ? 1 : 64 * F4];
     uint32_t gid[SF ? 64 : 1];
     int pos[64];
@@ -185,7 +188,6 @@ __device__ __forceinline__ int stage_candidates_p_rec(WaveStageP<F4, fwd_sfeat<N
         base[3 * 64 + e] = A.w;
         base[4 * 64 + e] = B.x;
         base[5 * 64 + e] = B.y;
-        base[6 * 64 + e] = B.z;
         st.pos[r] = pos;
         if constexpr (fwd_sfeat<NL>())
             st.gid[r] = gid;
@@ -355,14 +357,16 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 feature_row_uniform<NL, F4>(fr1, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j1]));
             }
             const f32x2 sX = st.X[e], sY = st.Y[e], sCA = st.CA[e], sCB = st.CB[e], sCC = st.CC[e];
-            const f32x2 CUT = st.CUT[e], OP = st.OP[e];
+            const f32x2 OP = st.OP[e];
             const f32x2 dx = sX - f32x2{pfx, pfx}, dy = sY - f32x2{pfy, pfy};
             const f32x2 P = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f},
                                                       __builtin_elementwise_fma(sCA * dx, dx, (sCC * dy) * dy),
                                                       -((sCB * dx) * dy));
             const float p0 = P.x, p1 = P.y;
-            bool ok0 = !done && !(p0 > 0.0f || p0 < CUT.x);
-            bool ok1 = two && !done && !(p1 > 0.0f || p1 < CUT.y);
+            // no exponent-cut test: below the cut alpha < e^-0.02 / 255, so the
+            // 1/255 test below rejects the pair anyway (exact, as in the T0 loop)
+            bool ok0 = !done && !(p0 > 0.0f);
+            bool ok1 = two && !done && !(p1 > 0.0f);
             const f32x2 EX = expf_det2(P);   // both exponents packed (bitwise = expf_det)
             const float al0 = fminf(0.99f, OP.x * EX.x);
             const float al1 = fminf(0.99f, OP.y * EX.y);
@@ -388,6 +392,9 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                         if (4 * f + 1 < C) acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
                         if (4 * f + 2 < C) acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
                         if (4 * f + 3 < C) acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
+                        // keep the 16-B read (ds_read_b128: 4 LDS cycles; the b96 the
+                        // compiler would narrow it to costs 8)
+                        else asm volatile("" ::"v"(v.w));
                     }
                 }
                 T = ok0 ? test_T : T;
@@ -412,6 +419,9 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                         if (4 * f + 1 < C) acc[4 * f + 1] = fmaf(v.y, aT, acc[4 * f + 1]);
                         if (4 * f + 2 < C) acc[4 * f + 2] = fmaf(v.z, aT, acc[4 * f + 2]);
                         if (4 * f + 3 < C) acc[4 * f + 3] = fmaf(v.w, aT, acc[4 * f + 3]);
+                        // keep the 16-B read (ds_read_b128: 4 LDS cycles; the b96 the
+                        // compiler would narrow it to costs 8)
+                        else asm volatile("" ::"v"(v.w));
                     }
                 }
                 T = ok1 ? test_T : T;
@@ -793,7 +803,11 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
         case 0: LSR_FWD_LAUNCH(k_render_fwd, 0); break;
         case 4: LSR_FWD_LAUNCH(k_render_fwd, 4); break;
         case 8: LSR_FWD_LAUNCH(k_render_fwd, 8); break;
+#if LSR_FWD_MF16
+        case 16: LSR_FWD_LAUNCH(k_render_fwd_mf, 16); break;
+#else
         case 16: LSR_FWD_LAUNCH(k_render_fwd, 16); break;
+#endif
         // measured (cfg3 geometry): D = 32 legacy 0.78 vs MFMA 0.81 ms; D = 64 legacy 1.38 vs MFMA 1.13 ms
         case 32: LSR_FWD_LAUNCH(k_render_fwd, 32); break;
         case 64: LSR_FWD_LAUNCH(k_render_fwd_mf, 64); break;
