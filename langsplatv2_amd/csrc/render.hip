@@ -28,6 +28,15 @@
 #ifndef LSR_BWD_SPLAT_PF
 #define LSR_BWD_SPLAT_PF 1  // bwd: chunk records loaded one chunk ahead (ids two ahead), D <= 32
 #endif
+#ifndef LSR_FWD_ML
+#define LSR_FWD_ML 0        // A/B: D = 16 forward with the language channels on MFMA (measured +2.6 % cfg3, +6.7 % cfg2)
+#endif
+#ifndef LSR_FWD_ML32
+#define LSR_FWD_ML32 1      // D = 32 forward: language channels on MFMA (cfg5 render_fwd 1.650 -> 1.266 ms)
+#endif
+#ifndef LSR_FWD_ML64
+#define LSR_FWD_ML64 0      // D = 64 forward: the ML form instead of k_render_fwd_mf (A/B)
+#endif
 #ifndef LSR_FWD_MF16
 #define LSR_FWD_MF16 0      // A/B: D = 16 forward on the MFMA-accumulated kernel
 #endif
@@ -123,6 +132,7 @@ struct WaveTile {
 };
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // Forward staging with the candidates' geometry pair-interleaved: entry
 // j >> 1, component j & 1, so the blend loop reads candidates (2i, 2i+1) of
@@ -229,13 +239,26 @@ __device__ __forceinline__ void zero_backward_accumulators(const RenderArgs& a)
 // ZERO: this launch also clears the backward's accumulators (a.zero set);
 // a separate instantiation, so a forward without a pending backward runs the
 // unchanged kernel (the clearing loop alone moved cfg5's D = 32 render by +2 %)
-template <int NL, bool ZERO = false>
+// ML (D = 16, LSR_FWD_ML): the language channels accumulate on the matrix
+// cores instead of the VALU.  Per 4 staged candidates the blend (alpha, the
+// serial transmittance / termination recurrence, the RGB sums) runs per pixel
+// lane as below; the 4 x 64 weights aT are transposed in registers (two
+// permlane swaps per pair of rows: lane group <-> candidate) into the B
+// operand of v_mfma_f32_16x16x4_f32, whose A operand is the candidates' 16
+// language values (the staged feature rows).  The MFMA is bitwise a fmaf
+// chain over its 4 K terms in order (tools/micro/mfma_order.hip) and a
+// skipped pair has aT = 0, so the outputs are bit-identical to the per-lane
+// sequential blend; the VALU no longer issues the 2 x 16 language FMAs per
+// candidate pair, which run on the otherwise idle matrix pipe.
+template <int NL, bool ZERO = false, bool ML = false>
 __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
 {
     if constexpr (ZERO) zero_backward_accumulators(a);
     constexpr int C = 3 + NL;
     constexpr int F4 = (C + 3) / 4;  // float4 per feature row
     constexpr bool SF = fwd_sfeat<NL>();
+    static_assert(!ML || NL == 16 || NL == 32 || NL == 64, "ML: whole 16-channel language blocks");
+    constexpr int MLB = ML ? NL / 16 : 1;   // ML: 16-channel output blocks
     __shared__ WaveStageP<F4, SF> st;
 
     const Cam& c = a.cam;
@@ -249,13 +272,18 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
 
     // T0 (scalar feature rows): a finished pixel carries T = 0 and its final T
     // in Tout, instead of a per-pixel `done` mask (see the T0 loop below)
-    constexpr bool T0 = SF && LSR_FWD_T0_SF;
+    constexpr bool T0 = SF && LSR_FWD_T0_SF && !ML;
     float T = (T0 && !inside) ? 0.f : 1.0f;
     float Tout = 0.f;
     bool done = !inside;
     float acc[F4 * 4];
 #pragma unroll
     for (int k = 0; k < F4 * 4; k++) acc[k] = 0.f;
+    f32x4 mlacc[MLB][4];   // ML: lane (li, lg) holds language channels 16 nb + 4 lg + r of block pixel 16 pb + li
+#pragma unroll
+    for (int nb = 0; nb < MLB; nb++)
+#pragma unroll
+        for (int pb = 0; pb < 4; pb++) mlacc[nb][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
     uint32_t last = 0;
 
     uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
@@ -299,7 +327,97 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
         // independent (ILP); T carries from the first to the second exactly
         // as in the sequential per-pixel order.
         int lastj = -1;   // LASTJ: staged index of the chunk's last contributor
-        if constexpr (T0) {
+        if constexpr (ML) {
+            const int lg = lane >> 4, li = lane & 15;
+            const float* const Fs = reinterpret_cast<const float*>(st.F);
+            for (int q0 = 0; q0 < n; q0 += 4) {
+                if (wave_ballot(!done) == 0) break;
+                // A operand: language channel 16 nb + li of candidate q0 + lg
+                // (0 past the chunk) -- from the staged rows, or (SF) gathered
+                float av[MLB];
+#pragma unroll
+                for (int nb = 0; nb < MLB; nb++) {
+                    float fa;
+                    if constexpr (SF)
+                        fa = a.lang[(size_t)st.gid[min(q0 + lg, n - 1)] * NL + 16 * nb + li];
+                    else
+                        fa = Fs[(q0 + lg) * (F4 * 4) + 3 + 16 * nb + li];
+                    av[nb] = q0 + lg < n ? fa : 0.f;
+                }
+                float al[4];
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int j0 = q0 + 2 * h, e = j0 >> 1;
+                    const f32x2 sX = st.X[e], sY = st.Y[e], sCA = st.CA[e], sCB = st.CB[e], sCC = st.CC[e];
+                    const f32x2 OP = st.OP[e];
+                    const f32x2 dx = sX - f32x2{pfx, pfx}, dy = sY - f32x2{pfy, pfy};
+                    const f32x2 P = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f},
+                                                              __builtin_elementwise_fma(sCA * dx, dx, (sCC * dy) * dy),
+                                                              -((sCB * dx) * dy));
+                    const f32x2 EX = expf_det2(P);
+                    const float a0 = fminf(0.99f, OP.x * EX.x), a1 = fminf(0.99f, OP.y * EX.y);
+                    // no exponent-cut test: below the cut the 1/255 test rejects the pair
+                    al[2 * h] = ((j0 < n) & !(P.x > 0.0f) & !(a0 < 1.0f / 255.0f)) ? a0 : 0.f;
+                    al[2 * h + 1] = ((j0 + 1 < n) & !(P.y > 0.0f) & !(a1 < 1.0f / 255.0f)) ? a1 : 0.f;
+                }
+                // the serial recurrence (the legacy loop's, one candidate at a time)
+                float s4[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const float alk = al[k];
+                    const float test_T = T * (1.0f - alk);
+                    const bool ok0 = (alk != 0.f) & !done;
+                    const bool term = ok0 & (test_T < 0.0001f);
+                    done = done | term;
+                    const bool ok = ok0 & !term;
+                    const float aT = ok ? alk * T : 0.f;
+                    // rgb; past the chunk a staged row's (aT = 0 there)
+                    const int kk = min(q0 + k, n - 1);
+                    float f0, f1, f2;
+                    if constexpr (SF) {   // uniform id: scalar loads
+                        const lsr_cfptr rgb = (lsr_cfptr)a.rgb;
+                        const uint32_t g = __builtin_amdgcn_readfirstlane(st.gid[kk]);
+                        f0 = rgb[3 * g];
+                        f1 = rgb[3 * g + 1];
+                        f2 = rgb[3 * g + 2];
+                    } else {
+                        const float4 f = st.F[kk * F4];
+                        f0 = f.x;
+                        f1 = f.y;
+                        f2 = f.z;
+                    }
+                    acc[0] = fmaf(f0, aT, acc[0]);
+                    acc[1] = fmaf(f1, aT, acc[1]);
+                    acc[2] = fmaf(f2, aT, acc[2]);
+                    T = ok ? test_T : T;
+                    lastj = ok ? q0 + k : lastj;
+                    s4[k] = aT;
+                }
+                // transpose (lane group, candidate): lane (li, lg) then holds
+                // candidate lg's aT at block pixel 16 pb + li in s4[pb]
+                {
+                    auto sw32 = [](float& x, float& y) {
+                        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+                        x = __uint_as_float(r[0]);
+                        y = __uint_as_float(r[1]);
+                    };
+                    auto sw16 = [](float& x, float& y) {
+                        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+                        x = __uint_as_float(r[0]);
+                        y = __uint_as_float(r[1]);
+                    };
+                    sw32(s4[0], s4[2]);
+                    sw32(s4[1], s4[3]);
+                    sw16(s4[0], s4[1]);
+                    sw16(s4[2], s4[3]);
+                }
+#pragma unroll
+                for (int pb = 0; pb < 4; pb++)
+#pragma unroll
+                    for (int nb = 0; nb < MLB; nb++)
+                        mlacc[nb][pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[nb], s4[pb], mlacc[nb][pb], 0, 0, 0);
+            }
+        } else if constexpr (T0) {
             // T0 form (r03): a finished pixel carries T = 0 (its final T kept in
             // Tout), so every later candidate is an exact no-op for it (alpha * 0
             // = 0, and the termination test stays true) without a per-pixel
@@ -439,9 +557,27 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
         a.n_contrib[pix] = last;
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) a.out_color[ch * HW + pix] = fmaf(T, c.bg[ch], acc[ch]);
+        if constexpr (!ML) {
 #pragma unroll
-        for (int k = 0; k < NL; k++)
-            if (k < D) a.out_lang[k * HW + pix] = acc[3 + k];
+            for (int k = 0; k < NL; k++)
+                if (k < D) a.out_lang[k * HW + pix] = acc[3 + k];
+        }
+    }
+    if constexpr (ML) {
+        const size_t HW = (size_t)c.H * c.W;
+        const int lg = lane >> 4, li = lane & 15;
+#pragma unroll
+        for (int pb = 0; pb < 4; pb++) {
+            const int q = pb * 16 + li;
+            const int qx = pm.bx + (q & 7), qy = pm.by + (q >> 3);
+            if (qx < c.W && qy < c.H) {
+                const size_t pix = (size_t)qy * c.W + qx;
+#pragma unroll
+                for (int nb = 0; nb < MLB; nb++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) a.out_lang[(size_t)(16 * nb + 4 * lg + r) * HW + pix] = mlacc[nb][pb][r];
+            }
+        }
     }
 }
 
@@ -806,11 +942,26 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
 #if LSR_FWD_MF16
         case 16: LSR_FWD_LAUNCH(k_render_fwd_mf, 16); break;
 #else
-        case 16: LSR_FWD_LAUNCH(k_render_fwd, 16); break;
+        case 16:
+            if (LSR_FWD_ML && a.D == 16) {
+                if (a.zero) k_render_fwd<16, true, true><<<4 * T, 64, 0, st>>>(a);
+                else k_render_fwd<16, false, true><<<4 * T, 64, 0, st>>>(a);
+            } else LSR_FWD_LAUNCH(k_render_fwd, 16);
+            break;
 #endif
         // measured (cfg3 geometry): D = 32 legacy 0.78 vs MFMA 0.81 ms; D = 64 legacy 1.38 vs MFMA 1.13 ms
-        case 32: LSR_FWD_LAUNCH(k_render_fwd, 32); break;
-        case 64: LSR_FWD_LAUNCH(k_render_fwd_mf, 64); break;
+        case 32:
+            if (LSR_FWD_ML32 && a.D == 32) {
+                if (a.zero) k_render_fwd<32, true, true><<<4 * T, 64, 0, st>>>(a);
+                else k_render_fwd<32, false, true><<<4 * T, 64, 0, st>>>(a);
+            } else LSR_FWD_LAUNCH(k_render_fwd, 32);
+            break;
+        case 64:
+            if (LSR_FWD_ML64 && a.D == 64) {
+                if (a.zero) k_render_fwd<64, true, true><<<4 * T, 64, 0, st>>>(a);
+                else k_render_fwd<64, false, true><<<4 * T, 64, 0, st>>>(a);
+            } else LSR_FWD_LAUNCH(k_render_fwd_mf, 64);
+            break;
 #undef LSR_FWD_LAUNCH
         default: return hipErrorInvalidValue;
     }
@@ -826,8 +977,6 @@ int grad_row_width(int D)
     const int nv = LSR_GROW_LANG + (nl > 0 ? nl : 0);
     return (nv + 31) / 32 * 32;
 }
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------ factorised backward ----
 // Every per-(pixel, instance) gradient term is a product of a per-pair
