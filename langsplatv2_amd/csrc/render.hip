@@ -34,12 +34,6 @@
 #ifndef LSR_FWD_ML32
 #define LSR_FWD_ML32 1      // D = 32 forward: language channels on MFMA (cfg5 render_fwd 1.650 -> 1.266 ms)
 #endif
-#ifndef LSR_FWD_ML64
-#define LSR_FWD_ML64 0      // D = 64 forward: the ML form instead of k_render_fwd_mf (A/B)
-#endif
-#ifndef LSR_FWD_MF16
-#define LSR_FWD_MF16 0      // A/B: D = 16 forward on the MFMA-accumulated kernel
-#endif
 #ifndef LSR_FWD_T0_SF
 #define LSR_FWD_T0_SF 1     // fwd, scalar feature rows (D >= LSR_FWD_SFEAT): the T0 blend loop (see k_render_fwd)
 #endif
@@ -150,7 +144,8 @@ struct WaveStageP {
     f32x2 X[32], Y[32], CA[32], CB[32], CC[32], OP[32];
     float4 F[SF ? 1 : 64 * F4];
     uint32_t gid[SF ? 64 : 1];
-    int pos[64];
+    uint8_t src[64];   // the staging lane (position = chunk base + src + 1): 192 B less LDS than
+                       // the positions themselves, so 6 instead of 5 waves/SIMD at D = 16
 };
 
 // Feature row (rgb + dense language, zero-padded) of a wave-uniform Gaussian:
@@ -198,7 +193,7 @@ __device__ __forceinline__ int stage_candidates_p_rec(WaveStageP<F4, fwd_sfeat<N
         base[3 * 64 + e] = A.w;
         base[4 * 64 + e] = B.x;
         base[5 * 64 + e] = B.y;
-        st.pos[r] = pos;
+        st.src[r] = (uint8_t)(threadIdx.x & 63);
         if constexpr (fwd_sfeat<NL>())
             st.gid[r] = gid;
         else
@@ -250,7 +245,9 @@ __device__ __forceinline__ void zero_backward_accumulators(const RenderArgs& a)
 // skipped pair has aT = 0, so the outputs are bit-identical to the per-lane
 // sequential blend; the VALU no longer issues the 2 x 16 language FMAs per
 // candidate pair, which run on the otherwise idle matrix pipe.
-template <int NL, bool ZERO = false, bool ML = false>
+// MLM (with ML): D below the language set's width NL (masked channels);
+// otherwise D == NL is a compile-time constant (fewer registers).
+template <int NL, bool ZERO = false, bool ML = false, bool MLM = false>
 __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
 {
     if constexpr (ZERO) zero_backward_accumulators(a);
@@ -268,7 +265,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
     const bool inside = pm.px < c.W && pm.py < c.H;
     const float pfx = (float)pm.px, pfy = (float)pm.py;
     const uint32_t rs = a.tile_start[wt.tile], re = a.tile_start[wt.tile + 1];
-    const int D = a.D;
+    const int D = (ML && !MLM) ? NL : a.D;
 
     // T0 (scalar feature rows): a finished pixel carries T = 0 and its final T
     // in Tout, instead of a per-pixel `done` mask (see the T0 loop below)
@@ -337,12 +334,14 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 float av[MLB];
 #pragma unroll
                 for (int nb = 0; nb < MLB; nb++) {
+                    // MLM: channels past D (a language set wider than D) read 0
+                    const int ch = 16 * nb + li;
                     float fa;
                     if constexpr (SF)
-                        fa = a.lang[(size_t)st.gid[min(q0 + lg, n - 1)] * NL + 16 * nb + li];
+                        fa = a.lang[(size_t)st.gid[min(q0 + lg, n - 1)] * D + (MLM ? min(ch, D - 1) : ch)];
                     else
-                        fa = Fs[(q0 + lg) * (F4 * 4) + 3 + 16 * nb + li];
-                    av[nb] = q0 + lg < n ? fa : 0.f;
+                        fa = Fs[(q0 + lg) * (F4 * 4) + 3 + ch];
+                    av[nb] = ((q0 + lg < n) & (!MLM || ch < D)) ? fa : 0.f;
                 }
                 float al[4];
 #pragma unroll
@@ -546,7 +545,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 lastj = ok1 ? j1 : lastj;
             }
         }
-        if (lastj >= 0) last = (uint32_t)st.pos[lastj];
+        if (lastj >= 0) last = (uint32_t)(base - rs) + 1u + st.src[lastj];
         wave_lds_fence();
     }
     if (inside) {
@@ -575,7 +574,8 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
 #pragma unroll
                 for (int nb = 0; nb < MLB; nb++)
 #pragma unroll
-                    for (int r = 0; r < 4; r++) a.out_lang[(size_t)(16 * nb + 4 * lg + r) * HW + pix] = mlacc[nb][pb][r];
+                    for (int r = 0; r < 4; r++)
+                        if (16 * nb + 4 * lg + r < D) a.out_lang[(size_t)(16 * nb + 4 * lg + r) * HW + pix] = mlacc[nb][pb][r];
             }
         }
     }
@@ -909,11 +909,6 @@ int lang_set_for(int D)
     return -1;
 }
 
-// (declarations carry the definitions' launch bounds: without them the
-// kernels would default to 1024-thread workgroups and a 128-register cap)
-template <int NL, bool ZERO = false>
-__global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_fwd_mf(RenderArgs a);
-
 hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
 {
     const int T = a.cam.gx * a.cam.gy;
@@ -939,28 +934,33 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
         case 0: LSR_FWD_LAUNCH(k_render_fwd, 0); break;
         case 4: LSR_FWD_LAUNCH(k_render_fwd, 4); break;
         case 8: LSR_FWD_LAUNCH(k_render_fwd, 8); break;
-#if LSR_FWD_MF16
-        case 16: LSR_FWD_LAUNCH(k_render_fwd_mf, 16); break;
-#else
         case 16:
             if (LSR_FWD_ML && a.D == 16) {
                 if (a.zero) k_render_fwd<16, true, true><<<4 * T, 64, 0, st>>>(a);
                 else k_render_fwd<16, false, true><<<4 * T, 64, 0, st>>>(a);
             } else LSR_FWD_LAUNCH(k_render_fwd, 16);
             break;
-#endif
         // measured (cfg3 geometry): D = 32 legacy 0.78 vs MFMA 0.81 ms; D = 64 legacy 1.38 vs MFMA 1.13 ms
         case 32:
             if (LSR_FWD_ML32 && a.D == 32) {
                 if (a.zero) k_render_fwd<32, true, true><<<4 * T, 64, 0, st>>>(a);
                 else k_render_fwd<32, false, true><<<4 * T, 64, 0, st>>>(a);
+            } else if (LSR_FWD_ML32) {
+                if (a.zero) k_render_fwd<32, true, true, true><<<4 * T, 64, 0, st>>>(a);
+                else k_render_fwd<32, false, true, true><<<4 * T, 64, 0, st>>>(a);
             } else LSR_FWD_LAUNCH(k_render_fwd, 32);
             break;
         case 64:
-            if (LSR_FWD_ML64 && a.D == 64) {
+            // D = 64: always the ML form (measured 0.996 -> 0.688 ms against the
+            // earlier 16-candidate-group MFMA kernel at cfg3 geometry; the
+            // VALU-only blend is slower still)
+            if (a.D == 64) {
                 if (a.zero) k_render_fwd<64, true, true><<<4 * T, 64, 0, st>>>(a);
                 else k_render_fwd<64, false, true><<<4 * T, 64, 0, st>>>(a);
-            } else LSR_FWD_LAUNCH(k_render_fwd_mf, 64);
+            } else {
+                if (a.zero) k_render_fwd<64, true, true, true><<<4 * T, 64, 0, st>>>(a);
+                else k_render_fwd<64, false, true, true><<<4 * T, 64, 0, st>>>(a);
+            }
             break;
 #undef LSR_FWD_LAUNCH
         default: return hipErrorInvalidValue;
@@ -1727,189 +1727,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
         BWD_STAMP(7);
     }
     BWD_STAMP_FLUSH();
-}
-
-
-// ------------------------------------------------ MFMA-accumulated forward ----
-// The blend's channel accumulation out[c][p] = sum_k f[k][c] * aT[k][p] (k in
-// front-to-back order) is a GEMM with the tile's instances as K.  On gfx950
-// v_mfma_f32_16x16x4_f32 is bitwise a fmaf chain over k = 0..3
-// (tools/micro/mfma_order.hip: 131072/131072), and non-contributing pairs carry
-// aT = 0 (fmaf(f, 0, acc) == acc), so accumulating on the matrix cores in
-// instance order is bit-identical to the sequential per-pixel blend.  Per group
-// of 16 candidates: phase 1 evaluates alpha independently per candidate (the
-// deterministic exp), phase 2 runs the serial transmittance / termination
-// recurrence and writes aT, phase 3 accumulates on MFMA.
-struct WaveStageF {
-    float4 A[80];
-    float4 B[80];         // .w = 1-based tile-list position (int bits)
-    uint32_t gid[80];
-};
-
-__device__ __forceinline__ int stage_candidates_f(WaveStageF& st, int carry, bool valid, uint32_t gid, int pos,
-                                                  int bx, int by, const float4* __restrict__ splatA,
-                                                  const float4* __restrict__ splatB)
-{
-    float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
-    if (valid) {
-        A = splatA[gid];
-        B = splatB[gid];
-    }
-    const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by) &&
-                    block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, bx, by);
-    const uint64_t m = wave_ballot(ok);
-    if (ok) {
-        const int r = carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        st.A[r] = A;
-        st.B[r] = make_float4(B.x, B.y, B.z, __int_as_float(pos));
-        st.gid[r] = gid;
-    }
-    wave_lds_fence();
-    return __popcll(m);
-}
-
-#define LSR_FWD_STRIDE 80   // aT tile row stride: conflict-free B-fragment reads
-
-template <int NL, bool ZERO>
-__global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_fwd_mf(RenderArgs a)
-{
-    constexpr int C = 3 + NL;
-    constexpr int F4 = (C + 3) / 4;
-    constexpr int RS = F4 * 4;                 // feature row stride (floats)
-    constexpr int NBC = (C + 15) / 16;         // 16-channel output blocks
-    constexpr int FS = LSR_FWD_STRIDE;
-    __shared__ WaveStageF st;
-    __shared__ float sAT[16 * FS];
-    __shared__ float sT[64];
-    if constexpr (ZERO) zero_backward_accumulators(a);
-
-    const Cam& c = a.cam;
-    const WaveTile wt(a);
-    const int lane = threadIdx.x;
-    const int lg = lane >> 4, li = lane & 15;
-    const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
-    const bool inside = pm.px < c.W && pm.py < c.H;
-    const float pfx = (float)pm.px, pfy = (float)pm.py;
-    const uint32_t rs = a.tile_start[wt.tile], re = a.tile_start[wt.tile + 1];
-    const int D = a.D;
-
-    for (int e = lane; e < 80; e += 64) {
-        st.A[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-        st.B[e] = make_float4(0.f, 0.f, 0.f, __int_as_float(0));
-        st.gid[e] = 0u;
-    }
-
-    float T = 1.0f;
-    uint32_t last = 0;
-    bool done = !inside;
-    f32x4 acc[NBC][4];
-#pragma unroll
-    for (int nb = 0; nb < NBC; nb++)
-#pragma unroll
-        for (int pb = 0; pb < 4; pb++) acc[nb][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    int carry = 0;
-    uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
-    for (uint32_t base = rs; base < re; base += 64) {
-        if (wave_ballot(!done) == 0) break;
-        const uint32_t idx = base + lane;
-        const bool valid = idx < re;
-        const uint32_t gid = next_gid;
-        next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;
-        const int n = carry + stage_candidates_f(st, carry, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, a.splatA,
-                                                 a.splatB);
-        const int nfull = (base + 64 >= re) ? n : (n & ~15);
-        bool all_done = false;
-        for (int g0 = 0; g0 < nfull; g0 += 16) {
-            if (wave_ballot(!done) == 0) {
-                all_done = true;
-                break;
-            }
-            const int kn = min(16, nfull - g0);
-            // A fragments (feature nb*16+li of candidate g0+4t+lg), gathered now,
-            // consumed in phase 3; rows >= kn carry aT = 0
-            float av[4][NBC];
-#pragma unroll
-            for (int t = 0; t < 4; t++) {
-                const uint32_t gk = st.gid[g0 + 4 * t + lg];
-#pragma unroll
-                for (int nb = 0; nb < NBC; nb++) av[t][nb] = feature_at<NL>(a, gk, nb * 16 + li);
-            }
-            // phase 1: alpha of the 16 candidates (0 = skipped), independent
-#pragma unroll 4
-            for (int k = 0; k < 16; k++) {
-                const float4 A = st.A[g0 + k];
-                const float4 B = st.B[g0 + k];
-                const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
-                const bool cut = (k < kn) & !(power > 0.0f) & !(power < B.z);
-                const float alpha = fminf(0.99f, B.y * expf_det(power));
-                sAT[k * FS + lane] = (cut & !(alpha < 1.0f / 255.0f)) ? alpha : 0.f;
-            }
-            // phase 2: serial transmittance and early termination per pixel
-#pragma unroll 4
-            for (int k = 0; k < 16; k++) {
-                const float al = sAT[k * FS + lane];
-                const int posk = __float_as_int(st.B[g0 + k].w);
-                bool ok = (al != 0.f) & !done;
-                const float test_T = T * (1.0f - al);
-                const bool term = ok & (test_T < 0.0001f);
-                done = done | term;
-                ok = ok & !term;
-                sAT[k * FS + lane] = ok ? al * T : 0.f;
-                T = ok ? test_T : T;
-                last = ok ? (uint32_t)posk : last;
-            }
-            wave_lds_fence();
-            // phase 3: out[c][p] += F[k][c] * aT[k][p] on MFMA, k in order
-#pragma unroll
-            for (int t = 0; t < 4; t++) {
-#pragma unroll
-                for (int pb = 0; pb < 4; pb++) {
-                    const float bv = sAT[(4 * t + lg) * FS + pb * 16 + li];
-#pragma unroll
-                    for (int nb = 0; nb < NBC; nb++)
-                        acc[nb][pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t][nb], bv, acc[nb][pb], 0, 0, 0);
-                }
-            }
-            wave_lds_fence();
-        }
-        if (all_done) break;
-        // carry the partial group to the front (source >= 16 > destination:
-        // no overlap; nothing to move when nfull == 0)
-        carry = n - nfull;
-        if (nfull > 0 && lane < carry) {
-            st.A[lane] = st.A[nfull + lane];
-            st.B[lane] = st.B[nfull + lane];
-            st.gid[lane] = st.gid[nfull + lane];
-        }
-        wave_lds_fence();
-    }
-    const size_t HW = (size_t)c.H * c.W;
-    if (inside) {
-        const size_t pix = (size_t)pm.py * c.W + pm.px;
-        a.final_T[pix] = T;
-        a.n_contrib[pix] = last;
-    }
-    sT[lane] = T;
-    wave_lds_fence();
-    // lane (lg, li) holds channel nb*16 + 4*lg + r of block pixel pb*16 + li
-#pragma unroll
-    for (int pb = 0; pb < 4; pb++) {
-        const int q = pb * 16 + li;
-        const int qx = pm.bx + (q & 7), qy = pm.by + (q >> 3);
-        if (qx < c.W && qy < c.H) {
-            const size_t pix = (size_t)qy * c.W + qx;
-            const float Tq = sT[q];
-#pragma unroll
-            for (int nb = 0; nb < NBC; nb++)
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int ch = nb * 16 + 4 * lg + r;
-                    if (ch < 3) a.out_color[ch * HW + pix] = fmaf(Tq, c.bg[ch], acc[nb][pb][r]);
-                    else if (ch < 3 + D) a.out_lang[(size_t)(ch - 3) * HW + pix] = acc[nb][pb][r];
-                }
-        }
-    }
 }
 
 

@@ -20,6 +20,10 @@ CASES = {
     "lang64_feature_mode": dict(N=4000, W=128, H=112, sh_degree=3, lang_dim=64, seed=7),
     "yaw_sh3_lang32": dict(N=8000, W=192, H=128, sh_degree=3, lang_dim=32, yaw=15.0, seed=8),
     "quick192": dict(N=5000, W=128, H=96, sh_degree=None, quick_k=4, seed=9),
+    # language widths below their compiled set (32, 64): the forward's MFMA
+    # language blocks mask the channels past D
+    "sh2_lang24_ragged": dict(N=6000, W=136, H=100, sh_degree=2, lang_dim=24, bg=(0.2, 0.1, 0.7), seed=10),
+    "lang48": dict(N=4000, W=112, H=96, sh_degree=3, lang_dim=48, seed=11),
 }
 
 
