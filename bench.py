@@ -109,14 +109,15 @@ def algorithmic_bytes(g, rs, D, S):
                    staged_bwd=staged_b, mean_n_contrib=float(nc.float().mean().item()))
 
 
-def pmc_traffic(stage):
+def pmc_traffic(stage, prefix="r"):
     """Measured HBM bytes per launch of `stage`'s kernel from the newest committed
-    profiles/r*_pmc_traffic.json (tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE
-    rocprofv3 passes over tools/pmc_step.py = this workload, gfx950-corrected)."""
+    profiles/<prefix>*_pmc_traffic.json (tools/pmc_traffic.py: separate FETCH_SIZE / WRITE_SIZE
+    rocprofv3 passes over tools/pmc_step.py = this workload, gfx950-corrected); the
+    cfg5 line reads the cfg5_r* files (pmc_step.py with LSR_CFG=5)."""
     import glob
     import re
     # natural order: r01v10 after r01v9
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")),
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", prefix + "*_pmc_traffic.json")),
                    key=lambda f: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(f))])
     if not files:
         return None, None
@@ -339,6 +340,7 @@ def main_forward_replicas(args, world, rank, dev) -> int:
         dom_gbps = bytes_[dom] / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
         step_ms = elapsed / args.steps * 1e3
         fwd_keys = ("preprocess", "bin_count", "scan_tile_counts", "bin_scatter", "tile_sort", "render_fwd")
+        traffic, traffic_src = pmc_traffic(dom, prefix="cfg5_r")
         out = {
             "metric": "frames/s fwd @ 5M Gaussians 4K 3+32ch (BASELINE configs[4], replicas)",
             "value": round(world * args.steps / elapsed, 3),
@@ -361,9 +363,13 @@ def main_forward_replicas(args, world, rank, dev) -> int:
             "ranks_seen": dist.get_world_size() if world > 1 else 1,
             "roofline": {
                 "bound": "hbm", "kernel": dom, "achieved": round(dom_gbps, 1), "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(dom_gbps / HBM_PEAK_GBPS, 4), "traffic": None,
+                "unit": "GB/s", "frac": round(dom_gbps / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": int(bytes_[dom]),
                 "bytes_formula": "SURVEY.md §8d (bench.py:algorithmic_bytes)",
+                "note": "frac can exceed 1 here: §8d charges every instance its 4C-byte feature row "
+                        "(M*4C, most of the bytes at C = 35), which the kernel re-reads from L2; "
+                        "the measured HBM traffic is `traffic`, and the kernel is VALU/MFMA-issue bound (DESIGN.md §3)",
                 "ms_per_launch": round(dom_ms, 4), "launches_timed": dom_calls,
             },
             "stages_ms": {k: round(v, 4) for k, v in per_stage.items()},
