@@ -1553,20 +1553,30 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 C0 = fmaf(aa, d.x, C0);
                 C1 = fmaf(aa, d.y, C1);
                 C2 = fmaf(aa, d.z, C2);
+                // lx is a lane constant per column parity (lxe even t, lxo odd t)
+                // and ly a constant per t, so the six moments follow from the
+                // column-parity sums of u, ly u and ly^2 u (3 VALU per t instead
+                // of 11 per t pair; combined with lxe / lxo after the loop)
+                const float ly = (float)(t >> 1) - 3.5f;
                 if ((t & 1) == 0) {
-                    ue = au;
+                    M0 += au;
+                    M2 = fmaf(ly, au, M2);
+                    M5 = fmaf(ly * ly, au, M5);
                 } else {
-                    const float ly = (float)(t >> 1) - 3.5f;
-                    const float R0 = ue + au;
-                    const float R1 = fmaf(ue, lxe, au * lxo);
-                    const float R2 = fmaf(ue, lxe2, au * lxo2);
-                    M0 += R0;
-                    M1 += R1;
-                    M2 = fmaf(ly, R0, M2);
-                    M3 += R2;
-                    M4 = fmaf(ly, R1, M4);
-                    M5 = fmaf(ly * ly, R0, M5);
+                    M1 += au;
+                    M3 = fmaf(ly, au, M3);
+                    M4 = fmaf(ly * ly, au, M4);
                 }
+            }
+            {
+                // (M0, M2, M5) = even-column sums of (u, ly u, ly^2 u); (M1, M3, M4) the odd columns'
+                const float se = M0, so = M1, ye = M2, yo = M3, qe = M5, qo = M4;
+                M0 = se + so;
+                M1 = fmaf(lxe, se, lxo * so);
+                M2 = ye + yo;
+                M3 = fmaf(lxe2, se, lxo2 * so);
+                M4 = fmaf(lxe, ye, lxo * yo);
+                M5 = qe + qo;
             }
             // The nine partial sums over the four lane groups, reduced two at a
             // time: a permlane swap exchanges half of one value for half of
