@@ -34,6 +34,9 @@
 #ifndef LSR_FWD_ML32
 #define LSR_FWD_ML32 1      // D = 32 forward: language channels on MFMA (cfg5 render_fwd 1.650 -> 1.266 ms)
 #endif
+#ifndef LSR_BWD_LO_RREG
+#define LSR_BWD_LO_RREG 1   // language-only bwd: atomics straight from the MFMA accumulators (no LDS row tile)
+#endif
 #ifndef LSR_FWD_T0_SF
 #define LSR_FWD_T0_SF 1     // fwd, scalar feature rows (D >= LSR_FWD_SFEAT): the T0 blend loop (see k_render_fwd)
 #endif
@@ -1190,7 +1193,9 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     // RREG (direct dL/dlang): the language lines' atomics take their values
     // straight from the MFMA accumulators, lane (li, lg) adding candidate
     // 4 lg + q's channel li (the C layout), so those rows skip LDS
-    constexpr bool RREG = LD;
+    // (LO, not SP: every line is a language line, so all of them come
+    // straight from the accumulators and the LDS row tile is not used)
+    constexpr bool RREG = LD || (LO && !SP && LSR_BWD_LO_RREG);
     // MFMA channel blocks cover the language channels only; RGB (3) and the
     // six geometry moments are summed on the VALU (see phase 3)
     constexpr int NBC = (NL + 15) / 16;
@@ -1675,7 +1680,9 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 for (int h = 0; h < GRL; h++)
 #pragma unroll
                     for (int q = 0; q < 4; q++) {
-                        if (RREG && h > 0)
+                        if (RREG && LO)
+                            vq[h][q] = ch[h][q];
+                        else if (RREG && h > 0)
                             vq[h][q] = ch[h - 1][q];
                         else
                             vq[h][q] = sGr[slot_of(q) * GRS + 16 * h + li];
