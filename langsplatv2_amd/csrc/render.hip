@@ -37,6 +37,9 @@
 #ifndef LSR_BWD_LO_RREG
 #define LSR_BWD_LO_RREG 1   // language-only bwd: atomics straight from the MFMA accumulators (no LDS row tile)
 #endif
+#ifndef LSR_FWD_SF_RGB
+#define LSR_FWD_SF_RGB 1    // scalar-feature forward: RGB staged in LDS with the candidate (ML blend reads a line)
+#endif
 #ifndef LSR_FWD_T0_SF
 #define LSR_FWD_T0_SF 1     // fwd, scalar feature rows (D >= LSR_FWD_SFEAT): the T0 blend loop (see k_render_fwd)
 #endif
@@ -147,6 +150,7 @@ struct WaveStageP {
     f32x2 X[32], Y[32], CA[32], CB[32], CC[32], OP[32];
     float4 F[SF ? 1 : 64 * F4];
     uint32_t gid[SF ? 64 : 1];
+    float4 R[SF ? 64 : 1];   // SF: the candidates' RGB (read by the ML blend as one broadcast line)
     uint8_t src[64];   // the staging lane (position = chunk base + src + 1): 192 B less LDS than
                        // the positions themselves, so 6 instead of 5 waves/SIMD at D = 16
 };
@@ -197,9 +201,10 @@ __device__ __forceinline__ int stage_candidates_p_rec(WaveStageP<F4, fwd_sfeat<N
         base[4 * 64 + e] = B.x;
         base[5 * 64 + e] = B.y;
         st.src[r] = (uint8_t)(threadIdx.x & 63);
-        if constexpr (fwd_sfeat<NL>())
+        if constexpr (fwd_sfeat<NL>()) {
             st.gid[r] = gid;
-        else
+            if (LSR_FWD_SF_RGB) st.R[r] = make_float4(rgb[3 * (size_t)gid], rgb[3 * (size_t)gid + 1], rgb[3 * (size_t)gid + 2], 0.f);
+        } else
             stage_features<NL, F4>(&st.F[r * F4], rgb, lang, D, gid);
     }
     wave_lds_fence();
@@ -376,7 +381,12 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                     // rgb; past the chunk a staged row's (aT = 0 there)
                     const int kk = min(q0 + k, n - 1);
                     float f0, f1, f2;
-                    if constexpr (SF) {   // uniform id: scalar loads
+                    if constexpr (SF && LSR_FWD_SF_RGB) {   // the staged line
+                        const float4 f = st.R[kk];
+                        f0 = f.x;
+                        f1 = f.y;
+                        f2 = f.z;
+                    } else if constexpr (SF) {   // uniform id: scalar loads
                         const lsr_cfptr rgb = (lsr_cfptr)a.rgb;
                         const uint32_t g = __builtin_amdgcn_readfirstlane(st.gid[kk]);
                         f0 = rgb[3 * g];
