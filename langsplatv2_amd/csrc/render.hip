@@ -28,20 +28,8 @@
 #ifndef LSR_BWD_SPLAT_PF
 #define LSR_BWD_SPLAT_PF 1  // bwd: chunk records loaded one chunk ahead (ids two ahead), D <= 32
 #endif
-#ifndef LSR_FWD_ML
-#define LSR_FWD_ML 0        // A/B: D = 16 forward with the language channels on MFMA (measured +2.6 % cfg3, +6.7 % cfg2)
-#endif
-#ifndef LSR_FWD_ML32
-#define LSR_FWD_ML32 1      // D = 32 forward: language channels on MFMA (cfg5 render_fwd 1.650 -> 1.266 ms)
-#endif
 #ifndef LSR_BWD_LO_RREG
 #define LSR_BWD_LO_RREG 1   // language-only bwd: atomics straight from the MFMA accumulators (no LDS row tile)
-#endif
-#ifndef LSR_FWD_SF_RGB
-#define LSR_FWD_SF_RGB 1    // scalar-feature forward: RGB staged in LDS with the candidate (ML blend reads a line)
-#endif
-#ifndef LSR_FWD_T0_SF
-#define LSR_FWD_T0_SF 1     // fwd, scalar feature rows (D >= LSR_FWD_SFEAT): the T0 blend loop (see k_render_fwd)
 #endif
 #ifndef LSR_MF_WAVES
 #define LSR_MF_WAVES 2      // MFMA render kernels: min waves per SIMD (caps VGPRs at 256)
@@ -139,9 +127,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // each field with one ds_read_b64 and evaluates both exponents with packed
 // f32 instructions (bitwise identical to the scalar ones).
 #ifndef LSR_FWD_SFEAT
-#define LSR_FWD_SFEAT 32    // fwd: from this many language channels up, feature rows are read with scalar
-                            // loads at blend time instead of staged in LDS (cfg5 D = 32: 2.46 -> 2.02 ms;
-                            // at D = 16 the SGPR pressure makes it slower: 0.36 -> 0.61 ms)
+#define LSR_FWD_SFEAT 32    // fwd: from this many language channels up, feature rows are not staged in LDS:
+                            // the ML form gathers the candidates' language slices as MFMA operands and
+                            // stages only their RGB
 #endif
 template <int NL>
 constexpr bool fwd_sfeat() { return LSR_FWD_SFEAT > 0 && NL >= LSR_FWD_SFEAT; }
@@ -154,31 +142,6 @@ struct WaveStageP {
     uint8_t src[64];   // the staging lane (position = chunk base + src + 1): 192 B less LDS than
                        // the positions themselves, so 6 instead of 5 waves/SIMD at D = 16
 };
-
-// Feature row (rgb + dense language, zero-padded) of a wave-uniform Gaussian:
-// the address is uniform, so these are scalar loads through the constant
-// cache, off the LDS path the blend is otherwise bound by (every lane reads
-// the same row).
-typedef const float __attribute__((address_space(4)))* lsr_cfptr;   // constant address space: scalar loads
-template <int NL, int F4>
-__device__ __forceinline__ void feature_row_uniform(float (&row)[F4 * 4], const float* __restrict__ rgb_g,
-                                                    const float* __restrict__ lang_g, int D, uint32_t gid)
-{
-    const lsr_cfptr rgb = (lsr_cfptr)rgb_g;
-    const lsr_cfptr lang = (lsr_cfptr)lang_g;
-    row[0] = rgb[3 * gid];
-    row[1] = rgb[3 * gid + 1];
-    row[2] = rgb[3 * gid + 2];
-    if (NL > 0 && D == NL) {
-#pragma unroll
-        for (int k = 0; k < NL; k++) row[3 + k] = lang[(size_t)gid * NL + k];
-    } else {
-#pragma unroll
-        for (int k = 0; k < NL; k++) row[3 + k] = (k < D) ? lang[(size_t)gid * D + k] : 0.f;
-    }
-#pragma unroll
-    for (int k = 3 + NL; k < F4 * 4; k++) row[k] = 0.f;
-}
 
 template <int NL, int F4>
 __device__ __forceinline__ int stage_candidates_p_rec(WaveStageP<F4, fwd_sfeat<NL>()>& st, bool valid, uint32_t gid,
@@ -203,7 +166,7 @@ __device__ __forceinline__ int stage_candidates_p_rec(WaveStageP<F4, fwd_sfeat<N
         st.src[r] = (uint8_t)(threadIdx.x & 63);
         if constexpr (fwd_sfeat<NL>()) {
             st.gid[r] = gid;
-            if (LSR_FWD_SF_RGB) st.R[r] = make_float4(rgb[3 * (size_t)gid], rgb[3 * (size_t)gid + 1], rgb[3 * (size_t)gid + 2], 0.f);
+            st.R[r] = make_float4(rgb[3 * (size_t)gid], rgb[3 * (size_t)gid + 1], rgb[3 * (size_t)gid + 2], 0.f);
         } else
             stage_features<NL, F4>(&st.F[r * F4], rgb, lang, D, gid);
     }
@@ -242,17 +205,19 @@ __device__ __forceinline__ void zero_backward_accumulators(const RenderArgs& a)
 // ZERO: this launch also clears the backward's accumulators (a.zero set);
 // a separate instantiation, so a forward without a pending backward runs the
 // unchanged kernel (the clearing loop alone moved cfg5's D = 32 render by +2 %)
-// ML (D = 16, LSR_FWD_ML): the language channels accumulate on the matrix
+// ML (D > 16): the language channels accumulate on the matrix
 // cores instead of the VALU.  Per 4 staged candidates the blend (alpha, the
 // serial transmittance / termination recurrence, the RGB sums) runs per pixel
 // lane as below; the 4 x 64 weights aT are transposed in registers (two
 // permlane swaps per pair of rows: lane group <-> candidate) into the B
-// operand of v_mfma_f32_16x16x4_f32, whose A operand is the candidates' 16
-// language values (the staged feature rows).  The MFMA is bitwise a fmaf
-// chain over its 4 K terms in order (tools/micro/mfma_order.hip) and a
-// skipped pair has aT = 0, so the outputs are bit-identical to the per-lane
-// sequential blend; the VALU no longer issues the 2 x 16 language FMAs per
-// candidate pair, which run on the otherwise idle matrix pipe.
+// operand of v_mfma_f32_16x16x4_f32, whose A operand is each 16-channel
+// block of the 4 candidates' language rows (gathered per lane; their RGB is
+// staged in LDS with the candidate).  The MFMA is bitwise a fmaf chain over
+// its 4 K terms in order (tools/micro/mfma_order.hip) and a skipped pair has
+// aT = 0, so the outputs are bit-identical to the per-lane sequential blend;
+// the VALU no longer issues the 2 x D language FMAs per candidate pair, which
+// run on the otherwise idle matrix pipe.  (The LDS-staged-row form, D = 16,
+// measured slower than the VALU blend and is not launched.)
 // MLM (with ML): D below the language set's width NL (masked channels);
 // otherwise D == NL is a compile-time constant (fewer registers).
 template <int NL, bool ZERO = false, bool ML = false, bool MLM = false>
@@ -263,6 +228,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
     constexpr int F4 = (C + 3) / 4;  // float4 per feature row
     constexpr bool SF = fwd_sfeat<NL>();
     static_assert(!ML || NL == 16 || NL == 32 || NL == 64, "ML: whole 16-channel language blocks");
+    static_assert(ML || !SF, "scalar feature rows (D >= LSR_FWD_SFEAT) feed the ML form only");
     constexpr int MLB = ML ? NL / 16 : 1;   // ML: 16-channel output blocks
     __shared__ WaveStageP<F4, SF> st;
 
@@ -275,11 +241,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
     const uint32_t rs = a.tile_start[wt.tile], re = a.tile_start[wt.tile + 1];
     const int D = (ML && !MLM) ? NL : a.D;
 
-    // T0 (scalar feature rows): a finished pixel carries T = 0 and its final T
-    // in Tout, instead of a per-pixel `done` mask (see the T0 loop below)
-    constexpr bool T0 = SF && LSR_FWD_T0_SF && !ML;
-    float T = (T0 && !inside) ? 0.f : 1.0f;
-    float Tout = 0.f;
+    float T = 1.0f;
     bool done = !inside;
     float acc[F4 * 4];
 #pragma unroll
@@ -306,7 +268,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
         B1 = a.splatB[next_gid];
     }
     for (uint32_t base = rs; base < re; base += 64) {
-        if (wave_ballot(T0 ? (T > 0.f) : !done) == 0) break;
+        if (wave_ballot(!done) == 0) break;
         const uint32_t idx = base + lane;
         const bool valid = idx < re;
         const uint32_t gid = next_gid;
@@ -381,17 +343,11 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                     // rgb; past the chunk a staged row's (aT = 0 there)
                     const int kk = min(q0 + k, n - 1);
                     float f0, f1, f2;
-                    if constexpr (SF && LSR_FWD_SF_RGB) {   // the staged line
+                    if constexpr (SF) {   // the line staged with the candidate
                         const float4 f = st.R[kk];
                         f0 = f.x;
                         f1 = f.y;
                         f2 = f.z;
-                    } else if constexpr (SF) {   // uniform id: scalar loads
-                        const lsr_cfptr rgb = (lsr_cfptr)a.rgb;
-                        const uint32_t g = __builtin_amdgcn_readfirstlane(st.gid[kk]);
-                        f0 = rgb[3 * g];
-                        f1 = rgb[3 * g + 1];
-                        f2 = rgb[3 * g + 2];
                     } else {
                         const float4 f = st.F[kk * F4];
                         f0 = f.x;
@@ -429,49 +385,6 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                     for (int nb = 0; nb < MLB; nb++)
                         mlacc[nb][pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[nb], s4[pb], mlacc[nb][pb], 0, 0, 0);
             }
-        } else if constexpr (T0) {
-            // T0 form (r03): a finished pixel carries T = 0 (its final T kept in
-            // Tout), so every later candidate is an exact no-op for it (alpha * 0
-            // = 0, and the termination test stays true) without a per-pixel
-            // `done` mask; the wave's early exit is voted once per 8 candidates.
-            // The exponent-cut test is dropped: below the cut alpha < e^-0.02 /
-            // 255 already fails the 1/255 test.  Per pixel the blend is the same
-            // sequence of operations, so the outputs are bit-identical.  Taken
-            // with scalar feature rows only (D >= 32: cfg5 render 1.715 ->
-            // 1.682 ms); with LDS-staged rows (D = 16) it measured +2 %.
-            for (int j0 = 0; j0 < n; j0 += 2) {
-                if ((j0 & 7) == 0 && wave_ballot(T > 0.f) == 0) break;
-                const bool two = j0 + 1 < n;
-                const int j1 = two ? j0 + 1 : j0;
-                const int e = j0 >> 1;
-                float fr0[F4 * 4], fr1[F4 * 4];
-                feature_row_uniform<NL, F4>(fr0, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j0]));
-                feature_row_uniform<NL, F4>(fr1, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j1]));
-                const f32x2 sX = st.X[e], sY = st.Y[e], sCA = st.CA[e], sCB = st.CB[e], sCC = st.CC[e];
-                const f32x2 OP = st.OP[e];
-                const f32x2 dx = sX - f32x2{pfx, pfx}, dy = sY - f32x2{pfy, pfy};
-                const f32x2 P = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f},
-                                                          __builtin_elementwise_fma(sCA * dx, dx, (sCC * dy) * dy),
-                                                          -((sCB * dx) * dy));
-                const f32x2 EX = expf_det2(P);
-                const float al0 = fminf(0.99f, OP.x * EX.x);
-                const float al1 = fminf(0.99f, OP.y * EX.y);
-                const float e0 = (!(P.x > 0.0f) && !(al0 < 1.0f / 255.0f)) ? al0 : 0.f;
-                const float e1 = (two && !(P.y > 0.0f) && !(al1 < 1.0f / 255.0f)) ? al1 : 0.f;
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const float ev = h ? e1 : e0;
-                    const float test_T = T * (1.0f - ev);
-                    const bool term = test_T < 0.0001f;
-                    const bool ok = (ev != 0.f) & !term;
-                    Tout = (term & (T > 0.f)) ? T : Tout;
-                    const float aT = ok ? ev * T : 0.f;
-#pragma unroll
-                    for (int k = 0; k < C; k++) acc[k] = fmaf(h ? fr1[k] : fr0[k], aT, acc[k]);
-                    T = term ? 0.f : test_T;
-                    lastj = ok ? (h ? j1 : j0) : lastj;
-                }
-            }
         } else
         for (int j0 = 0; j0 < n; j0 += 2) {
             if (wave_ballot(!done) == 0) break;
@@ -480,12 +393,6 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
             // both candidates' exponents at once (splat_power, lane-wise);
             // a missing second candidate reads a stale slot: ok1 masks it
             const int e = j0 >> 1;
-            // SF: the pair's feature rows (scalar loads; uniform ids)
-            float fr0[F4 * 4], fr1[F4 * 4];
-            if constexpr (SF) {
-                feature_row_uniform<NL, F4>(fr0, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j0]));
-                feature_row_uniform<NL, F4>(fr1, a.rgb, a.lang, D, __builtin_amdgcn_readfirstlane(st.gid[j1]));
-            }
             const f32x2 sX = st.X[e], sY = st.Y[e], sCA = st.CA[e], sCB = st.CB[e], sCC = st.CC[e];
             const f32x2 OP = st.OP[e];
             const f32x2 dx = sX - f32x2{pfx, pfx}, dy = sY - f32x2{pfy, pfy};
@@ -494,7 +401,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                                                       -((sCB * dx) * dy));
             const float p0 = P.x, p1 = P.y;
             // no exponent-cut test: below the cut alpha < e^-0.02 / 255, so the
-            // 1/255 test below rejects the pair anyway (exact, as in the T0 loop)
+            // 1/255 test below rejects the pair anyway (exact)
             bool ok0 = !done && !(p0 > 0.0f);
             bool ok1 = two && !done && !(p1 > 0.0f);
             const f32x2 EX = expf_det2(P);   // both exponents packed (bitwise = expf_det)
@@ -509,10 +416,6 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 ok0 = ok0 && !term;
                 ok1 = ok1 && !term;
                 const float aT = ok0 ? al0 * T : 0.f;
-                if constexpr (SF) {
-#pragma unroll
-                    for (int k = 0; k < C; k++) acc[k] = fmaf(fr0[k], aT, acc[k]);
-                } else
                 {
 #pragma unroll
                     for (int f = 0; f < F4; f++) {
@@ -536,10 +439,6 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 done = done || term;
                 ok1 = ok1 && !term;
                 const float aT = ok1 ? al1 * T : 0.f;
-                if constexpr (SF) {
-#pragma unroll
-                    for (int k = 0; k < C; k++) acc[k] = fmaf(fr1[k], aT, acc[k]);
-                } else
                 {
 #pragma unroll
                     for (int f = 0; f < F4; f++) {
@@ -564,7 +463,6 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
     if (inside) {
         const size_t HW = (size_t)c.H * c.W;
         const size_t pix = (size_t)pm.py * c.W + pm.px;
-        if (T0 && !(T > 0.f)) T = Tout;
         a.final_T[pix] = T;
         a.n_contrib[pix] = last;
 #pragma unroll
@@ -947,21 +845,17 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
         case 0: LSR_FWD_LAUNCH(k_render_fwd, 0); break;
         case 4: LSR_FWD_LAUNCH(k_render_fwd, 4); break;
         case 8: LSR_FWD_LAUNCH(k_render_fwd, 8); break;
-        case 16:
-            if (LSR_FWD_ML && a.D == 16) {
-                if (a.zero) k_render_fwd<16, true, true><<<4 * T, 64, 0, st>>>(a);
-                else k_render_fwd<16, false, true><<<4 * T, 64, 0, st>>>(a);
-            } else LSR_FWD_LAUNCH(k_render_fwd, 16);
-            break;
-        // measured (cfg3 geometry): D = 32 legacy 0.78 vs MFMA 0.81 ms; D = 64 legacy 1.38 vs MFMA 1.13 ms
+        // D <= 16: the VALU blend (the ML form measured +2.6 % at cfg3, +6.7 % at cfg2)
+        case 16: LSR_FWD_LAUNCH(k_render_fwd, 16); break;
         case 32:
-            if (LSR_FWD_ML32 && a.D == 32) {
+            // D in (16, 32]: the ML form (cfg5 render_fwd 1.650 -> 1.266 ms against the VALU blend)
+            if (a.D == 32) {
                 if (a.zero) k_render_fwd<32, true, true><<<4 * T, 64, 0, st>>>(a);
                 else k_render_fwd<32, false, true><<<4 * T, 64, 0, st>>>(a);
-            } else if (LSR_FWD_ML32) {
+            } else {
                 if (a.zero) k_render_fwd<32, true, true, true><<<4 * T, 64, 0, st>>>(a);
                 else k_render_fwd<32, false, true, true><<<4 * T, 64, 0, st>>>(a);
-            } else LSR_FWD_LAUNCH(k_render_fwd, 32);
+            }
             break;
         case 64:
             // D = 64: always the ML form (measured 0.996 -> 0.688 ms against the
