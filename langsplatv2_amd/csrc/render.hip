@@ -127,7 +127,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // each field with one ds_read_b64 and evaluates both exponents with packed
 // f32 instructions (bitwise identical to the scalar ones).
 #ifndef LSR_FWD_SFEAT
-#define LSR_FWD_SFEAT 32    // fwd: from this many language channels up, feature rows are not staged in LDS:
+#define LSR_FWD_SFEAT 16    // fwd: from this many language channels up, feature rows are not staged in LDS:
                             // the ML form gathers the candidates' language slices as MFMA operands and
                             // stages only their RGB
 #endif
@@ -845,8 +845,21 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
         case 0: LSR_FWD_LAUNCH(k_render_fwd, 0); break;
         case 4: LSR_FWD_LAUNCH(k_render_fwd, 4); break;
         case 8: LSR_FWD_LAUNCH(k_render_fwd, 8); break;
-        // D <= 16: the VALU blend (the ML form measured +2.6 % at cfg3, +6.7 % at cfg2)
-        case 16: LSR_FWD_LAUNCH(k_render_fwd, 16); break;
+        // D in (8, 16]: the ML form with gathered rows (cfg3 render_fwd 0.307 -> 0.299 ms against the
+        // VALU blend; the ML form with LDS-staged rows measured +2.6 %)
+        case 16:
+            if constexpr (fwd_sfeat<16>()) {
+                if (a.D == 16) {
+                    if (a.zero) k_render_fwd<16, true, true><<<4 * T, 64, 0, st>>>(a);
+                    else k_render_fwd<16, false, true><<<4 * T, 64, 0, st>>>(a);
+                } else {
+                    if (a.zero) k_render_fwd<16, true, true, true><<<4 * T, 64, 0, st>>>(a);
+                    else k_render_fwd<16, false, true, true><<<4 * T, 64, 0, st>>>(a);
+                }
+            } else {
+                LSR_FWD_LAUNCH(k_render_fwd, 16);
+            }
+            break;
         case 32:
             // D in (16, 32]: the ML form (cfg5 render_fwd 1.650 -> 1.266 ms against the VALU blend)
             if (a.D == 32) {
