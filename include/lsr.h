@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 6
+#define LSR_ABI_VERSION 7
 
 enum {
     LSR_OK = 0,
@@ -51,7 +51,8 @@ enum {
     LSR_EHIP = 3,          /* HIP launch / runtime failure */
     LSR_ENOMEM = 4,        /* alloc callback returned NULL */
     LSR_EOVERFLOW = 5,     /* num_rendered does not fit 32-bit instance indices */
-    LSR_ENONFINITE = 6     /* debug guard: NaN/Inf in an input or output */
+    LSR_ENONFINITE = 6,    /* debug guard: NaN/Inf in an input or output */
+    LSR_ELISTS = 7         /* debug check: corrupt binning lists (id >= P, tile ranges not monotone) */
 };
 
 /* GaussianRasterizationSettings (gaussian_renderer/__init__.py:37-52),

@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("LSR_LIB", os.path.join(_HERE, "liblsr.so"))
 
 LSR_OK = 0
 LSR_ENONFINITE = 6
+LSR_ELISTS = 7
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_GRAD, LSR_BUF_DECODE, LSR_BUF_KNN, LSR_BUF_LOSS = 0, 1, 2, 3, 4, 5, 6
 LSR_BUF_GUARD, LSR_BUF_SPARSE = 7, 8
 LSR_INDEX_F32, LSR_INDEX_I32, LSR_INDEX_I64 = 0, 1, 2

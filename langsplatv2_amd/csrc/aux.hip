@@ -6,6 +6,8 @@
 //    call and returns LSR_ENONFINITE naming the first offending array; the
 //    reference's nearest hooks are pipe.debug (gaussian_renderer/__init__.py:49)
 //    and --detect_anomaly (train.py:362).
+//  * k_check_lists: the debug-mode check of the binning lists (ids in range,
+//    tile ranges monotone) before a render gathers through them.
 //  * k_sparse_expand / k_sparse_gather: the quick (sparse) language input
 //    (weights (N,K), indices (N,K), utils/vq_utils.py:26-40) expanded to dense
 //    (N,Dq) rows, and the dense language gradient gathered back to dL/dweights.
@@ -34,6 +36,32 @@ hipError_t launch_nonfinite(const float* p, size_t n, uint32_t* flag, hipStream_
     if (n == 0) return hipSuccess;
     const size_t blocks = (n / 4 + 255) / 256;
     k_nonfinite<<<(unsigned)(blocks < 2048 ? (blocks > 0 ? blocks : 1) : 2048), 256, 0, st>>>(p, n, flag);
+    return hipGetLastError();
+}
+
+// Debug check of the binning lists before a render reads them (settings.debug):
+// every point_list id < P, tile_start[0] == 0, tile_start non-decreasing and
+// tile_start[T] == M.  A corrupt list (a sort or scatter bug) then returns
+// LSR_ELISTS instead of faulting inside the render's gathers.
+__global__ void __launch_bounds__(256) k_check_lists(const uint32_t* __restrict__ point_list, size_t M, uint32_t P,
+                                                     const uint32_t* __restrict__ tile_start, size_t T,
+                                                     uint32_t* __restrict__ flag)
+{
+    const size_t stride = (size_t)gridDim.x * 256;
+    bool bad = false;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < M; i += stride) bad |= point_list[i] >= P;
+    for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < T; t += stride) bad |= tile_start[t + 1] < tile_start[t];
+    if (blockIdx.x == 0 && threadIdx.x == 0) bad |= tile_start[0] != 0u || (size_t)tile_start[T] != M;
+    if (wave_any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
+hipError_t launch_check_lists(const uint32_t* point_list, size_t M, uint32_t P, const uint32_t* tile_start, size_t T,
+                              uint32_t* flag, hipStream_t st)
+{
+    const size_t n = M > T ? M : T;
+    const size_t blocks = (n + 255) / 256;
+    k_check_lists<<<(unsigned)(blocks < 2048 ? (blocks > 0 ? blocks : 1) : 2048), 256, 0, st>>>(point_list, M, P,
+                                                                                                  tile_start, T, flag);
     return hipGetLastError();
 }
 

@@ -23,9 +23,6 @@
 
 #include <algorithm>
 
-#ifndef LSR_SCATTER_PROBE
-#define LSR_SCATTER_PROBE 0
-#endif
 #ifndef LSR_BIN_TARGET
 #define LSR_BIN_TARGET 512   // (chunk x band) blocks of the privatised count / scatter
 #endif
@@ -501,9 +498,6 @@ __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int r
     WaveSpans& ws = wss[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
     const int g0 = blk * chunk, g1 = min(P, g0 + chunk);
-#ifdef LSR_PROBE_CNT
-    uint32_t probe_acc = 0;
-#endif
     BinRec nx;
     if (g0 < g1) nx.load(geom, P, g1, radii, g0 + (threadIdx.x & ~63) + lane, false);
     for (int i0 = g0 + (threadIdx.x & ~63); i0 < g1; i0 += BB) {
@@ -517,19 +511,12 @@ __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int r
             int sx0, sx1, yr;
             row_entry(ws, e, bd.ty0, sx0, sx1, yr);
             if (sx1 > sx0) {
-#ifdef LSR_PROBE_CNT   // timing probe only (wrong counts): no LDS atomics
-                probe_acc += (uint32_t)(yr * c.gx + sx0 + sx1);
-#else
                 atomicAdd(&hist[yr * c.gx + sx0], 1u);
                 if (sx1 < c.gx) atomicAdd(&hist[yr * c.gx + sx1], 0xffffffffu);
-#endif
             }
         }
         wave_lds_fence();
     }
-#ifdef LSR_PROBE_CNT
-    if (probe_acc == 0xdeadbeefu) hist[0] = probe_acc;
-#endif
     __syncthreads();
     // per band row: counts = running sum of the differences (mod 2^32), written
     // straight into the block's table row; one wave per row, 64 columns a step
@@ -775,13 +762,8 @@ __global__ void __launch_bounds__(BB) k_bin_scatter(Cam c, int P, int chunk, int
                         sb = atomicAdd(&base[sw.y * c.gx + sw.x], 1u);
                         kb = key[sw.o];
                     }
-#if LSR_SCATTER_PROBE
-                    if (sa == 0xffffffffu) keys[0] = ka;
-                    if (two && sb == 0xffffffffu) keys[0] = kb;
-#else
                     keys[sa] = ka;
                     if (two) keys[sb] = kb;
-#endif
                     k += 2;
                     if (k >= kend) break;
                     sw.next(ws);
@@ -1055,38 +1037,8 @@ __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m)
 #ifndef LSR_SORT_XBATCH
 #define LSR_SORT_XBATCH 1
 #endif
-// Partner value across lanes l <-> l ^ M without the LDS crossbar: the ISA
-// has a register path for every distance: v_permlane32_swap (M = 32),
-// v_permlane16_swap (M = 16), DPP row_ror:8 (M = 8), two DPP row rotations
-// and a select (M = 4), DPP quad_perm (M = 2, 1).
-template <int M>
-__device__ __forceinline__ uint32_t xor_lane_u32(uint32_t x)
-{
-    const int lane = threadIdx.x & 63;
-    if constexpr (M == 32) {
-        auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-        return (lane & 32) ? r[0] : r[1];
-    } else if constexpr (M == 16) {
-        auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
-        return (lane & 16) ? r[0] : r[1];
-    } else if constexpr (M == 8) {
-        return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, false);   // row_ror:8
-    } else if constexpr (M == 4) {
-        // l ^ 4 inside a row of 16.  row_ror:N makes lane l read lane (l - N) mod 16
-        // (as row_shr:N reads l - N), so row_ror:4 gives x[l - 4] (the partner
-        // where bit 2 of l is set) and row_ror:12 gives x[l + 4] (bit 2 clear).
-        const uint32_t from_below = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x124, 0xF, 0xF, false);
-        const uint32_t from_above = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x12C, 0xF, 0xF, false);
-        return (lane & 4) ? from_below : from_above;
-    } else if constexpr (M == 2) {
-        return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
-    } else if constexpr (M == 1) {
-        return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
-    } else {
-        return (uint32_t)__shfl_xor((int)x, M, 64);
-    }
-}
-
+// xor_lane_u32 (the register-path lane exchange) lives in lsr_device.h, where
+// tests/micro/micro_checks.hip checks it against __shfl_xor on the GPU.
 template <int M>
 __device__ __forceinline__ uint64_t xor_lane_u64(uint64_t v)
 {

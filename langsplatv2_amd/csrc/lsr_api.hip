@@ -126,6 +126,26 @@ struct Guard {
         }
         return LSR_OK;
     }
+    // the binning lists a render is about to gather through (debug only)
+    int check_lists(const char* what, const uint32_t* point_list, size_t M, int P, const uint32_t* tile_start, size_t T)
+    {
+        if (!s->debug || !tile_start || T == 0) return LSR_OK;
+        if (!flag) {
+            if (!alloc) return LSR_EINVAL;
+            flag = (uint32_t*)alloc(ctx, 256, LSR_BUF_GUARD);
+            if (!flag) return LSR_ENOMEM;
+        }
+        uint32_t h = 0;
+        LSR_HIP(hipMemsetAsync(flag, 0, 4, st));
+        LSR_HIP(launch_check_lists(point_list, M, (uint32_t)P, tile_start, T, flag, st));
+        LSR_HIP(hipMemcpyAsync(&h, flag, 4, hipMemcpyDeviceToHost, st));
+        LSR_HIP(hipStreamSynchronize(st));
+        if (h) {
+            fprintf(stderr, "[lsr] corrupt binning lists before %s\n", what);
+            return LSR_ELISTS;
+        }
+        return LSR_OK;
+    }
 };
 
 #define LSR_GUARD(g, what, p, n)                          \
@@ -253,6 +273,7 @@ const char* lsr_strerror(int code)
         case LSR_ENOMEM: return "workspace allocation failed";
         case LSR_EOVERFLOW: return "num_rendered exceeds 32-bit instance indexing";
         case LSR_ENONFINITE: return "non-finite (NaN/Inf) values in an input or output (debug guard)";
+        case LSR_ELISTS: return "corrupt binning lists: a Gaussian id out of range or tile ranges not monotone (debug check)";
         default: return "unknown error";
     }
 }
@@ -681,11 +702,6 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     }
     out->binning = bin;
     out->binning_bytes = bin_cap;
-#if LSR_SCATTER_PROBE
-    // measurement build: the probe scatter stores no keys, so give the sort
-    // and the render valid ids (all 0)
-    if (priv) LSR_HIP(hipMemsetAsync(bin + BL.keys, 0, (size_t)M * 8, st));
-#endif
     if (priv) {
         StageScope sc(ST_SCATTER, st);
         LSR_HIP(launch_bin_scatter(c, P, chunk, B, geom, out->radii, table, tile_start, (uint64_t*)(bin + BL.keys),
@@ -715,6 +731,10 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
 
     // 4. render (and the backward's accumulators zeroed alongside it)
     RenderArgs ra = make_render_args(s, in, c, geom, bin, img, (int64_t)M);
+    {
+        const int lrc = guard.check_lists("render", ra.point_list, (size_t)M, P, ra.tile_start, (size_t)T);
+        if (lrc != LSR_OK) return lrc;
+    }
     ra.out_color = out->out_color;
     ra.out_lang = out->out_lang;
     out->grad_ws = nullptr;
@@ -883,6 +903,13 @@ int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* 
     Guard guard(s, alloc, ctx, st);
     LSR_GUARD(guard, "dL_dout_color", b->dL_dout_color, 3 * NPIX);
     LSR_GUARD(guard, "dL_dout_lang", b->dL_dout_lang, (size_t)(s->quick_render ? quick_dim(s) : Dd) * NPIX);
+    if (s->debug) {   // the saved lists the render backward gathers through
+        const RenderArgs la = make_render_args(s, in, c, (const uint8_t*)b->geom, (const uint8_t*)b->binning,
+                                               (const uint8_t*)b->image, b->num_rendered);
+        const int lrc = guard.check_lists("render_bwd", la.point_list, (size_t)b->num_rendered, P, la.tile_start,
+                                          (size_t)c.gx * c.gy);
+        if (lrc != LSR_OK) return lrc;
+    }
     if (s->quick_render) return backward_quick(s, in, b, out, alloc, ctx, st, guard);
     return backward_dense(s, in, b, out, alloc, ctx, st, guard);
 }

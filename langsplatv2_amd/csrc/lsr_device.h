@@ -282,6 +282,28 @@ __device__ __forceinline__ float power_cut(float o)
     return (float)(-log((double)(255.0f * o))) - 0.02f;
 }
 
+// The cut as stored in the splat record: power_cut widened by the fp32
+// conic's conditioning K = ca cc / det (>= 1).  Every test that uses the cut
+// (the binning's cull_box / row_span, the render's block_overlap_exact and
+// cut_extent) evaluates an ellipse from ca, cb, cc in fp32, and the render
+// evaluates splat_power in fp32; for a needle splat (K ~ 1e5 after the 0.3 px
+// dilation) det = ca cc - cb^2 keeps only ~log2(1/K) of its bits and the
+// quadratic form's rounding grows like eps K |q|.  Scaling the cut by
+// (1 + 8e-6 K) -- 4x the worst-case fp32 error of both (2 eps K for det,
+// ~12 eps K for q) -- keeps every test conservative however thin the splat;
+// at the usual K < 100 it widens the cut by < 1e-3.  A widened cut only keeps
+// more instances / candidates, never changes an output.  det <= 0 in fp32:
+// -inf (no cull at all).  The oracle restates it operation for operation
+// (lso_cut_widen).
+__device__ __forceinline__ float cut_widen(float cut, float ca, float cb, float cc)
+{
+    const float p = ca * cc;
+    const float det = p - cb * cb;
+    if (!(det > 0.f)) return -INFINITY;
+    const float K = p / det;
+    return cut * fmaf(K, 8e-6f, 1.0f);
+}
+
 // Conservative half-extents (pixels) of the region where power >= cut, i.e.
 // where a pair can contribute: the cut ellipse Q(d) <= 2|cut| has bounding
 // half-widths sqrt(2|cut| * cov2D.xx) and sqrt(2|cut| * cov2D.yy) (the conic
@@ -441,6 +463,38 @@ __device__ __forceinline__ void row_span(const SpanPrep& s, int ty, int bx0, int
 __device__ __forceinline__ SpanPrep span_prep(const float4& A, const float4& B)
 {
     return span_prep(A.x, A.y, A.z, A.w, B.x, B.z);
+}
+
+// Partner value across lanes l <-> l ^ M without the LDS crossbar: the ISA
+// has a register path for every distance: v_permlane32_swap (M = 32),
+// v_permlane16_swap (M = 16), DPP row_ror:8 (M = 8), two DPP row rotations
+// and a select (M = 4), DPP quad_perm (M = 2, 1).
+template <int M>
+__device__ __forceinline__ uint32_t xor_lane_u32(uint32_t x)
+{
+    const int lane = threadIdx.x & 63;
+    if constexpr (M == 32) {
+        auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        return (lane & 32) ? r[0] : r[1];
+    } else if constexpr (M == 16) {
+        auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+        return (lane & 16) ? r[0] : r[1];
+    } else if constexpr (M == 8) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, false);   // row_ror:8
+    } else if constexpr (M == 4) {
+        // l ^ 4 inside a row of 16.  row_ror:N makes lane l read lane (l - N) mod 16
+        // (as row_shr:N reads l - N), so row_ror:4 gives x[l - 4] (the partner
+        // where bit 2 of l is set) and row_ror:12 gives x[l + 4] (bit 2 clear).
+        const uint32_t from_below = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x124, 0xF, 0xF, false);
+        const uint32_t from_above = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x12C, 0xF, 0xF, false);
+        return (lane & 4) ? from_below : from_above;
+    } else if constexpr (M == 2) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+    } else if constexpr (M == 1) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+    } else {
+        return (uint32_t)__shfl_xor((int)x, M, 64);
+    }
 }
 
 // ------------------------------------------------------------- layouts --

@@ -133,6 +133,8 @@ hipError_t launch_lang_loss(const float* wmap, const float* cb, int Df, int H, i
 // aux.hip: debug NaN/Inf guard (flag |= 1 if any element of p[0..n) is not
 // finite) and the quick-input dense expansion / gradient gather
 hipError_t launch_nonfinite(const float* p, size_t n, uint32_t* flag, hipStream_t st);
+hipError_t launch_check_lists(const uint32_t* point_list, size_t M, uint32_t P, const uint32_t* tile_start, size_t T,
+                              uint32_t* flag, hipStream_t st);
 hipError_t launch_sparse_expand(const float* qw, const void* qi, int dtype, int N, int K, int Dq, float* dense,
                                 hipStream_t st);
 hipError_t launch_sparse_gather(const float* g, const void* qi, int dtype, int N, int K, int Dq, float* dw,

@@ -195,9 +195,10 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
     if (!LSR_PRE_SH_EARLY) o = in.opacities[i];
     depth[i] = pv.z;
     radii[i] = r;
-    splatA[i] = make_float4(px, py, cc * det_inv, -b * det_inv);
-    const float cut = power_cut(o);
-    splatB[i] = make_float4(a * det_inv, o, cut, __uint_as_float(cut_extent(cut, a, cc, det)));
+    const float ca = cc * det_inv, cb = -b * det_inv, ccn = a * det_inv;   // the conic as stored
+    splatA[i] = make_float4(px, py, ca, cb);
+    const float cut = cut_widen(power_cut(o), ca, cb, ccn);
+    splatB[i] = make_float4(ccn, o, cut, __uint_as_float(cut_extent(cut, a, cc, det)));
     tiles[i] = (uint32_t)area;
 }
 

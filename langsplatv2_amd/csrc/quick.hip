@@ -327,16 +327,9 @@ __global__ void __launch_bounds__(64, LSR_DEC_WAVES) k_quick_decode_h(const floa
 #pragma unroll
                 for (int pb = 0; pb < PB; pb++) {
                     f32x4q acc = {0.f, 0.f, 0.f, 0.f};
-#ifdef LSR_PROBE_DEC_NOMFMA   // timing probe only (wrong results): stores without the matrix work
-                    acc = f32x4q{(float)db, (float)pb, (float)lane, 1.f};
-#else
                     LSR_DEC_MFMA6(acc, pb);
-#endif
                     const int xo = bx + 16 * pb + 4 * lg;
                     float* o = od + xo;
-#ifdef LSR_PROBE_DEC_NOSTORE   // timing probe only: matrix work without the stores
-                    if (acc[0] != 1234.5f) continue;
-#endif
                     if (VEC && xo + 3 < W) {
                         *reinterpret_cast<float4*>(o) = make_float4(acc[0] * mul[pb][0], acc[1] * mul[pb][1],
                                                                     acc[2] * mul[pb][2], acc[3] * mul[pb][3]);
@@ -519,6 +512,9 @@ __global__ void __launch_bounds__(64 * LSR_DEC2_WAVES, 1)
             m = fmaxf(m, __shfl_xor(m, 32, 64));
             int e = 0;
             if (m > 0.f && m < 3.0e38f) (void)frexpf(m, &e);
+            // both factors stay finite normals: a subnormal m (e down to -148)
+            // or m >= 2^127 would otherwise make inv or psc infinite
+            e = min(max(e, -126), 126);
             psc[pb] = ldexpf(1.f, e);
             const float inv = ldexpf(1.f, -e);
 #pragma unroll

@@ -12,10 +12,13 @@
 // ahead), the 32-B splat records and feature rows, tests each against its
 // 8x8 block with the per-Gaussian cut ellipse (block_overlap), and compacts
 // the survivors in order with __ballot + mbcnt into its private LDS stage.
-// The conservative exponent cut (splat record B.z) skips pairs whose alpha is
-// certainly < 1/255 without evaluating exp.  No MFMA in the forward: the blend
-// is a serial per-pixel recurrence; two instances per step keep two
-// independent exp chains in flight.
+// The per-pixel blend recurrence (alpha, transmittance, early termination)
+// is serial and stays on the VALU, two candidates per step (two independent
+// exp chains in flight).  For D > 8 the language channels accumulate on the
+// matrix cores (the ML form of k_render_fwd: per 4 candidates the 4 x 64
+// weights aT are transposed in registers into the B operand of
+// v_mfma_f32_16x16x4_f32, bitwise the sequential fmaf chain); the quick path
+// adds its sparse codes into register-resident accumulators.
 //
 // Backward (k_render_bwd_mf): same mapping, instances replayed back to front
 // from the wave's largest n_contrib in groups of 16 candidates: alpha/G per
@@ -938,20 +941,10 @@ __device__ __forceinline__ float gd_at(const RenderBwdArgs& b, int c, int q, int
 #ifndef LSR_GRP_STRIDE
 #define LSR_GRP_STRIDE 66   // dot/u and aT tiles: conflict-free A-fragment reads (li*66 mod 32 = 2 li)
 #endif
-#ifndef LSR_PROBE_ATOM_ON      // timing probe only: (false) every atomic's offset out of range (no memory traffic)
-#define LSR_PROBE_ATOM_ON(on) (on)
-#endif
-#ifndef LSR_PROBE_ATOM_ISSUE   // timing probe only: (0) no atomic instructions at all
-#define LSR_PROBE_ATOM_ISSUE 1
-#endif
 #define LSR_BUF_OOB 0x7ffffffc  // a byte offset past every buffer the backward addresses this way
 #define LSR_MOM9_STRIDE 12  // reduced moment + colour sums per candidate (16-B aligned rows)
 #define LSR_LOG2E 1.4426950408889634f
-#ifdef LSR_MF_NO_ATOMIC   // timing experiment only: keeps the work, drops the atomics
-#define LSR_MF_ATOMIC(ptr, v) do { if ((v) == 1234.5678f) atomicAdd((ptr), (v)); } while (0)
-#else
 #define LSR_MF_ATOMIC(ptr, v) atomicAdd((ptr), (v))
-#endif
 
 // Lane mask of |v| < bound, straight from the compare (the compiler otherwise
 // round-trips a ballot's operand through a VGPR: two extra VALU per use).
@@ -1064,13 +1057,7 @@ __device__ __forceinline__ void dot_features(const RenderArgs& a, uint32_t gid, 
     }
 }
 
-#if defined(LSR_EXP_NOMF2)   // timing experiment only (wrong results): a lane-wise FMA instead of each MFMA
-#define BWD_MFMA(a, b_, c) ((c) + f32x4{(a) * (b_), (a) + (b_), (a), (b_)})
-#elif defined(LSR_EXP_NOMF)   // timing experiment only (wrong results): no matrix-core work
-#define BWD_MFMA(a, b_, c) (c)
-#else
 #define BWD_MFMA(a, b_, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b_), (c), 0, 0, 0)
-#endif
 // LO (language only): the autograd call needs dL/dlanguage alone (feature-mode
 // training: geometry frozen, scene/gaussian_model.py:238-243, and means2D not
 // requiring grad).  Then dL/dlang[j][c] = sum_p aT[j][p] dL/dout[c][p] is all
@@ -1121,10 +1108,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     __shared__ float sBc[64];         // dL/dout B
     constexpr int GS = LSR_GRP_STRIDE;
     __shared__ WaveStageG st;
-#ifdef LSR_BWD_LDS_PAD   // occupancy experiment only: extra LDS per wave
-    __shared__ float lds_pad[LSR_BWD_LDS_PAD];
-    if (b.VP == -12345) lds_pad[blockIdx.x % LSR_BWD_LDS_PAD] = 0.f;
-#endif
     // first language column of a staged row; LD: the language lines start at
     // 16 and go to b.lang_acc, the first line (geometry + colour) to the row
     constexpr int GCOL0 = LO ? 0 : (LD ? 16 : LSR_GROW_LANG);
@@ -1248,21 +1231,13 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
         for (int t = 0; t < KS; t++)
 #pragma unroll
             for (int pb = 0; pb < 4; pb++)
-#ifdef LSR_PROBE_NOPRO   // timing probe only (wrong results): no prologue dL/dout loads
-                dotB[t][pb] = (float)(t * 4 + pb + lane);
-#else
                 dotB[t][pb] = gd_at<NL>(b, dot_channel<NL, VEC>(t, lg), pb * 16 + li, pm.bx, pm.by);
-#endif
     }
 #pragma unroll
     for (int nb = 0; nb < NBC; nb++)
 #pragma unroll
         for (int t = 0; t < 16; t++)
-#ifdef LSR_PROBE_NOPRO
-            chB[nb][t] = (float)(t + lane);
-#else
             chB[nb][t] = gd_at<NL>(b, 3 + nb * 16 + li, 4 * t + lg, pm.bx, pm.by);
-#endif
     }
     // block-centred x of the pixels this lane's fragments cover: columns lg
     // (even K-steps) and 4 + lg (odd K-steps)
@@ -1314,12 +1289,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             // gathered now, consumed after phase 1
             if constexpr (!LO) {
                 const uint32_t gi = st.gid[g0 + (li < kn ? li : 0)];
-#ifdef LSR_PROBE_NOFEAT   // timing probe only (wrong results): no feature gather
-#pragma unroll
-                for (int t = 0; t < KS; t++) af[t] = __uint_as_float(gi) * 1e-30f;
-#else
                 dot_features<NL, VEC>(a, gi, lg, af);
-#endif
             }
             // phase 1: G of the 16 candidates (0 where the pair does not
             // contribute), independent across candidates; straight-line code.
@@ -1368,19 +1338,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 }
             }
             BWD_STAMP(2);
-#ifdef LSR_PROBE_ADDVALU   // timing probe only: LSR_PROBE_ADDVALU extra independent VALU ops per group
-            {
-                float z0 = __uint_as_float(lane), z1 = z0 + 1.f, z2 = z0 + 2.f, z3 = z0 + 3.f;
-#pragma unroll
-                for (int i = 0; i < LSR_PROBE_ADDVALU / 4; i++) {
-                    asm volatile("v_fmac_f32 %0, %1, %1" : "+v"(z0) : "v"(z1));
-                    asm volatile("v_fmac_f32 %0, %1, %1" : "+v"(z1) : "v"(z2));
-                    asm volatile("v_fmac_f32 %0, %1, %1" : "+v"(z2) : "v"(z3));
-                    asm volatile("v_fmac_f32 %0, %1, %1" : "+v"(z3) : "v"(z0));
-                }
-                if (z0 == 1234.5f) sAT[lane] = z3;
-            }
-#endif
             // dot[k][p] of the group's candidates on MFMA: (16 x C) . (C x 64)
             if constexpr (!LO) {
                 f32x4 acc[4];
@@ -1621,10 +1578,10 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                             const bool on = fcol & (slot_of(q) < kn) & (v != 0.f);
                             if (LD && h > 0) {
                                 const int off = (int)(gq[q] * (uint32_t)D + (uint32_t)(f - 16)) * 4;
-                                if (LSR_PROBE_ATOM_ISSUE) __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, rl, LSR_PROBE_ATOM_ON(on) ? off : LSR_BUF_OOB, 0, 0);
+                                __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, rl, on ? off : LSR_BUF_OOB, 0, 0);
                             } else {
                                 const int off = (int)(gq[q] * (uint32_t)VP + (uint32_t)f) * 4;
-                                if (LSR_PROBE_ATOM_ISSUE) __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, rg, LSR_PROBE_ATOM_ON(on) ? off : LSR_BUF_OOB, 0, 0);
+                                __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, rg, on ? off : LSR_BUF_OOB, 0, 0);
                             }
                         }
                     }

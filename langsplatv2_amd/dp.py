@@ -150,9 +150,16 @@ class ViewShardedExchange:
     `grads` are views of the reduced buckets in `params` order."""
 
     def __init__(self, params: list[torch.Tensor], with_stats: bool = True, group=None, names=None,
-                 factor_sh: bool | None = None):
+                 factor_sh: bool | None = None, force_collectives: bool = False):
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        # force_collectives (test hook): take every collective branch even at
+        # world size 1 (side-stream early all-reduce, factored SH all-gather,
+        # MAX of the radii), so the RCCL code paths run on a one-GPU box
+        # (tests/test_rccl_paths.py); the sums over one rank are identities
+        if force_collectives and not dist.is_initialized():
+            raise ValueError("force_collectives needs an initialised process group")
+        self.collective = self.world > 1 or force_collectives
         self.group = group
         self.names = list(names) if names is not None else [None] * len(params)
         if len(self.names) != len(params):
@@ -162,7 +169,7 @@ class ViewShardedExchange:
         # view-factored SH gradient (see the module docstring): GPU, R > 1, SH parameter present
         sh_i = self.names.index("shs") if "shs" in self.names else None
         if factor_sh is None:
-            factor_sh = self.world > 1 and params[0].is_cuda and sh_i is not None
+            factor_sh = self.collective and params[0].is_cuda and sh_i is not None
         self.sh_idx = sh_i if factor_sh else None
         if self.sh_idx is not None:
             shp = params[self.sh_idx]
@@ -183,7 +190,7 @@ class ViewShardedExchange:
         self.cuda = params[0].is_cuda
         self._params = list(params)
         self._sink = None
-        if self.cuda and self.early is not None and self.world > 1:
+        if self.cuda and self.early is not None and self.collective:
             self._ev = torch.cuda.Event()
             self._side = torch.cuda.Stream(device=params[0].device)
 
@@ -215,7 +222,7 @@ class ViewShardedExchange:
             self._launch_early()
 
     def _launch_early(self):
-        if self.world <= 1 or self.early is None or self._early_work is not None:
+        if not self.collective or self.early is None or self._early_work is not None:
             return
         if self._side is not None:
             self._side.wait_event(self._ev)
@@ -258,7 +265,10 @@ class ViewShardedExchange:
     def finish(self, means2D_grad=None, radii=None, grads=None, campos=None, means3D=None, sh_degree=None):
         """Complete the exchange after a `sink()` backward: any gradient in
         `grads` that did not land in its bucket view (e.g. a parameter without
-        grad this step) is packed (None -> zeros), the statistics are added, the
+        grad this step) is packed (None -> zeros); a gradient the backward wrote
+        into its view through the sink is taken from the view whatever `grads`
+        holds for it (torch.autograd.grad returns the view itself, loss.backward()
+        leaves a copy in p.grad); the statistics are added, the
         remaining all-reduce runs and every pending one is waited for.  With the
         factored SH gradient, `campos` (this view's camera centre), `means3D`
         and `sh_degree` (the rasterizer settings') are required."""
@@ -272,6 +282,14 @@ class ViewShardedExchange:
                 if i == self.sh_idx and factored:
                     continue   # filled by _factored_sh below
                 if g is not None and g.data_ptr() == v.data_ptr():
+                    continue
+                if self.names[i] in used:
+                    # the backward wrote this bucket view itself: the view is the
+                    # gradient.  With loss.backward() inside `with ex.sink():`
+                    # AccumulateGrad keeps a COPY of the returned view as p.grad
+                    # (the sink holds a second reference), so `grads` may carry
+                    # that copy; packing it would race with an early all-reduce
+                    # already running on the view.
                     continue
                 if i in self.early_idx and self._early_work is not None:
                     # the early all-reduce is in flight on this view: packing it now would race
@@ -288,7 +306,7 @@ class ViewShardedExchange:
                 raise ValueError("finish: densification statistics need means2D.grad and radii")
             self.main.flat[self.main.stats_offset:].copy_(densify_increment(means2D_grad, radii).reshape(-1))
         max_radii = radii
-        if self.world > 1:
+        if self.collective:
             self._launch_early()   # no-op if the backward already started it
             work = self.main.allreduce(self.group, async_op=True)
             if factored:
@@ -329,7 +347,7 @@ class ViewShardedExchange:
 
     def _finish_packed(self, radii):
         max_radii = radii
-        if self.world > 1:
+        if self.collective:
             if self.early is not None:
                 self._early_work = self.early.allreduce(self.group, async_op=True)
             if self.sh_idx is not None:

@@ -332,6 +332,19 @@ float lso_power_cut(float o)
     return (float)(-log((double)(255.0f * o))) - 0.02f;
 }
 
+/* The cut as the product stores it in the splat record (lsr_device.h
+ * cut_widen): power_cut scaled by (1 + 8e-6 K), K = ca cc / det of the fp32
+ * conic, so the cull stays conservative for needle splats; -inf when det <= 0
+ * in fp32. */
+float lso_cut_widen(float cut, float ca, float cb, float cc)
+{
+    const float p = ca * cc;
+    const float det = p - cb * cb;
+    if (!(det > 0.f)) return -INFINITY;
+    const float K = p / det;
+    return cut * fmaf(K, 8e-6f, 1.0f);
+}
+
 /* The product's cull box (csrc/lsr_device.h cull_box), restated operation for
  * operation: the tiles meeting the cut ellipse's axis-aligned box, widened by
  * 1e-4 relative + 0.5 px.  The cull keeps (Gaussian, tile) iff the tile is in
@@ -425,7 +438,8 @@ int64_t lso_num_rendered_ex(const lso_settings* s, int N, const lso_geom* g, int
         if (g->radii[i] <= 0) continue;
         int r0[2], r1[2];
         get_rect(g->xy[2 * i], g->xy[2 * i + 1], g->radii[i], gx, gy, r0, r1);
-        const float cut = lso_power_cut(g->conic_opacity[4 * i + 3]);
+        const float* coi = g->conic_opacity + 4 * i;
+        const float cut = lso_cut_widen(lso_power_cut(coi[3]), coi[0], coi[1], coi[2]);
         lso_span sp;
         gaussian_prep(g, i, cut, 1, r0, r1, &sp);
         if (r1[0] <= r0[0]) continue;
@@ -463,7 +477,8 @@ void lso_binning_ex(const lso_settings* s, int N, const lso_geom* g, uint32_t* p
         if (g->radii[i] <= 0) continue;
         int r0[2], r1[2];
         get_rect(g->xy[2 * i], g->xy[2 * i + 1], g->radii[i], gx, gy, r0, r1);
-        const float cut = lso_power_cut(g->conic_opacity[4 * i + 3]);
+        const float* coi = g->conic_opacity + 4 * i;
+        const float cut = lso_cut_widen(lso_power_cut(coi[3]), coi[0], coi[1], coi[2]);
         lso_span sp;
         gaussian_prep(g, i, cut, cull, r0, r1, &sp);
         if (r1[0] <= r0[0]) continue;
@@ -483,7 +498,8 @@ void lso_binning_ex(const lso_settings* s, int N, const lso_geom* g, uint32_t* p
         get_rect(g->xy[2 * i], g->xy[2 * i + 1], g->radii[i], gx, gy, r0, r1);
         uint32_t db;
         memcpy(&db, &g->depth[i], 4);
-        const float cut = lso_power_cut(g->conic_opacity[4 * i + 3]);
+        const float* coi = g->conic_opacity + 4 * i;
+        const float cut = lso_cut_widen(lso_power_cut(coi[3]), coi[0], coi[1], coi[2]);
         lso_span sp;
         gaussian_prep(g, i, cut, cull, r0, r1, &sp);
         if (r1[0] <= r0[0]) continue;

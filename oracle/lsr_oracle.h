@@ -97,6 +97,7 @@ int64_t lso_num_rendered_ex(const lso_settings* s, int N, const lso_geom* g, int
 void lso_binning_ex(const lso_settings* s, int N, const lso_geom* g,
                     uint32_t* point_list, uint32_t* ranges, int cull);
 float lso_power_cut(float opacity);
+float lso_cut_widen(float cut, float ca, float cb, float cc);
 /* the cull's box (lsr_device.h cull_box): shrinks the rect [r0, r1) to the
  * tiles meeting the cut ellipse's bounding box */
 void lso_cull_box(float x, float y, float ca, float cb, float cc, float cut, int* r0, int* r1);

@@ -25,6 +25,32 @@ def make_case(N, W, H, seed=0, sh_degree=None, lang_dim=0, quick_k=0, yaw=0.0, c
     return dict(cam=cam, g=g, bg=bg, scale_modifier=scale_modifier, quick=quick_k > 0)
 
 
+def add_needles(case, frac=0.25, seed=0, sigma_px=(60.0, 600.0), angle_deg=(30.0, 60.0)):
+    """Turn a fraction of the case's Gaussians into needle splats: one long axis
+    whose projected sigma is log-uniform in `sigma_px` pixels, two tiny axes
+    (the 0.3 px dilation then sets the short axis, so the 2D condition number
+    is ~sigma^2 / 0.3 = 1e4 .. 1e6), rotated in the image plane by an angle
+    uniform in `angle_deg` (either sign).  The camera looks along +z, so a
+    rotation about z is an in-plane rotation.  The needles are the regime where
+    det = ca cc - cb^2 of the fp32 conic loses most of its bits."""
+    g = case["g"]
+    assert "scales" in g, "needles need scales/rotations"
+    N = g["means3D"].shape[0]
+    rng = np.random.default_rng(seed)
+    idx = np.sort(rng.choice(N, size=max(1, int(frac * N)), replace=False))
+    cam = case["cam"]
+    focal = cam["W"] / (2.0 * cam["tanfovx"])
+    z = g["means3D"][idx, 2].numpy().astype(np.float64)
+    z = np.where(z > 0.5, z, 5.0)
+    sig = np.exp(rng.uniform(np.log(sigma_px[0]), np.log(sigma_px[1]), idx.size))
+    s = np.stack([sig * z / focal, np.full(idx.size, 1e-5), np.full(idx.size, 1e-5)], 1)
+    th = np.radians(rng.uniform(*angle_deg, idx.size)) * rng.choice([-1.0, 1.0], idx.size)
+    q = np.stack([np.cos(th / 2), np.zeros_like(th), np.zeros_like(th), np.sin(th / 2)], 1)
+    g["scales"][idx] = torch.from_numpy(s).float()
+    g["rotations"][idx] = torch.from_numpy(q).float()
+    return case
+
+
 def cov3d_torch(s, q):
     q = q.double()
     r, x, y, z = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
@@ -117,3 +143,34 @@ def assert_grad_close(name, got, ref, rtol=GRAD_RTOL, atol=GRAD_ATOL):
     err = float(np.abs(got - ref).max(initial=0.0))
     assert err <= atol + rtol * scale, f"{name}: max|err|={err:.3e} > {atol + rtol * scale:.3e} (max|ref|={scale:.3e})"
     return err, scale
+
+
+def needle_contributing_tiles(out, W, H, band=4.0):
+    """Per visible Gaussian of `out`: the tiles holding a pixel where the
+    render's fp32 evaluation (splat_power, alpha = min(0.99, o exp(power)))
+    gives alpha >= 1/255 and power <= 0.  Only pixels within `band` px of the
+    long axis are evaluated (needles: the contributing band is < 2 px wide)."""
+    xy, co, radii = out["xy"], out["conic_opacity"], out["radii"]
+    gx = (W + 15) // 16
+    res = {}
+    for i in np.nonzero(radii > 0)[0]:
+        x, y = xy[i]
+        ca, cb, cc, o = (np.float32(v) for v in co[i])
+        Q = np.array([[ca, cb], [cb, cc]], np.float64)
+        w, V = np.linalg.eigh(Q)
+        ax = V[:, 0]                      # long axis (smallest conic eigenvalue)
+        half = 3.0 / np.sqrt(max(w[0], 1e-12))
+        t = np.arange(-half, half + 1.0, 0.5)
+        s = np.arange(-band, band + 0.5, 0.5)
+        px = np.rint(x + t[:, None] * ax[0] + s[None, :] * ax[1]).astype(np.int64).ravel()
+        py = np.rint(y + t[:, None] * ax[1] - s[None, :] * ax[0]).astype(np.int64).ravel()
+        ok = (px >= 0) & (px < W) & (py >= 0) & (py < H)
+        pix = np.unique(py[ok] * W + px[ok])
+        ys, xs = pix // W, pix % W
+        dx = (np.float32(x) - xs.astype(np.float32)).astype(np.float32)
+        dy = (np.float32(y) - ys.astype(np.float32)).astype(np.float32)
+        p = np.float32(-0.5) * ((ca * dx) * dx + (cc * dy) * dy) - ((cb * dx) * dy)
+        a = np.minimum(np.float32(0.99), o * np.exp(p.astype(np.float64)).astype(np.float32))
+        m = (a >= np.float32(1 / 255.0)) & (p <= 0)
+        res[int(i)] = set(((ys[m] // 16) * gx + xs[m] // 16).tolist())
+    return res

@@ -109,3 +109,30 @@ def test_cfg3_culled_gpu_equals_full_reference_lists(gpu, oracle_lib):
     assert_grad_close("scales", got["grad_scales"], rb["dscales"])
     assert_grad_close("rotations", got["grad_rotations"], rb["drot"])
     assert_grad_close("language_feature_precomp", got["grad_language_feature_precomp"], rb["dlang"])
+
+
+def test_needles_culled_gpu_equals_full_reference_lists(gpu, oracle_lib):
+    """Needle splats (2D condition numbers 1e5-1e7, 30-60 degrees):
+    the GPU's culled lists equal the oracle's culled lists bit for bit, those
+    keep every (Gaussian, tile) with a contributing pixel, and the GPU's image
+    equals the oracle rendering the reference's UNCULLED lists on every tile a
+    needle contributes to (sampled)."""
+    from harness import add_needles, needle_contributing_tiles
+    W = H = 3072
+    case = add_needles(make_case(N=60, W=W, H=H, seed=31, sh_degree=None, lang_dim=3), frac=1.0, seed=1,
+                       sigma_px=(400.0, 1500.0))
+    gx = (W + 15) // 16
+    pb = oracle_problem(case)
+    culled = oracle_lib.forward(pb, nthreads=_threads(), tiles=np.zeros(0, np.int32), cull=True)
+    contrib = needle_contributing_tiles(culled, W, H)
+    alltiles = sorted(set().union(*contrib.values()))
+    tiles = np.sort(np.random.default_rng(4).choice(alltiles, size=min(96, len(alltiles)), replace=False)).astype(np.int32)
+    ref = oracle_lib.forward(pb, nthreads=_threads(), tiles=tiles, cull=False)
+    got = run_gpu_forward(case, gpu)
+    np.testing.assert_array_equal(got["point_list"], culled["point_list"].astype(np.int32))
+    np.testing.assert_array_equal(got["ranges"], culled["ranges"].astype(np.int32))
+    ys, xs = _tile_pixels(tiles, gx, W, H)
+    np.testing.assert_array_equal(got["color"][:, ys, xs], ref["color"][:, ys, xs])
+    np.testing.assert_array_equal(got["lang"][:, ys, xs], ref["lang"][:, ys, xs])
+    np.testing.assert_array_equal(got["final_T"][ys, xs], ref["final_T"][ys, xs])
+    assert float(ref["color"][:, ys, xs].max()) > 0.05

@@ -187,3 +187,42 @@ def test_early_allreduce_only_when_backward_wrote_the_early_bucket():
     sink.used.add("language_feature_precomp")
     ex._on_lang_ready(sink)
     assert launched == [1]
+
+
+def _backward_pattern_worker(rank, world, port):
+    """loss.backward() inside `with ex.sink():` -- the backward writes
+    the bucket views through the sink (and the early all-reduce starts from the
+    lang-ready callback), but AccumulateGrad leaves COPIES of the views in
+    p.grad, so finish() receives gradients that are not the views.  It must take
+    the views (not raise, not re-pack over the running all-reduce)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        names = ["means3D", "opacities", "language_feature_precomp"]
+        params = [torch.zeros(7, 3), torch.zeros(7, 1), torch.zeros(7, 16)]
+        ex = dp.ViewShardedExchange(params, with_stats=False, names=names)
+        g = torch.Generator().manual_seed(10 + rank)
+        local = [torch.randn(p.shape, generator=g) for p in params]
+        sink = ex.sink()
+        for nm, p, loc in zip(names, params, local):      # what the rasterizer backward does
+            buf = sink.take(nm, tuple(p.shape), p.device, id(p))
+            assert buf is not None
+            buf.copy_(loc)
+        ex._on_lang_ready(sink)                           # early (language) all-reduce starts now
+        assert ex._early_work is not None
+        copies = [loc.clone() for loc in local]           # AccumulateGrad's copies in p.grad
+        red, _, _ = ex.finish(None, None, copies)
+        exp = [torch.zeros_like(p) for p in params]
+        for r in range(world):
+            gr = torch.Generator().manual_seed(10 + r)
+            for i, p in enumerate(params):
+                exp[i] += torch.randn(p.shape, generator=gr)
+        for i in range(3):
+            assert torch.allclose(red[i], exp[i], rtol=0, atol=1e-6), names[i]
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_finish_after_backward_pattern_gloo_world2():
+    mp.spawn(_backward_pattern_worker, args=(2, _free_port()), nprocs=2, join=True)

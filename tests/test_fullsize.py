@@ -183,3 +183,68 @@ def test_cfg5_binning_and_image_properties(gpu):
     assert bool(torch.isfinite(color).all()) and bool(torch.isfinite(lang).all())
     fT = dec["final_T"]
     assert bool(((fT >= 0) & (fT <= 1)).all()) and bool((color >= 0).all())
+
+
+# --- the paths the bench and tools time at full size ---
+
+def test_quick_1mpix_full_binning_and_sampled_tiles(gpu, oracle_lib):
+    """bench.py quick_1mpix's render: 1M Gaussians, 1280x800, 3 levels x top-4
+    codes -> 192 channels (k_render_fwd_quick_v<6>, the VGPR-index-mode kernel,
+    reference eval_lerf.py:210-220).  The whole binning and 32 seeded tiles'
+    colour, 192-channel weight map, final_T and n_contrib bit-exact."""
+    case = make_case(N=1_000_000, W=1280, H=800, sh_degree=3, quick_k=4, seed=0)
+    W, H = 1280, 800
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    tiles = _sample_tiles(gx, gy, n=32, seed=9)
+    ref = oracle_lib.forward(oracle_problem(case), nthreads=_threads(), tiles=tiles)
+    got = run_gpu_forward(case, gpu)
+    assert got["lang"].shape == (192, H, W)
+    _compare_forward(got, ref, True, tiles, gx, W, H)
+    ys, xs = _tile_pixels(tiles, gx, W, H)
+    assert float(np.abs(ref["lang"][:, ys, xs]).max()) > 0.1     # the sampled tiles carry weights
+
+
+def _lang_only_grad(case, gpu, dcol, dlang):
+    """Feature-mode autograd (scene/gaussian_model.py:238-243): geometry frozen,
+    means2D without grad, only the language input requires grad -> the
+    library's language-only backward k_render_bwd_mf<NL, true>."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    from harness import settings_for
+    t = {k: v.to(gpu) for k, v in case["g"].items() if isinstance(v, torch.Tensor)}
+    lang = t["language_feature_precomp"].clone().requires_grad_(True)
+    r = GaussianRasterizer(settings_for(case, gpu))
+    color, lo, _ = r(means3D=t["means3D"], means2D=torch.zeros_like(t["means3D"]), opacities=t["opacities"],
+                     shs=t["shs"], scales=t["scales"], rotations=t["rotations"], language_feature_precomp=lang)
+    torch.autograd.backward([color, lo], [torch.from_numpy(dcol).to(gpu), torch.from_numpy(dlang).to(gpu)])
+    return lo.detach().cpu().numpy(), lang.grad.cpu().numpy()
+
+
+def test_d64_feature_step_shape_sampled_tiles(gpu, oracle_lib):
+    """tools/bench_train_step.py's rasterizer shape (BASELINE cfg4's step):
+    1M Gaussians, 1920x1080, SH3 + 64 language channels.  The ML-form forward
+    k_render_fwd<64, ., true> bit-exact on 48 seeded tiles (and the whole
+    binning), and the language-only backward k_render_bwd_mf<64, true> with
+    dL/dout zero outside 32 of them equal to the oracle's tile-restricted
+    backward (GRAD_RTOL)."""
+    case = make_case(N=1_000_000, W=1920, H=1080, sh_degree=3, lang_dim=64, seed=0)
+    W, H = 1920, 1080
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    tiles = _sample_tiles(gx, gy, n=48, seed=11)
+    pb = oracle_problem(case)
+    ref = oracle_lib.forward(pb, nthreads=_threads(), tiles=tiles)
+    got = run_gpu_forward(case, gpu)
+    assert got["lang"].shape == (64, H, W)
+    _compare_forward(got, ref, True, tiles, gx, W, H)
+    del got
+    btiles = tiles[:32]
+    ys, xs = _tile_pixels(btiles, gx, W, H)
+    rng = np.random.default_rng(2)
+    dcol = np.zeros((3, H, W), np.float32)
+    dlang = np.zeros((64, H, W), np.float32)
+    dcol[:, ys, xs] = rng.standard_normal((3, ys.size)).astype(np.float32)
+    dlang[:, ys, xs] = rng.standard_normal((64, ys.size)).astype(np.float32)
+    rb = oracle_lib.backward(pb, ref, dcol, dlang, tiles=btiles, nthreads=_threads())
+    lo, g = _lang_only_grad(case, gpu, dcol, dlang)
+    np.testing.assert_array_equal(lo[:, ys, xs], ref["lang"][:, ys, xs])
+    assert float(np.abs(rb["dlang"]).max()) > 0.0
+    assert_grad_close("language_feature_precomp", g, rb["dlang"])

@@ -15,7 +15,8 @@ from langsplatv2_amd import _lib
 def test_status_codes_have_text():
     lib = _lib.load()
     assert b"non-finite" in lib.lsr_strerror(_lib.LSR_ENONFINITE).lower()
-    assert lib.lsr_abi_version() == 6
+    assert b"binning lists" in lib.lsr_strerror(_lib.LSR_ELISTS).lower()
+    assert lib.lsr_abi_version() == 7
 
 
 def _render(case, dev, debug, poison=None):
@@ -51,3 +52,22 @@ def test_debug_guard_catches_nan_inputs_and_grads(gpu, tmp_path, monkeypatch):
         torch.autograd.backward([color, lang], [bad, torch.ones_like(lang)])
     # without debug nothing is scanned (the product path pays nothing)
     _render(case, gpu, False, poison="means3D")
+
+
+@pytest.mark.gpu
+def test_debug_list_check_catches_bad_ids(gpu, tmp_path, monkeypatch):
+    """with settings.debug the binning lists are checked
+    before a render gathers through them, so a corrupt list (an id >= P, as a
+    faulty sort would produce) returns LSR_ELISTS instead of faulting the GPU.
+    Here the forward's saved point_list is corrupted before the backward."""
+    from langsplatv2_amd import layout
+    monkeypatch.chdir(tmp_path)
+    case = make_case(N=2000, W=96, H=80, sh_degree=3, lang_dim=16, seed=0)
+    t, (color, lang, radii) = _render(case, gpu, True)
+    node = color.grad_fn                       # the autograd ctx of the rasterizer call
+    binning = node.saved_tensors[-2]           # (..., radii, geom, binning, image)
+    pl_off = layout.bin_layout(int(node.num_rendered))["point_list"]
+    # through .data: the saved tensor's version counter stays, as a kernel's stray write would leave it
+    binning.data[pl_off:pl_off + 4].view(torch.int32)[0] = 10 ** 8      # id far past P
+    with pytest.raises(RuntimeError, match="binning lists"):
+        torch.autograd.backward([color, lang], [torch.ones_like(color), torch.ones_like(lang)])

@@ -354,3 +354,31 @@ def test_tile_cull_changes_no_output(oracle_lib, name):
     for k, v in gf.items():
         if isinstance(v, np.ndarray) and v.dtype.kind == "f":
             np.testing.assert_array_equal(gc[k], v, err_msg=k)
+
+
+def test_tile_cull_keeps_needle_splats(oracle_lib):
+    """the cull sizes each Gaussian's box and row spans
+    from det = ca cc - cb^2 of the fp32 conic, which for needle splats (2D
+    condition number 1e5-1e7 after the 0.3 px dilation, rotated 30-60 degrees)
+    loses most of its bits.  The stored cut is widened by the conditioning
+    (lsr_device.h cut_widen / lso_cut_widen), so every (Gaussian, tile) with a
+    contributing pixel -- alpha >= 1/255 by the render's own fp32 evaluation --
+    stays in the culled lists.  (Without the widening this case drops
+    contributing needle-tip tiles.)"""
+    from harness import add_needles, needle_contributing_tiles
+    from oracle import oracle as O
+    W = H = 3072
+    miss = 0
+    for seed in range(2):
+        case = add_needles(make_case(N=60, W=W, H=H, seed=30 + seed, sh_degree=None), frac=1.0, seed=seed,
+                           sigma_px=(400.0, 1500.0))
+        out = O.forward(O.Problem(case["cam"], case["g"]), nthreads=4, tiles=np.zeros(0, np.int32), cull=True)
+        co = out["conic_opacity"].astype(np.float64)[out["radii"] > 0]
+        K = co[:, 0] * co[:, 2] / (co[:, 0] * co[:, 2] - co[:, 1] ** 2)
+        assert np.median(K) > 1e5          # the ill-conditioned regime
+        rg = out["ranges"].astype(np.int64)
+        tile_of = np.repeat(np.arange(rg.shape[0]), rg[:, 1] - rg[:, 0])
+        kept = set(zip(out["point_list"].astype(np.int64).tolist(), tile_of.tolist()))
+        for i, tiles in needle_contributing_tiles(out, W, H).items():
+            miss += sum((i, t) not in kept for t in tiles)
+    assert miss == 0

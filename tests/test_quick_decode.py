@@ -51,6 +51,23 @@ def test_decode_matches_float64(gpu, H, W):
 
 
 @pytest.mark.gpu
+def test_decode_subnormal_and_tiny_weights(gpu):
+    """the per-pixel power-of-two scaling before the f16 split
+    must stay finite when a pixel's largest weight is subnormal (or tiny):
+    such a pixel decodes to ~0 as the reference's einsum / (norm + 1e-10)
+    does, never to NaN/Inf; its neighbours are unaffected."""
+    g = np.random.default_rng(11)
+    L, K, Df, H, W = 3, 64, 512, 24, 40
+    wmap = (g.random((L * K, H, W)) * (g.random((L * K, H, W)) < 0.2)).astype(np.float32)
+    for (y, x), s in {(0, 0): 1e-40, (3, 5): 1e-44, (7, 9): 1e-30, (11, 20): 1e-20, (23, 39): 2e-38}.items():
+        wmap[:, y, x] = (wmap[:, y, x].astype(np.float64) * s).astype(np.float32)
+    cb = g.standard_normal((L, K, Df)).astype(np.float32)
+    got = quick.decode_language_features(torch.from_numpy(wmap).to(gpu), torch.from_numpy(cb).to(gpu)).cpu().numpy()
+    assert np.isfinite(got).all()
+    np.testing.assert_allclose(got, ref_decode(wmap, cb), atol=DEC_ATOL, rtol=0)
+
+
+@pytest.mark.gpu
 def test_unnormalised_and_dense_map(gpu):
     g = np.random.default_rng(7)
     wmap = g.random((64, 40, 56)).astype(np.float32)
