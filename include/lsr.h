@@ -102,7 +102,7 @@ typedef struct lsr_inputs {
  * the last pointer returned for a kind is the one the call uses. */
 typedef void* (*lsr_alloc_fn)(void* ctx, size_t bytes, int which);
 enum { LSR_BUF_GEOM = 0, LSR_BUF_BINNING = 1, LSR_BUF_IMAGE = 2, LSR_BUF_GRAD = 3, LSR_BUF_DECODE = 4,
-       LSR_BUF_KNN = 5, LSR_BUF_LOSS = 6, LSR_BUF_GUARD = 7, LSR_BUF_SPARSE = 8 };
+       LSR_BUF_KNN = 5, LSR_BUF_LOSS = 6, LSR_BUF_GUARD = 7, LSR_BUF_SPARSE = 8, LSR_BUF_GRAD_LANG = 9 };
 
 typedef struct lsr_fwd_out {
     float* out_color;     /* (3,H,W)  caller-allocated */
@@ -116,14 +116,16 @@ typedef struct lsr_fwd_out {
     /* Optional: the backward's accumulators, prepared by the forward.  In:
      * grad_ws_request = LSR_GWS_GEOM (the backward will request geometry /
      * colour gradients) | LSR_GWS_LANG (it will request dL_dlang).  The
-     * forward then allocates them (LSR_BUF_GRAD) and zeroes them inside the
-     * render kernel instead of the backward clearing them with memsets; out:
-     * grad_ws / grad_ws_bytes / grad_ws_kind, and grad_ws_lang_off = byte
-     * offset of an (N,D) dL/dlang accumulator inside grad_ws (SIZE_MAX: none).
+     * forward then allocates them and zeroes them inside the render kernel
+     * instead of the backward clearing them with memsets; out: grad_ws /
+     * grad_ws_bytes (the gradient rows, LSR_BUF_GRAD; NULL when only dL/dlang
+     * is requested), grad_ws_lang (an (N,D) dL/dlang accumulator in its OWN
+     * allocation, LSR_BUF_GRAD_LANG, so the gradient returned from it keeps
+     * nothing else alive; NULL: none) and grad_ws_kind.
      * Dense language path only (quick_render: nothing prepared). */
     int grad_ws_request;
     int grad_ws_kind;
-    void* grad_ws; size_t grad_ws_bytes; size_t grad_ws_lang_off;
+    void* grad_ws; size_t grad_ws_bytes; void* grad_ws_lang;
 } lsr_fwd_out;
 enum { LSR_GWS_GEOM = 1, LSR_GWS_LANG = 2 };
 
@@ -142,12 +144,13 @@ typedef struct lsr_bwd_in {
     const int32_t* radii;           /* (N,) from forward */
     const float* dL_dout_color;     /* (3,H,W) */
     const float* dL_dout_lang;      /* (D,H,W) or NULL */
-    /* Optional: lsr_fwd_out.grad_ws / _bytes / _kind of the same forward
-     * (zeroed accumulators; hand them to ONE backward).  Used when the kind
-     * matches what this call's requested outputs need (otherwise the call
-     * allocates and clears its own); dL_dlang == grad_ws + grad_ws_lang_off
-     * then needs no clearing either. */
+    /* Optional: lsr_fwd_out.grad_ws / _bytes / _kind / _lang of the same
+     * forward (zeroed accumulators; hand them to ONE backward).  Used when the
+     * kind matches what this call's requested outputs need (otherwise the call
+     * allocates and clears its own); dL_dlang == grad_ws_lang then needs no
+     * clearing either. */
     void* grad_ws; size_t grad_ws_bytes; int grad_ws_kind;
+    void* grad_ws_lang;
 } lsr_bwd_in;
 
 /* Gradient outputs; NULL = not requested (needs_input_grad False).  Every

@@ -571,15 +571,17 @@ static int wait_published(HostSlot& hs, uint32_t seq, hipStream_t st, uint64_t* 
     }
 }
 
-// The dense backward's accumulators (lsr_fwd_out.grad_ws): gradient rows
-// (P x VP, unless only dL/dlang is requested) and, where the render backward
-// adds dL/dlang straight into an (P, D) array (language-only, or D = 16 / 32
-// with aligned rows), that array.  kind encodes the configuration, so a
-// backward uses a forward's workspace only when it needs exactly this one.
+// The dense backward's accumulators (lsr_fwd_out.grad_ws / grad_ws_lang):
+// gradient rows (P x VP, unless only dL/dlang is requested) and, where the
+// render backward adds dL/dlang straight into an (P, D) array (language-only,
+// or D = 16 / 32 with aligned rows), that array -- a separate allocation, so
+// the gradient the caller keeps holds no gradient rows alive.  kind encodes
+// the configuration, so a backward uses a forward's accumulators only when it
+// needs exactly these.
 struct GradWs {
     int kind = 0;          // 0: nothing to prepare
     int VP = 0;
-    size_t lang_off = SIZE_MAX, total = 0;
+    size_t rows_bytes = 0, lang_bytes = 0;
     bool lang_only = false, lang_direct = false;
 };
 static GradWs grad_ws_layout(int P, int Dd, bool geom, bool lang, bool lang_aligned)
@@ -589,17 +591,10 @@ static GradWs grad_ws_layout(int P, int Dd, bool geom, bool lang, bool lang_alig
     if (P <= 0 || (!geom && !lang)) return w;
     w.lang_only = lang && !geom;
     w.lang_direct = lang && geom && bwd_lang_direct(Dd) && lang_aligned;
-    const size_t lang_bytes = (size_t)P * Dd * 4;
-    if (w.lang_only) {
-        w.lang_off = 0;
-        w.total = lang_bytes;
-    } else {
+    if (w.lang_only || w.lang_direct) w.lang_bytes = (size_t)P * Dd * 4;
+    if (!w.lang_only) {
         w.VP = w.lang_direct ? 16 : grad_row_width(Dd);
-        w.total = (size_t)P * w.VP * 4;
-        if (w.lang_direct) {
-            w.lang_off = (w.total + 255) / 256 * 256;
-            w.total = w.lang_off + lang_bytes;
-        }
+        w.rows_bytes = (size_t)P * w.VP * 4;
     }
     w.kind = (geom ? 1 : 0) | (lang ? 2 : 0) | (w.lang_direct ? 4 : 0) | (w.VP << 8);
     return w;
@@ -740,21 +735,30 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     out->grad_ws = nullptr;
     out->grad_ws_bytes = 0;
     out->grad_ws_kind = 0;
-    out->grad_ws_lang_off = SIZE_MAX;
+    out->grad_ws_lang = nullptr;
     if (out->grad_ws_request && !s->quick_render) {
         const GradWs w = grad_ws_layout(P, Dd, (out->grad_ws_request & LSR_GWS_GEOM) != 0,
                                         (out->grad_ws_request & LSR_GWS_LANG) != 0,
                                         (uintptr_t)in->language_feature_precomp % 16 == 0);
         if (w.kind) {
-            const size_t bytes = (w.total + 255) / 256 * 256;
-            void* ws = alloc(ctx, bytes, LSR_BUF_GRAD);
-            if (!ws) return LSR_ENOMEM;
-            out->grad_ws = ws;
-            out->grad_ws_bytes = w.total;
+            if (w.rows_bytes) {
+                const size_t bytes = (w.rows_bytes + 255) / 256 * 256;
+                void* ws = alloc(ctx, bytes, LSR_BUF_GRAD);
+                if (!ws) return LSR_ENOMEM;
+                out->grad_ws = ws;
+                out->grad_ws_bytes = w.rows_bytes;
+                ra.zero = (float4*)ws;
+                ra.zero_n16 = bytes / 16;
+            }
+            if (w.lang_bytes) {
+                const size_t bytes = (w.lang_bytes + 255) / 256 * 256;
+                void* wl = alloc(ctx, bytes, LSR_BUF_GRAD_LANG);
+                if (!wl) return LSR_ENOMEM;
+                out->grad_ws_lang = wl;
+                ra.zero2 = (float4*)wl;
+                ra.zero2_n16 = bytes / 16;
+            }
             out->grad_ws_kind = w.kind;
-            out->grad_ws_lang_off = w.lang_off;
-            ra.zero = (float4*)ws;
-            ra.zero_n16 = bytes / 16;
         }
     }
     { StageScope sc(ST_RENDER, st); LSR_HIP(launch_render_fwd(ra, st)); }
@@ -931,8 +935,9 @@ static int backward_dense(const lsr_settings* s, const lsr_inputs* in, const lsr
     // the forward's zeroed accumulators, when they are exactly what this call needs
     const GradWs W = grad_ws_layout(P, Dd, geometry_requested(out), out->dL_dlang != nullptr,
                                     (uintptr_t)in->language_feature_precomp % 16 == 0);
-    const bool ws_ok = b->grad_ws && W.kind != 0 && b->grad_ws_kind == W.kind && b->grad_ws_bytes >= W.total;
-    const bool ws_lang = ws_ok && W.lang_off != SIZE_MAX && out->dL_dlang == (float*)((uint8_t*)b->grad_ws + W.lang_off);
+    const bool ws_kind = W.kind != 0 && b->grad_ws_kind == W.kind;
+    const bool ws_ok = ws_kind && W.rows_bytes > 0 && b->grad_ws && b->grad_ws_bytes >= W.rows_bytes;
+    const bool ws_lang = ws_kind && W.lang_bytes > 0 && b->grad_ws_lang && out->dL_dlang == (float*)b->grad_ws_lang;
     if (lang_only) {
         RenderBwdArgs rb;
         rb.f = make_render_args(s, in, c, (const uint8_t*)b->geom, (const uint8_t*)b->binning,

@@ -77,6 +77,8 @@ struct RenderArgs {
     // the backward's accumulators, zeroed by the dense forward render (NULL: none)
     float4* zero = nullptr;
     size_t zero_n16 = 0;
+    float4* zero2 = nullptr;   // the (N, D) dL/dlang accumulator (its own allocation)
+    size_t zero2_n16 = 0;
 };
 hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st);
 

@@ -197,12 +197,18 @@ __device__ __forceinline__ int stage_candidates_p(WaveStageP<F4, fwd_sfeat<NL>()
 // the backward's two memset launches.
 __device__ __forceinline__ void zero_backward_accumulators(const RenderArgs& a)
 {
-    if (!a.zero) return;
     typedef float v4f __attribute__((ext_vector_type(4)));
-    v4f* const z = reinterpret_cast<v4f*>(a.zero);
     const size_t stride = (size_t)gridDim.x * 64;
-    for (size_t i = (size_t)blockIdx.x * 64 + threadIdx.x; i < a.zero_n16; i += stride)
-        __builtin_nontemporal_store(v4f{0.f, 0.f, 0.f, 0.f}, z + i);
+    if (a.zero) {
+        v4f* const z = reinterpret_cast<v4f*>(a.zero);
+        for (size_t i = (size_t)blockIdx.x * 64 + threadIdx.x; i < a.zero_n16; i += stride)
+            __builtin_nontemporal_store(v4f{0.f, 0.f, 0.f, 0.f}, z + i);
+    }
+    if (a.zero2) {
+        v4f* const z = reinterpret_cast<v4f*>(a.zero2);
+        for (size_t i = (size_t)blockIdx.x * 64 + threadIdx.x; i < a.zero2_n16; i += stride)
+            __builtin_nontemporal_store(v4f{0.f, 0.f, 0.f, 0.f}, z + i);
+    }
 }
 
 // ZERO: this launch also clears the backward's accumulators (a.zero set);
@@ -844,7 +850,7 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
         return hipGetLastError();
     }
     switch (lang_set_for(a.D)) {
-#define LSR_FWD_LAUNCH(K, NL) (a.zero ? K<NL, true><<<4 * T, 64, 0, st>>>(a) : K<NL, false><<<4 * T, 64, 0, st>>>(a))
+#define LSR_FWD_LAUNCH(K, NL) ((a.zero || a.zero2) ? K<NL, true><<<4 * T, 64, 0, st>>>(a) : K<NL, false><<<4 * T, 64, 0, st>>>(a))
         case 0: LSR_FWD_LAUNCH(k_render_fwd, 0); break;
         case 4: LSR_FWD_LAUNCH(k_render_fwd, 4); break;
         case 8: LSR_FWD_LAUNCH(k_render_fwd, 8); break;
@@ -853,10 +859,10 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
         case 16:
             if constexpr (fwd_sfeat<16>()) {
                 if (a.D == 16) {
-                    if (a.zero) k_render_fwd<16, true, true><<<4 * T, 64, 0, st>>>(a);
+                    if (a.zero || a.zero2) k_render_fwd<16, true, true><<<4 * T, 64, 0, st>>>(a);
                     else k_render_fwd<16, false, true><<<4 * T, 64, 0, st>>>(a);
                 } else {
-                    if (a.zero) k_render_fwd<16, true, true, true><<<4 * T, 64, 0, st>>>(a);
+                    if (a.zero || a.zero2) k_render_fwd<16, true, true, true><<<4 * T, 64, 0, st>>>(a);
                     else k_render_fwd<16, false, true, true><<<4 * T, 64, 0, st>>>(a);
                 }
             } else {
@@ -866,10 +872,10 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
         case 32:
             // D in (16, 32]: the ML form (cfg5 render_fwd 1.650 -> 1.266 ms against the VALU blend)
             if (a.D == 32) {
-                if (a.zero) k_render_fwd<32, true, true><<<4 * T, 64, 0, st>>>(a);
+                if (a.zero || a.zero2) k_render_fwd<32, true, true><<<4 * T, 64, 0, st>>>(a);
                 else k_render_fwd<32, false, true><<<4 * T, 64, 0, st>>>(a);
             } else {
-                if (a.zero) k_render_fwd<32, true, true, true><<<4 * T, 64, 0, st>>>(a);
+                if (a.zero || a.zero2) k_render_fwd<32, true, true, true><<<4 * T, 64, 0, st>>>(a);
                 else k_render_fwd<32, false, true, true><<<4 * T, 64, 0, st>>>(a);
             }
             break;
@@ -878,10 +884,10 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
             // earlier 16-candidate-group MFMA kernel at cfg3 geometry; the
             // VALU-only blend is slower still)
             if (a.D == 64) {
-                if (a.zero) k_render_fwd<64, true, true><<<4 * T, 64, 0, st>>>(a);
+                if (a.zero || a.zero2) k_render_fwd<64, true, true><<<4 * T, 64, 0, st>>>(a);
                 else k_render_fwd<64, false, true><<<4 * T, 64, 0, st>>>(a);
             } else {
-                if (a.zero) k_render_fwd<64, true, true, true><<<4 * T, 64, 0, st>>>(a);
+                if (a.zero || a.zero2) k_render_fwd<64, true, true, true><<<4 * T, 64, 0, st>>>(a);
                 else k_render_fwd<64, false, true, true><<<4 * T, 64, 0, st>>>(a);
             }
             break;

@@ -266,13 +266,15 @@ def _run_forward(means3D, sh, colors_precomp, language_feature_precomp, language
         _lib.check(rc, "rasterize_gaussians (forward)")
     saved = (means3D_c, opac_c, sh_c, col_c, sc_c, rot_c, cov_c, lang_c, qw_c, qi_c)
     grad_ws = None
-    if out.grad_ws:
-        grad_ws = (alloc.bufs[_lib.LSR_BUF_GRAD], int(out.grad_ws_bytes), int(out.grad_ws_kind),
-                   int(out.grad_ws_lang_off))
+    if out.grad_ws_kind:
+        # (rows or None, rows bytes, kind, (N, D) dL/dlang accumulator or None): the
+        # accumulator is its own allocation (LSR_BUF_GRAD_LANG), so the gradient handed
+        # to autograd from it keeps no gradient rows alive
+        grad_ws = (alloc.bufs.get(_lib.LSR_BUF_GRAD) if out.grad_ws else None, int(out.grad_ws_bytes),
+                   int(out.grad_ws_kind), alloc.bufs.get(_lib.LSR_BUF_GRAD_LANG) if out.grad_ws_lang else None)
     return color, lang_out, radii, int(out.num_rendered), alloc.bufs, saved, (N, M, D, K), grad_ws
 
 
-_SIZE_MAX = ctypes.c_size_t(-1).value
 _CALL = threading.local()   # grad mode at the rasterize_gaussians call (see _grad_request)
 
 
@@ -346,7 +348,9 @@ class _RasterizeGaussians(torch.autograd.Function):
         ws = ctx.grad_ws
         ctx.grad_ws = None   # a second backward (retain_graph) clears its own
         if ws is not None:
-            bin_.grad_ws, bin_.grad_ws_bytes, bin_.grad_ws_kind = ws[0].data_ptr(), ws[1], ws[2]
+            bin_.grad_ws = ws[0].data_ptr() if ws[0] is not None else None
+            bin_.grad_ws_bytes, bin_.grad_ws_kind = ws[1], ws[2]
+            bin_.grad_ws_lang = ws[3].data_ptr() if ws[3] is not None else None
         sink = _sink()
 
         def mk(name, shape, flag):
@@ -369,9 +373,9 @@ class _RasterizeGaussians(torch.autograd.Function):
         if lang is not None and need[4]:
             if sink is not None:
                 g_lang = sink.take("language_feature_precomp", (N, D), dev, ctx.input_ids["language_feature_precomp"])
-            if g_lang is None and ws is not None and ws[3] != _SIZE_MAX:
+            if g_lang is None and ws is not None and ws[3] is not None:
                 # the forward's zeroed (N, D) accumulator: the library adds into it in place
-                g_lang = ws[0][ws[3]:ws[3] + N * D * 4].view(torch.float32).view(N, D)
+                g_lang = ws[3][:N * D * 4].view(torch.float32).view(N, D)
             if g_lang is None:
                 g_lang = torch.empty((N, D), dtype=torch.float32, device=dev)
         g_qw = mk("language_feature_weights_quick", (N, K), need[5]) if (quick and qw is not None) else None
