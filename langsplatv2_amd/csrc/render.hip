@@ -816,6 +816,266 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
         }
     }
 }
+
+// Quick path with the chunk records prefetched by LDS-DMA (default when the
+// sparse rows allow 16-B copies: K % 4 == 0, 16-B aligned weights/indices).
+// k_render_fwd_quick_v gathers each chunk's records, rgb, 12 weights and 12
+// indices into VGPRs when it reaches the chunk, so every chunk waits for two
+// dependent global round trips, and at 2 waves/SIMD (the 192 accumulators take
+// the register file) nothing hides them (r03 PMC: waves parked in s_waitcnt
+// 59 % of their cycles).  Here the NEXT chunk's raw rows are copied straight
+// into a per-wave LDS buffer by global_load_lds (no VGPR destination, ids
+// loaded two chunks ahead) while the current chunk blends; staging then reads
+// LDS.  Blend, accumulation and outputs are k_render_fwd_quick_v's, bit for bit.
+template <int QB>
+struct WaveRawQ {
+    float4 A[64];
+    float4 B[64];
+    float rgb[64 * 3];                  // 12-B DMA: lane l at 12 l
+    float4 W[3][64];                    // weight row part p (4 weights) of lane l
+    uint4 Q[3 * QB / 4][64];            // index row bytes [16 p, 16 p + 16) of lane l
+};
+
+template <int DT>
+__device__ __forceinline__ int quick_code_raw(const WaveRawQ<DT == 2 ? 8 : 4>& raw, int lane, int k)
+{
+    if constexpr (DT == 2) {
+        const uint4 q = raw.Q[k >> 1][lane];
+        const uint32_t lo = (k & 1) ? q.z : q.x, hi = (k & 1) ? q.w : q.y;
+        return hi != 0u || lo > 0x7fffffffu ? -1 : (int)lo;
+    } else {
+        const uint4 q = raw.Q[k >> 2][lane];
+        const uint32_t v = (k & 3) == 0 ? q.x : (k & 3) == 1 ? q.y : (k & 3) == 2 ? q.z : q.w;
+        return DT == 0 ? f2i(__uint_as_float(v) + 0.5f) : (int)v;
+    }
+}
+
+// One chunk's rows -> raw by LDS-DMA (K = 12 codes per Gaussian): lane l's
+// record, rgb, weight row and index row land at slot l of each array (an LDS-
+// DMA writes wave-uniform M0 + lane x size).  One asm block walks M0 through
+// the arrays (raw's layout is fixed by the static_asserts below); the weight
+// and index row parts are the immediate offsets of one address each.  (The
+// __builtin_amdgcn_global_load_lds form crashes ROCm 7.2's SIFixSGPRCopies in
+// this kernel, and per-call M0 constants spilled SGPRs.)  The caller waits with
+// s_waitcnt vmcnt before reading raw.
+#define LSR_GLDS(step, insn) "s_add_u32 m0, m0, " #step "\n\ts_nop 0\n\t" insn "\n\t"
+template <int QB>
+__device__ __forceinline__ void quick_dma12(WaveRawQ<QB>& raw, const RenderArgs& a, uint32_t g)
+{
+    static_assert(offsetof(WaveRawQ<QB>, B) == 1024 && offsetof(WaveRawQ<QB>, rgb) == 2048 &&
+                  offsetof(WaveRawQ<QB>, W) == 2816 && offsetof(WaveRawQ<QB>, Q) == 5888, "raw layout");
+    const uint32_t base = (uint32_t)(uintptr_t)&raw;   // the LDS byte address (low half of the flat address)
+    const float4* pA = a.splatA + g;
+    const float4* pB = a.splatB + g;
+    const float* pR = a.rgb + 3 * (size_t)g;
+    const float* pW = a.qw + 12 * (size_t)g;
+    const char* pQ = reinterpret_cast<const char*>(a.qi) + (size_t)g * (12 * QB);
+    uint32_t keep;
+    if constexpr (QB == 4) {
+        asm volatile("s_mov_b32 %[keep], m0\n\t"
+                     "s_mov_b32 m0, %[base]\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[pA], off\n\t"
+                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pB], off")
+                     LSR_GLDS(1024, "global_load_lds_dwordx3 %[pR], off")
+                     LSR_GLDS(768, "global_load_lds_dwordx4 %[pW], off")
+                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pW], off offset:16")
+                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pW], off offset:32")
+                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off")
+                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off offset:16")
+                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off offset:32")
+                     "s_mov_b32 m0, %[keep]"
+                     : [keep] "=&s"(keep)
+                     : [base] "s"(base), [pA] "v"(pA), [pB] "v"(pB), [pR] "v"(pR), [pW] "v"(pW), [pQ] "v"(pQ)
+                     : "memory", "scc");
+    } else {
+        asm volatile("s_mov_b32 %[keep], m0\n\t"
+                     "s_mov_b32 m0, %[base]\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[pA], off\n\t"
+                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pB], off")
+                     LSR_GLDS(1024, "global_load_lds_dwordx3 %[pR], off")
+                     LSR_GLDS(768, "global_load_lds_dwordx4 %[pW], off")
+                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pW], off offset:16")
+                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pW], off offset:32")
+                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off")
+                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off offset:16")
+                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off offset:32")
+                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off offset:48")
+                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off offset:64")
+                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off offset:80")
+                     "s_mov_b32 m0, %[keep]"
+                     : [keep] "=&s"(keep)
+                     : [base] "s"(base), [pA] "v"(pA), [pB] "v"(pB), [pR] "v"(pR), [pW] "v"(pW), [pQ] "v"(pQ)
+                     : "memory", "scc");
+    }
+}
+#undef LSR_GLDS
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"   // the v255 clobber is the point: it sizes the allocation
+template <int DT>
+__global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_render_fwd_quick_d(RenderArgs a)
+{
+    constexpr int QB = DT == 2 ? 8 : 4;
+    __shared__ WaveStageV st;
+    __shared__ WaveRawQ<QB> raw;
+    const Cam& c = a.cam;
+    const WaveTile wt(a);
+    const int lane = threadIdx.x;
+    const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
+    const bool inside = pm.px < c.W && pm.py < c.H;
+    const float pfx = (float)pm.px, pfy = (float)pm.py;
+    const uint32_t rs = a.tile_start[wt.tile], re = a.tile_start[wt.tile + 1];
+    const int Dq = a.Dq;
+
+    {   // zero v63 (junk) .. v255 (accumulators)
+        uint32_t i, sv;
+        asm volatile(
+            "s_mov_b32 %[sv], m0\n\t"
+            "s_mov_b32 %[i], 0\n\t"
+            "s_set_gpr_idx_on 0, gpr_idx(DST)\n\t"
+            "1:\n\t"
+            "s_set_gpr_idx_idx %[i]\n\t"
+            "s_nop 0\n\t"
+            "v_mov_b32 v63, 0\n\t"
+            "s_add_u32 %[i], %[i], 1\n\t"
+            "s_cmp_lt_u32 %[i], 193\n\t"
+            "s_cbranch_scc1 1b\n\t"
+            "s_set_gpr_idx_off\n\t"
+            "s_mov_b32 m0, %[sv]"
+            : [i] "=&s"(i), [sv] "=&s"(sv)
+            :
+            : "scc", "v63", "v255", "memory");
+    }
+    float T = 1.0f, cr = 0.f, cg = 0.f, cbl = 0.f;
+    uint32_t last = 0;
+    bool done = !inside;
+    // ids two chunks ahead; positions past the list read gid 0 (a valid row, never staged)
+    uint32_t gid_n = (rs + 64 + lane < re) ? a.point_list[rs + 64 + lane] : 0u;
+    if (rs < re) quick_dma12<QB>(raw, a, (rs + lane < re) ? a.point_list[rs + lane] : 0u);
+    for (uint32_t base = rs; base < re; base += 64) {
+        if (wave_ballot(!done) == 0) break;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this chunk's rows have landed in raw
+        const uint32_t idx = base + lane;
+        const bool valid = idx < re;
+        const float4 A = raw.A[lane], B = raw.B[lane];
+        const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), pm.bx, pm.by) &&
+                        block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, pm.bx, pm.by);
+        const uint64_t m = wave_ballot(ok);
+        if (ok) {
+            const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            st.A[r] = A;
+            st.B[r] = make_float4(B.x, B.y, B.z, __int_as_float((int)(idx - rs) + 1));
+            st.C[r] = make_float4(raw.rgb[3 * lane], raw.rgb[3 * lane + 1], raw.rgb[3 * lane + 2], 0.f);
+            st.Wt[r][0] = raw.W[0][lane];
+            st.Wt[r][1] = raw.W[1][lane];
+            st.Wt[r][2] = raw.W[2][lane];
+            uint32_t qv[3] = {0u, 0u, 0u};   // register index q + 1 per code; 0 = the junk register
+#pragma unroll
+            for (int k = 0; k < 12; k++) {   // K = 12 (quick_dma_ok)
+                const int q = quick_code_raw<DT>(raw, lane, k);
+                const uint32_t qb = (q >= 0 && q < Dq) ? (uint32_t)(q + 1) : 0u;
+                qv[k >> 2] |= qb << (8 * (k & 3));
+            }
+            st.Q[r] = make_uint4(qv[0], qv[1], qv[2], 0u);
+        }
+        wave_lds_fence();   // raw read, stage written: raw may be refilled
+        if (base + 64 < re) quick_dma12<QB>(raw, a, gid_n);
+        {
+            const uint32_t q = min(idx + 128, re - 1);   // re > base: a valid position
+            const uint32_t v = a.point_list[q];
+            gid_n = idx + 128 < re ? v : 0u;
+        }
+        const int n = __popcll(m);
+        // the blend of k_render_fwd_quick_v, unchanged
+        for (int j0 = 0; j0 < n; j0 += 2) {
+            if (wave_ballot(!done) == 0) break;
+            const bool two = j0 + 1 < n;
+            const int j1 = two ? j0 + 1 : j0;
+            const float4 A0 = st.A[j0], B0 = st.B[j0];
+            const float4 A1 = st.A[j1], B1 = st.B[j1];
+            const float p0 = splat_power(A0.z, A0.w, B0.x, A0.x - pfx, A0.y - pfy);
+            const float p1 = splat_power(A1.z, A1.w, B1.x, A1.x - pfx, A1.y - pfy);
+            bool ok0 = !done && !(p0 > 0.0f || p0 < B0.z);
+            bool ok1 = two && !done && !(p1 > 0.0f || p1 < B1.z);
+            if (!wave_any(ok0 || ok1)) continue;
+            const f32x2 EX = expf_det2(f32x2{p0, p1});
+            const float al0 = fminf(0.99f, B0.y * EX.x);
+            const float al1 = fminf(0.99f, B1.y * EX.y);
+            ok0 = ok0 && !(al0 < 1.0f / 255.0f);
+            ok1 = ok1 && !(al1 < 1.0f / 255.0f);
+            float aT0, aT1;
+            {
+                const float test_T = T * (1.0f - al0);
+                const bool term = ok0 && (test_T < 0.0001f);
+                done = done || term;
+                ok0 = ok0 && !term;
+                ok1 = ok1 && !term;
+                aT0 = ok0 ? al0 * T : 0.f;
+                if (ok0) {
+                    const float4 C0 = st.C[j0];
+                    cr = fmaf(C0.x, aT0, cr);
+                    cg = fmaf(C0.y, aT0, cg);
+                    cbl = fmaf(C0.z, aT0, cbl);
+                    T = test_T;
+                    last = (uint32_t)__float_as_int(B0.w);
+                }
+            }
+            {
+                const float test_T = T * (1.0f - al1);
+                const bool term = ok1 && (test_T < 0.0001f);
+                done = done || term;
+                ok1 = ok1 && !term;
+                aT1 = ok1 ? al1 * T : 0.f;
+                if (ok1) {
+                    const float4 C1 = st.C[j1];
+                    cr = fmaf(C1.x, aT1, cr);
+                    cg = fmaf(C1.y, aT1, cg);
+                    cbl = fmaf(C1.z, aT1, cbl);
+                    T = test_T;
+                    last = (uint32_t)__float_as_int(B1.w);
+                }
+            }
+            if (wave_any(ok0)) LSR_QV_UPDATE(aT0, st.Q[j0], st.Wt[j0][0], st.Wt[j0][1], st.Wt[j0][2]);
+            if (wave_any(ok1)) LSR_QV_UPDATE(aT1, st.Q[j1], st.Wt[j1][0], st.Wt[j1][1], st.Wt[j1][2]);
+        }
+        wave_lds_fence();
+    }
+    // no LDS-DMA may land after the wave (and its LDS) is gone
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const size_t HW = (size_t)c.H * c.W;
+    if (inside) {
+        const size_t pix = (size_t)pm.py * c.W + pm.px;
+        a.final_T[pix] = T;
+        a.n_contrib[pix] = last;
+        a.out_color[pix] = fmaf(T, c.bg[0], cr);
+        a.out_color[HW + pix] = fmaf(T, c.bg[1], cg);
+        a.out_color[2 * HW + pix] = fmaf(T, c.bg[2], cbl);
+        float* const o = a.out_lang + pix;
+        for (int q = 0; q < Dq; q++) {
+            float v;
+            uint32_t sv;
+            asm volatile(
+                "s_mov_b32 %[sv], m0\n\t"
+                "s_set_gpr_idx_on %[q], gpr_idx(SRC0)\n\t"
+                "s_nop 0\n\t"
+                "v_mov_b32 %[v], v64\n\t"
+                "s_set_gpr_idx_off\n\t"
+                "s_mov_b32 m0, %[sv]"
+                : [v] "=v"(v), [sv] "=&s"(sv)
+                : [q] "s"(q)
+                : "memory");
+            o[(size_t)q * HW] = v;
+        }
+    }
+}
+#pragma clang diagnostic pop
+
+// the LDS-DMA quick kernel applies: 12 codes per Gaussian (3 levels x top-4), 16-B aligned rows
+static bool quick_dma_ok(const RenderArgs& a)
+{
+    const int qb = a.qidx_dtype == LSR_INDEX_I64 ? 8 : 4;
+    return a.K == 12 && a.Dq <= 192 && ((uintptr_t)a.qw % 16) == 0 && ((uintptr_t)a.qi % 16) == 0 &&
+           ((uintptr_t)a.rgb % 4) == 0 && qb > 0;
+}
+
 #pragma clang diagnostic pop
 
 int lang_set_for(int D)
@@ -834,6 +1094,14 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
     const int T = a.cam.gx * a.cam.gy;
     if (T == 0) return hipSuccess;
     if (a.qw) {
+        if (quick_dma_ok(a)) {
+            switch (a.qidx_dtype) {
+                case LSR_INDEX_F32: k_render_fwd_quick_d<0><<<T * 4, 64, 0, st>>>(a); break;
+                case LSR_INDEX_I32: k_render_fwd_quick_d<1><<<T * 4, 64, 0, st>>>(a); break;
+                default: k_render_fwd_quick_d<2><<<T * 4, 64, 0, st>>>(a); break;
+            }
+            return hipGetLastError();
+        }
         if (a.K <= 12 && a.Dq <= 192) {
             switch ((a.Dq + 31) / 32) {
                 case 1: k_render_fwd_quick_v<1><<<T * 4, 64, 0, st>>>(a); break;
