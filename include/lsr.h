@@ -102,7 +102,8 @@ typedef struct lsr_inputs {
  * the last pointer returned for a kind is the one the call uses. */
 typedef void* (*lsr_alloc_fn)(void* ctx, size_t bytes, int which);
 enum { LSR_BUF_GEOM = 0, LSR_BUF_BINNING = 1, LSR_BUF_IMAGE = 2, LSR_BUF_GRAD = 3, LSR_BUF_DECODE = 4,
-       LSR_BUF_KNN = 5, LSR_BUF_LOSS = 6, LSR_BUF_GUARD = 7, LSR_BUF_SPARSE = 8, LSR_BUF_GRAD_LANG = 9 };
+       LSR_BUF_KNN = 5, LSR_BUF_LOSS = 6, LSR_BUF_GUARD = 7, LSR_BUF_SPARSE = 8, LSR_BUF_GRAD_LANG = 9,
+       LSR_BUF_LISTS = 10 };
 
 typedef struct lsr_fwd_out {
     float* out_color;     /* (3,H,W)  caller-allocated */
@@ -126,6 +127,11 @@ typedef struct lsr_fwd_out {
     int grad_ws_request;
     int grad_ws_kind;
     void* grad_ws; size_t grad_ws_bytes; void* grad_ws_lang;
+    /* With grad_ws_request set (dense path), also: each 8x8 block's candidate
+     * list for the backward (LSR_BUF_LISTS; NULL when not prepared), written by
+     * the render: pass it in lsr_bwd_in.lists to let the backward read its
+     * candidates instead of re-staging them from the tile lists. */
+    void* lists; size_t lists_bytes;
 } lsr_fwd_out;
 enum { LSR_GWS_GEOM = 1, LSR_GWS_LANG = 2 };
 
@@ -151,6 +157,9 @@ typedef struct lsr_bwd_in {
      * clearing either. */
     void* grad_ws; size_t grad_ws_bytes; int grad_ws_kind;
     void* grad_ws_lang;
+    /* Optional: lsr_fwd_out.lists of the same forward (read only; any number of
+     * backwards over that forward may use it). */
+    const void* lists;
 } lsr_bwd_in;
 
 /* Gradient outputs; NULL = not requested (needs_input_grad False).  Every

@@ -17,7 +17,7 @@ LSR_OK = 0
 LSR_ENONFINITE = 6
 LSR_ELISTS = 7
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_GRAD, LSR_BUF_DECODE, LSR_BUF_KNN, LSR_BUF_LOSS = 0, 1, 2, 3, 4, 5, 6
-LSR_BUF_GUARD, LSR_BUF_SPARSE, LSR_BUF_GRAD_LANG = 7, 8, 9
+LSR_BUF_GUARD, LSR_BUF_SPARSE, LSR_BUF_GRAD_LANG, LSR_BUF_LISTS = 7, 8, 9, 10
 LSR_INDEX_F32, LSR_INDEX_I32, LSR_INDEX_I64 = 0, 1, 2
 LSR_GWS_GEOM, LSR_GWS_LANG = 1, 2
 
@@ -81,6 +81,8 @@ class FwdOut(ctypes.Structure):
         ("grad_ws", _vp),
         ("grad_ws_bytes", ctypes.c_size_t),
         ("grad_ws_lang", _vp),
+        ("lists", _vp),
+        ("lists_bytes", ctypes.c_size_t),
     ]
 
 
@@ -97,6 +99,7 @@ class BwdIn(ctypes.Structure):
         ("grad_ws_bytes", ctypes.c_size_t),
         ("grad_ws_kind", ctypes.c_int),
         ("grad_ws_lang", _vp),
+        ("lists", _vp),
     ]
 
 

@@ -600,6 +600,22 @@ static GradWs grad_ws_layout(int P, int Dd, bool geom, bool lang, bool lang_alig
     return w;
 }
 
+// The backward's per-block candidate lists (RenderArgs::listA/B/lcount): A and
+// B arrays of 4 M entries (block b = 4 tile + sub owns [4 tile_start + sub n_tile,
+// + n_tile)), then the 4 T per-block counts.
+static size_t block_lists_bytes(size_t M, size_t T)
+{
+    if (M == 0 || T == 0) return 0;
+    return 2 * align256(4 * M * 16) + align256(4 * T * 4);
+}
+static void set_block_lists(RenderArgs& ra, void* lb, size_t M)
+{
+    uint8_t* p = (uint8_t*)lb;
+    ra.listA = (float4*)p;
+    ra.listB = (float4*)(p + align256(4 * M * 16));
+    ra.lcount = (uint32_t*)(p + 2 * align256(4 * M * 16));
+}
+
 int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, lsr_alloc_fn alloc, void* ctx,
                 void* stream)
 {
@@ -736,6 +752,8 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     out->grad_ws_bytes = 0;
     out->grad_ws_kind = 0;
     out->grad_ws_lang = nullptr;
+    out->lists = nullptr;
+    out->lists_bytes = 0;
     if (out->grad_ws_request && !s->quick_render) {
         const GradWs w = grad_ws_layout(P, Dd, (out->grad_ws_request & LSR_GWS_GEOM) != 0,
                                         (out->grad_ws_request & LSR_GWS_LANG) != 0,
@@ -759,6 +777,16 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
                 ra.zero2_n16 = bytes / 16;
             }
             out->grad_ws_kind = w.kind;
+            // the backward's per-block candidate lists (render.hip LST): the render
+            // writes each 8x8 block's staged candidates; capacity 4 entries per instance
+            const size_t L = block_lists_bytes((size_t)M, (size_t)T);
+            if (L) {
+                void* lb = alloc(ctx, L, LSR_BUF_LISTS);
+                if (!lb) return LSR_ENOMEM;
+                out->lists = lb;
+                out->lists_bytes = L;
+                set_block_lists(ra, lb, (size_t)M);
+            }
         }
     }
     { StageScope sc(ST_RENDER, st); LSR_HIP(launch_render_fwd(ra, st)); }
@@ -942,6 +970,7 @@ static int backward_dense(const lsr_settings* s, const lsr_inputs* in, const lsr
         RenderBwdArgs rb;
         rb.f = make_render_args(s, in, c, (const uint8_t*)b->geom, (const uint8_t*)b->binning,
                                 (const uint8_t*)b->image, b->num_rendered);
+        if (b->lists) set_block_lists(rb.f, (void*)b->lists, (size_t)b->num_rendered);
         rb.f.qw = nullptr;
         rb.f.D = Dd;
         rb.f.lang = in->language_feature_precomp;
@@ -974,6 +1003,7 @@ static int backward_dense(const lsr_settings* s, const lsr_inputs* in, const lsr
     RenderBwdArgs rb;
     rb.f = make_render_args(s, in, c, (const uint8_t*)b->geom, (const uint8_t*)b->binning, (const uint8_t*)b->image,
                             b->num_rendered);
+    if (b->lists) set_block_lists(rb.f, (void*)b->lists, (size_t)b->num_rendered);
     rb.f.qw = nullptr;
     rb.f.D = Dd;
     rb.f.lang = Dd ? in->language_feature_precomp : nullptr;

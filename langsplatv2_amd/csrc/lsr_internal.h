@@ -79,6 +79,13 @@ struct RenderArgs {
     size_t zero_n16 = 0;
     float4* zero2 = nullptr;   // the (N, D) dL/dlang accumulator (its own allocation)
     size_t zero2_n16 = 0;
+    // per-8x8-block candidate lists for the backward (lsr_fwd_out.lists; NULL: none).
+    // Block b = 4 tile + sub owns entries [4 tile_start[tile] + sub n_tile, + n_tile)
+    // of listA / listB (n_tile = the tile's instance count); lcount[b] = its entries
+    // below the block's largest n_contrib (an over-count is harmless)
+    float4* listA = nullptr;   // the candidate's splat record A {x, y, conic.a, conic.b}
+    float4* listB = nullptr;   // {conic.c, opacity, id bits, 0-based tile-list position bits}
+    uint32_t* lcount = nullptr;
 };
 hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st);
 

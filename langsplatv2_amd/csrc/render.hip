@@ -28,6 +28,8 @@
 // added with line-coalesced buffer atomics (see the comment at the kernel).
 #include "lsr_internal.h"
 
+#include <type_traits>
+
 #ifndef LSR_BWD_SPLAT_PF
 #define LSR_BWD_SPLAT_PF 1  // bwd: chunk records loaded one chunk ahead (ids two ahead), D <= 32
 #endif
@@ -146,18 +148,35 @@ struct WaveStageP {
                        // the positions themselves, so 6 instead of 5 waves/SIMD at D = 16
 };
 
-template <int NL, int F4>
+// The backward's per-block candidate list (RenderArgs::listA/B): with LST the
+// staged candidates are also written to list entries [lpos, lpos + cnt) in
+// staging order (increasing tile-list position), B as {conic.c, opacity, id,
+// 0-based position}; *mo receives the chunk's staging mask.
+struct ListSink {
+    float4* A = nullptr;
+    float4* B = nullptr;
+    uint32_t pos = 0;
+};
+
+template <int NL, int F4, bool LST = false>
 __device__ __forceinline__ int stage_candidates_p_rec(WaveStageP<F4, fwd_sfeat<NL>()>& st, bool valid, uint32_t gid,
                                                       int pos, int bx, int by, float4 A, float4 B,
                                                       const float* __restrict__ rgb, const float* __restrict__ lang,
-                                                      int D)
+                                                      int D, const ListSink& ls = ListSink(), uint64_t* mo = nullptr)
 {
     const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by) &&
                     block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, bx, by);
     const uint64_t m = wave_ballot(ok);
     const int cnt = __popcll(m);
+    if constexpr (LST) *mo = m;
     if (ok) {
         const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if constexpr (LST) {
+            if (ls.A) {
+                ls.A[ls.pos + r] = A;
+                ls.B[ls.pos + r] = make_float4(B.x, B.y, __uint_as_float(gid), __int_as_float(pos - 1));
+            }
+        }
         float* base = reinterpret_cast<float*>(&st) + (r & 1);
         const int e = (r >> 1) * 2;
         base[0 * 64 + e] = A.x;
@@ -177,18 +196,19 @@ __device__ __forceinline__ int stage_candidates_p_rec(WaveStageP<F4, fwd_sfeat<N
     return cnt;
 }
 
-template <int NL, int F4>
+template <int NL, int F4, bool LST = false>
 __device__ __forceinline__ int stage_candidates_p(WaveStageP<F4, fwd_sfeat<NL>()>& st, bool valid, uint32_t gid, int pos, int bx,
                                                   int by, const float4* __restrict__ splatA,
                                                   const float4* __restrict__ splatB, const float* __restrict__ rgb,
-                                                  const float* __restrict__ lang, int D)
+                                                  const float* __restrict__ lang, int D, const ListSink& ls = ListSink(),
+                                                  uint64_t* mo = nullptr)
 {
     float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
     if (valid) {
         A = splatA[gid];
         B = splatB[gid];
     }
-    return stage_candidates_p_rec<NL, F4>(st, valid, gid, pos, bx, by, A, B, rgb, lang, D);
+    return stage_candidates_p_rec<NL, F4, LST>(st, valid, gid, pos, bx, by, A, B, rgb, lang, D, ls, mo);
 }
 
 // The backward's accumulators (RenderArgs::zero; lsr_fwd_out.grad_ws): a
@@ -262,6 +282,18 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
         for (int pb = 0; pb < 4; pb++) mlacc[nb][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
     uint32_t last = 0;
 
+    // ZERO (a backward is pending): the staged candidates also go to this
+    // block's list for the backward (RenderArgs::listA), nst entries so far;
+    // (mlast, nlast, blast): the last chunk's mask, entries before it, its start
+    ListSink ls;
+    uint32_t nst = 0, nlast = 0, blast = rs;
+    uint64_t mlast = 0;
+    if constexpr (ZERO) {
+        if (a.listA) {
+            ls.A = a.listA + (size_t)4 * rs + (size_t)wt.sub * (re - rs);
+            ls.B = a.listB + (size_t)4 * rs + (size_t)wt.sub * (re - rs);
+        }
+    }
     uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
     // SPF: a chunk's ids are loaded two chunks ahead and its records one chunk
     // ahead, issued after the current chunk's feature loads: the staging then
@@ -282,10 +314,12 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
         const bool valid = idx < re;
         const uint32_t gid = next_gid;
         int n;
+        uint64_t mchunk = 0;
+        ls.pos = nst;
         if constexpr (FSPF) {
             const float4 Ac = A1, Bc = B1;
-            n = stage_candidates_p_rec<NL, F4>(st, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, Ac, Bc, a.rgb,
-                                               a.lang, D);
+            n = stage_candidates_p_rec<NL, F4, ZERO>(st, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, Ac, Bc, a.rgb,
+                                                     a.lang, D, ls, &mchunk);
             next_gid = next_gid2;
             A1 = a.splatA[next_gid];
             B1 = a.splatB[next_gid];
@@ -294,8 +328,14 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
             next_gid2 = idx + 128 < re ? v : 0u;
         } else {
             next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;
-            n = stage_candidates_p<NL, F4>(st, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, a.splatA, a.splatB,
-                                           a.rgb, a.lang, D);
+            n = stage_candidates_p<NL, F4, ZERO>(st, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, a.splatA,
+                                                 a.splatB, a.rgb, a.lang, D, ls, &mchunk);
+        }
+        if constexpr (ZERO) {
+            mlast = mchunk;
+            nlast = nst;
+            blast = base;
+            nst += (uint32_t)n;
         }
         // Two instances per iteration, branch-free per lane: a lane that
         // skips an instance (exponent cut, alpha < 1/255, saturated or done)
@@ -468,6 +508,19 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
         }
         if (lastj >= 0) last = (uint32_t)(base - rs) + 1u + st.src[lastj];
         wave_lds_fence();
+    }
+    if constexpr (ZERO) {
+        if (a.listA) {
+            // entries the backward needs: 0-based position < wmax (the block's largest
+            // n_contrib).  Exact when wmax falls in the last staged chunk (the usual
+            // case); otherwise every entry before that chunk (the extra ones have
+            // position >= every pixel's n_contrib: the backward evaluates them to 0)
+            const int wmax = wave_max_i(inside ? (int)last : 0);
+            const int off = wmax - (int)(blast - rs);
+            uint32_t cnt = nlast;
+            if (off > 0) cnt += (uint32_t)__popcll(off >= 64 ? mlast : (mlast & ((1ull << off) - 1ull)));
+            if (lane == 0) a.lcount[4 * wt.tile + wt.sub] = cnt;
+        }
     }
     if (inside) {
         const size_t HW = (size_t)c.H * c.W;
@@ -1239,6 +1292,36 @@ struct WaveStageG {
     uint32_t gid[80];
 };
 
+// LST: the block's candidate list (written by the forward, RenderArgs::listA/B)
+// copied into LDS by LDS-DMA, 64 entries per chunk, two buffers (the next
+// chunk lands while this one is processed).  B = {conic.c, opacity, id bits,
+// 0-based position bits}.
+struct WaveStageL {
+    float4 A[128];
+    float4 B[128];
+};
+
+// LDS-DMA of one 16-B row part per lane: lane l's bytes land at lds + 16 l (an
+// LDS-DMA writes wave-uniform M0 + lane x size).  Inline asm with M0 saved and
+// restored (the builtin form crashed ROCm 7.2's SIFixSGPRCopies in the quick
+// kernel); the caller waits with s_waitcnt vmcnt before reading lds.
+__device__ __forceinline__ void glds16(const void* g, const void* lds)
+{
+    const uint32_t l = (uint32_t)(uintptr_t)lds;   // the LDS byte address (low half of the flat address)
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(l) : "memory");
+}
+
+// s_waitcnt vmcnt(N) only (gfx9 encoding: vmcnt[3:0] bits 3:0, [5:4] bits 15:14;
+// expcnt and lgkmcnt at their maxima)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt()
+{
+    static_assert(N >= 0 && N <= 63, "vmcnt is 6 bits");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");   // also a compiler barrier for the LDS reads after it
+}
+
 // Appends this chunk's candidates after the `carry` entries already staged.
 __device__ __forceinline__ int stage_candidates_geo(WaveStageG& st, int carry, bool valid, uint32_t gid, int pos,
                                                     int bx, int by, const float4* __restrict__ splatA,
@@ -1358,9 +1441,14 @@ __device__ unsigned long long g_bwd_stamps[16];
 // SP (with LO): the language input is the quick path's sparse (weights,
 // codes) rows; the per-channel gradient rows are gathered at each Gaussian's
 // codes into dL/dweights (b.qw_acc, (P, K)) instead of being added densely.
-template <int NL, bool LO = false, bool LD = false, bool SP = false>
+// LST: the candidates come from the forward's per-block list (RenderArgs::listA,
+// lcount) instead of being re-staged from the tile list: no ids -> records
+// gathers, no block tests, no compaction; the list chunks arrive by LDS-DMA one
+// chunk ahead.  The same candidates in the same order: results unchanged.
+template <int NL, bool LO = false, bool LD = false, bool SP = false, bool LST = false>
 __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArgs b)
 {
+    static_assert(!(LST && SP), "the sparse-input backward follows the quick forward (no lists)");
     static_assert(!LO || NL > 0, "language-only backward needs D > 0");
     static_assert(!SP || LO, "the sparse-input gradient is a language-only backward");
     static_assert(!LD || (!LO && NL % 16 == 0), "direct dL/dlang needs whole 16-channel lines");
@@ -1381,7 +1469,10 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     __shared__ float2 sRG[64];        // dL/dout R, G of the block's pixels
     __shared__ float sBc[64];         // dL/dout B
     constexpr int GS = LSR_GRP_STRIDE;
-    __shared__ WaveStageG st;
+    // the stage: re-staged tile-list candidates (!LST) or two list chunks (LST)
+    __shared__ std::conditional_t<LST, WaveStageL, WaveStageG> stv;
+    auto& st = stv;    // !LST
+    auto& stl = stv;   // LST
     // first language column of a staged row; LD: the language lines start at
     // 16 and go to b.lang_acc, the first line (geometry + colour) to the row
     constexpr int GCOL0 = LO ? 0 : (LD ? 16 : LSR_GROW_LANG);
@@ -1440,21 +1531,34 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     constexpr bool SPF = LSR_BWD_SPLAT_PF && NL <= 32;
     // tile-list position clamped to the range (wmax >= 1: position 0 exists), result selected
     auto pl_at = [&](int q) -> uint32_t { const uint32_t v = a.point_list[rs + max(q, 0)]; return q >= 0 ? v : 0u; };
-    uint32_t gid1 = pl_at(wmax - 1 - lane);
-    uint32_t gid2 = 0u;
+    uint32_t gid1 = 0u, gid2 = 0u;
     float4 A1 = make_float4(0.f, 0.f, 0.f, 0.f), B1 = A1;
-    if constexpr (SPF) {
-        gid2 = pl_at(wmax - 65 - lane);
-        A1 = a.splatA[gid1];   // gid 0 for positions past the range: a valid record, never staged
-        B1 = a.splatB[gid1];
+    // LST: entries [lbase, lbase + cnt) of the block's list, back to front
+    const uint32_t lcnt = LST ? a.lcount[4 * wt.tile + wt.sub] : 0u;
+    const size_t lbase = LST ? (size_t)4 * rs + (size_t)wt.sub * (a.tile_start[wt.tile + 1] - rs) : 0;
+    if constexpr (!LST) {
+        gid1 = pl_at(wmax - 1 - lane);
+        if constexpr (SPF) {
+            gid2 = pl_at(wmax - 65 - lane);
+            A1 = a.splatA[gid1];   // gid 0 for positions past the range: a valid record, never staged
+            B1 = a.splatB[gid1];
+        }
+        // entries past a group's end are read unconditionally (immediate-offset
+        // loads, no index clamps): keep them finite
+        for (int e = lane; e < 80; e += 64) {
+            st.A[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+            st.B[e] = make_float4(0.f, 0.f, 0.f, __int_as_float(0x7fffffff));
+            st.gid[e] = 0u;
+        }
     }
-    // entries past a group's end are read unconditionally (immediate-offset
-    // loads, no index clamps): keep them finite
-    for (int e = lane; e < 80; e += 64) {
-        st.A[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-        st.B[e] = make_float4(0.f, 0.f, 0.f, __int_as_float(0x7fffffff));
-        st.gid[e] = 0u;
-    }
+    // LST: chunk c0's entries lbase + lcnt - 1 - (c0 + lane) -> stl buffer `off`
+    // (lanes past the list copy entry 0: finite, and past the group's end)
+    auto list_dma = [&](int c0, int off) {
+        const int e = (int)lcnt - 1 - (c0 + lane);
+        const size_t src = lbase + (size_t)(e >= 0 ? e : 0);
+        glds16(a.listA + src, stl.A + off);
+        glds16(a.listB + src, stl.B + off);
+    };
 
     float dr0 = 0.f, dr1 = 0.f, dr2 = 0.f;   // the lane's own pixel's RGB dL/dout (0 outside the image)
     if constexpr (!LO) {
@@ -1534,26 +1638,52 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
         sRG[lane] = make_float2(dr0, dr1);
         sBc[lane] = dr2;
     }
+    // LST: a chunk's DMA is waited for with vmcnt(N), N = a lower bound of the
+    // VMEM operations the previous (full, 4-group) chunk issued after it -- its
+    // buffer atomics, GRL x 4 per group (unconditional, never merged; the
+    // feature gathers are not counted) -- so the wait does not drain them
+    constexpr int OPG = GRL * 4;
+    constexpr int CHUNK_OPS = 4 * OPG < 63 ? 4 * OPG : 63;
+    if constexpr (LST) list_dma(0, 0);
     BWD_STAMP(0);
-    for (int c0 = 0; c0 < wmax; c0 += 64) {
-        const int p = wmax - 1 - (c0 + lane);
-        const bool valid = p >= 0;
-        int n;
+    const int cend = LST ? (int)lcnt : wmax;
+    for (int c0 = 0; c0 < cend; c0 += 64) {
+        int n, nfull;
+        const float4* SA;
+        const float4* SB;
+        const uint32_t* SG;
         BWD_COUNT(8);
-        if constexpr (SPF) {
-            const uint32_t gid = gid1;
-            const float4 Ac = A1, Bc = B1;
-            gid1 = gid2;
-            A1 = a.splatA[gid1];
-            B1 = a.splatB[gid1];
-            gid2 = pl_at(p - 128);
-            n = carry + stage_candidates_geo_rec(st, carry, valid, gid, p, pm.bx, pm.by, Ac, Bc);
+        if constexpr (LST) {
+            const int off = (c0 >> 6 & 1) * 64;
+            if (c0 == 0 || !buf_atom) wait_vmcnt<0>();
+            else wait_vmcnt<CHUNK_OPS>();
+            if (c0 + 64 < cend) list_dma(c0 + 64, 64 - off);
+            n = nfull = min(64, cend - c0);
+            SA = stl.A + off;
+            SB = stl.B + off;
+            SG = reinterpret_cast<const uint32_t*>(stl.B + off) + 2;   // B.z, stride 4 words
         } else {
-            const uint32_t gid = gid1;
-            gid1 = pl_at(p - 64);
-            n = carry + stage_candidates_geo(st, carry, valid, gid, p, pm.bx, pm.by, a.splatA, a.splatB);
+            const int p = wmax - 1 - (c0 + lane);
+            const bool valid = p >= 0;
+            if constexpr (SPF) {
+                const uint32_t gid = gid1;
+                const float4 Ac = A1, Bc = B1;
+                gid1 = gid2;
+                A1 = a.splatA[gid1];
+                B1 = a.splatB[gid1];
+                gid2 = pl_at(p - 128);
+                n = carry + stage_candidates_geo_rec(st, carry, valid, gid, p, pm.bx, pm.by, Ac, Bc);
+            } else {
+                const uint32_t gid = gid1;
+                gid1 = pl_at(p - 64);
+                n = carry + stage_candidates_geo(st, carry, valid, gid, p, pm.bx, pm.by, a.splatA, a.splatB);
+            }
+            nfull = (c0 + 64 >= wmax) ? n : (n & ~15);
+            SA = st.A;
+            SB = st.B;
+            SG = st.gid;
         }
-        const int nfull = (c0 + 64 >= wmax) ? n : (n & ~15);
+        constexpr int SGS = LST ? 4 : 1;   // word stride of the id array
         BWD_STAMP(1);
 
         for (int g0 = 0; g0 < nfull; g0 += 16) {
@@ -1562,7 +1692,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             // A fragments of the dot product: feature 4t+lg of candidate g0+li,
             // gathered now, consumed after phase 1
             if constexpr (!LO) {
-                const uint32_t gi = st.gid[g0 + (li < kn ? li : 0)];
+                const uint32_t gi = SG[SGS * (g0 + (li < kn ? li : 0))];
                 dot_features<NL, VEC>(a, gi, lg, af);
             }
             // phase 1: G of the 16 candidates (0 where the pair does not
@@ -1575,15 +1705,15 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             const int kn_u = __builtin_amdgcn_readfirstlane(kn);   // uniform: scalar compares below
             // candidate li's opacity in lane li: phase 2 takes candidate k's
             // from lane k (v_readlane) instead of a broadcast LDS read per k
-            const int opl = __float_as_int(st.B[g0 + li].y);
+            const int opl = __float_as_int(SB[g0 + li].y);
 #define BWD_OP(k) __int_as_float(__builtin_amdgcn_readlane(opl, (k)))
             // GREG: G stays in registers from phase 1 to phase 2 (no LDS round trip)
             float Gr[16];
             (void)Gr;
 #pragma unroll
             for (int k = 0; k < 16; k++) {
-                const float4 A = st.A[g0 + k];
-                const float4 B = st.B[g0 + k];
+                const float4 A = SA[g0 + k];
+                const float4 B = SB[g0 + k];
                 const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
                 const bool cj = (k < kn_u) && (__float_as_int(B.w) < last) && !(power > 0.0f);
                 // G = 0 for a non-candidate pair: alpha - 1/255 is then far below the band
@@ -1599,10 +1729,10 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 for (int k = 0; k < 16; k++) {
                     if (k >= kn) break;
                     const int j = g0 + k;
-                    const float4 A = st.A[j];
-                    const float4 B = st.B[j];
+                    const float4 A = SA[j];
+                    const float4 B = SB[j];
                     const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
-                    const bool cj = (__float_as_int(B.w) < last) & !(power > 0.0f) & !(power < B.z);
+                    const bool cj = (__float_as_int(B.w) < last) & !(power > 0.0f) & (LST || !(power < B.z));
                     const float af2 = fminf(0.99f, B.y * __builtin_amdgcn_exp2f(power * LSR_LOG2E));
                     if (cj & (fabsf(af2 - (1.0f / 255.0f)) < 2e-8f)) {
                         const float G = expf_det(power);
@@ -1773,8 +1903,8 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             if constexpr (!LO) wave_lds_fence();
             if (!LO && lane < kn) {   // lane = candidate li (lg = 0)
                 const int j = g0 + lane;
-                const float4 A = st.A[j];
-                const float4 B = st.B[j];
+                const float4 A = SA[j];
+                const float4 B = SB[j];
                 const float* const mr = sMom + lane * LSR_MOM9_STRIDE;
                 const float4 m03 = *reinterpret_cast<const float4*>(mr);
                 const float4 m47 = *reinterpret_cast<const float4*>(mr + 4);
@@ -1807,7 +1937,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 for (int e = lane; e < 16 * K; e += 64) {
                     const int slot = e / K, m = e - slot * K;
                     if (slot < kn) {
-                        const size_t off = (size_t)st.gid[g0 + slot] * K + m;
+                        const size_t off = (size_t)SG[SGS * (g0 + slot)] * K + m;
                         const int q = quick_index(a.qi, a.qidx_dtype, off);
                         if (q >= 0 && q < D) {
                             const float v = sGr[slot * GRS + GCOL0 + q];
@@ -1823,7 +1953,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 // slot of the q-th atomic of this lane: 4q + lg, or (RREG) 4 lg + q
                 auto slot_of = [&](int q) { return RREG ? 4 * lg + q : 4 * q + lg; };
 #pragma unroll
-                for (int q = 0; q < 4; q++) gq[q] = st.gid[g0 + slot_of(q)];
+                for (int q = 0; q < 4; q++) gq[q] = SG[SGS * (g0 + slot_of(q))];
 #pragma unroll
                 for (int h = 0; h < GRL; h++)
 #pragma unroll
@@ -1882,11 +2012,13 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             BWD_STAMP(6);
         }
         // carry the partial group to the front of the stage
-        carry = n - nfull;
-        if (nfull > 0 && lane < carry) {   // source >= 16 > destination: no overlap
-            st.A[lane] = st.A[nfull + lane];
-            st.B[lane] = st.B[nfull + lane];
-            st.gid[lane] = st.gid[nfull + lane];
+        if constexpr (!LST) {
+            carry = n - nfull;
+            if (nfull > 0 && lane < carry) {   // source >= 16 > destination: no overlap
+                st.A[lane] = st.A[nfull + lane];
+                st.B[lane] = st.B[nfull + lane];
+                st.gid[lane] = st.gid[nfull + lane];
+            }
         }
         wave_lds_fence();
         BWD_STAMP(7);
@@ -1899,14 +2031,18 @@ hipError_t launch_render_bwd_lang(const RenderBwdArgs& b, hipStream_t st)
 {
     const int T = b.f.cam.gx * b.f.cam.gy;
     if (T == 0) return hipSuccess;
+    // LST: the forward's per-block candidate lists (RenderArgs::listA)
+#define LSR_BWD_LO(NL) (b.f.listA ? k_render_bwd_mf<NL, true, false, false, true><<<4 * T, 64, 0, st>>>(b) \
+                                   : k_render_bwd_mf<NL, true><<<4 * T, 64, 0, st>>>(b))
     switch (lang_set_for(b.f.D)) {
-        case 4: k_render_bwd_mf<4, true><<<4 * T, 64, 0, st>>>(b); break;
-        case 8: k_render_bwd_mf<8, true><<<4 * T, 64, 0, st>>>(b); break;
-        case 16: k_render_bwd_mf<16, true><<<4 * T, 64, 0, st>>>(b); break;
-        case 32: k_render_bwd_mf<32, true><<<4 * T, 64, 0, st>>>(b); break;
-        case 64: k_render_bwd_mf<64, true><<<4 * T, 64, 0, st>>>(b); break;
+        case 4: LSR_BWD_LO(4); break;
+        case 8: LSR_BWD_LO(8); break;
+        case 16: LSR_BWD_LO(16); break;
+        case 32: LSR_BWD_LO(32); break;
+        case 64: LSR_BWD_LO(64); break;
         default: return hipErrorInvalidValue;
     }
+#undef LSR_BWD_LO
     return hipGetLastError();
 }
 
@@ -1947,21 +2083,31 @@ hipError_t launch_render_bwd(const RenderBwdArgs& b, hipStream_t st)
 {
     const int T = b.f.cam.gx * b.f.cam.gy;
     if (T == 0) return hipSuccess;
+    // LST: the forward's per-block candidate lists (RenderArgs::listA)
+    const bool lst = b.f.listA != nullptr;
     if (b.lang_acc) {
         if (!bwd_lang_direct(b.f.D) || (uintptr_t)b.f.lang % 16 != 0) return hipErrorInvalidValue;
-        if (b.f.D == 16) k_render_bwd_mf<16, false, true><<<4 * T, 64, 0, st>>>(b);
-        else k_render_bwd_mf<32, false, true><<<4 * T, 64, 0, st>>>(b);
+        if (b.f.D == 16) {
+            if (lst) k_render_bwd_mf<16, false, true, false, true><<<4 * T, 64, 0, st>>>(b);
+            else k_render_bwd_mf<16, false, true><<<4 * T, 64, 0, st>>>(b);
+        } else {
+            if (lst) k_render_bwd_mf<32, false, true, false, true><<<4 * T, 64, 0, st>>>(b);
+            else k_render_bwd_mf<32, false, true><<<4 * T, 64, 0, st>>>(b);
+        }
         return hipGetLastError();
     }
+#define LSR_BWD_FULL(NL) (lst ? k_render_bwd_mf<NL, false, false, false, true><<<4 * T, 64, 0, st>>>(b) \
+                              : k_render_bwd_mf<NL><<<4 * T, 64, 0, st>>>(b))
     switch (lang_set_for(b.f.D)) {
-        case 0: k_render_bwd_mf<0><<<4 * T, 64, 0, st>>>(b); break;
-        case 4: k_render_bwd_mf<4><<<4 * T, 64, 0, st>>>(b); break;
-        case 8: k_render_bwd_mf<8><<<4 * T, 64, 0, st>>>(b); break;
-        case 16: k_render_bwd_mf<16><<<4 * T, 64, 0, st>>>(b); break;
-        case 32: k_render_bwd_mf<32><<<4 * T, 64, 0, st>>>(b); break;
-        case 64: k_render_bwd_mf<64><<<4 * T, 64, 0, st>>>(b); break;
+        case 0: LSR_BWD_FULL(0); break;
+        case 4: LSR_BWD_FULL(4); break;
+        case 8: LSR_BWD_FULL(8); break;
+        case 16: LSR_BWD_FULL(16); break;
+        case 32: LSR_BWD_FULL(32); break;
+        case 64: LSR_BWD_FULL(64); break;
         default: return hipErrorInvalidValue;
     }
+#undef LSR_BWD_FULL
     return hipGetLastError();
 }
 

@@ -312,6 +312,9 @@ class _RasterizeGaussians(torch.autograd.Function):
                          "opacities": id(opacities), "scales": id(scales), "rotations": id(rotations),
                          "cov3D_precomp": id(cov3Ds_precomp)}
         ctx.dims = dims
+        # each 8x8 block's candidate list, written by the forward render for the
+        # backward (lsr_fwd_out.lists; read only, kept for every backward of this graph)
+        ctx.lists = bufs.get(_lib.LSR_BUF_LISTS)
         ctx.save_for_backward(*saved, radii, bufs[_lib.LSR_BUF_GEOM], bufs[_lib.LSR_BUF_BINNING],
                               bufs[_lib.LSR_BUF_IMAGE])
         ctx.mark_non_differentiable(radii)
@@ -345,6 +348,8 @@ class _RasterizeGaussians(torch.autograd.Function):
                           _ptr(qw) if quick else None, _ptr(qi) if quick else None)
         bin_ = _lib.BwdIn(geom.data_ptr(), binning.data_ptr(), image.data_ptr(), ctx.num_rendered, radii.data_ptr(),
                           grad_color.data_ptr(), _ptr(gl))
+        if ctx.lists is not None:
+            bin_.lists = ctx.lists.data_ptr()
         ws = ctx.grad_ws
         ctx.grad_ws = None   # a second backward (retain_graph) clears its own
         if ws is not None:

@@ -207,3 +207,37 @@ def test_global_atomic_binning_fallback(gpu, oracle_lib):
         np.testing.assert_array_equal(got["color"][(slice(None),) + sl], ref["color"][(slice(None),) + sl])
         np.testing.assert_array_equal(got["final_T"][sl], ref["final_T"][sl])
         np.testing.assert_array_equal(got["n_contrib"][sl], ref["n_contrib"][sl].astype(np.int32))
+
+
+@pytest.mark.parametrize("name", ["sh3_lang16_ragged", "yaw_sh3_lang32", "lang64_feature_mode", "cfg1_rgb"])
+def test_backward_without_block_lists(name, gpu, oracle_lib):
+    """The backward re-stages its candidates from the tile lists when the
+    forward's per-block candidate lists are absent (a host that does not pass
+    lsr_fwd_out.lists back): same gradients as the list path and the oracle."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    from harness import gpu_inputs, settings_for
+    case = make_case(**CASES[name])
+    pb = oracle_problem(case)
+    ref = oracle_lib.forward(pb)
+    rng = np.random.default_rng(1)
+    H, W = case["cam"]["H"], case["cam"]["W"]
+    dcol = rng.standard_normal((3, H, W)).astype(np.float32)
+    dlang = rng.standard_normal((pb.D, H, W)).astype(np.float32) if pb.D else None
+    rb = oracle_lib.backward(pb, ref, dcol, dlang)
+    t = gpu_inputs(case, gpu, requires_grad=True)
+    kw = {k: t[k] for k in ("shs", "colors_precomp", "scales", "rotations", "language_feature_precomp") if k in t}
+    color, lang, _ = GaussianRasterizer(settings_for(case, gpu))(means3D=t["means3D"], means2D=t["means2D"],
+                                                                 opacities=t["opacities"], **kw)
+    node = color.grad_fn
+    assert node.lists is not None            # the forward prepared them
+    node.lists = None                        # ... and the backward does not get them
+    outs, grads = [color], [torch.from_numpy(dcol).to(gpu)]
+    if pb.D:
+        outs.append(lang)
+        grads.append(torch.from_numpy(dlang).to(gpu))
+    torch.autograd.backward(outs, grads)
+    assert_grad_close("means2D", t["means2D"].grad.cpu().numpy(), rb["dmean2D"])
+    assert_grad_close("means3D", t["means3D"].grad.cpu().numpy(), rb["dmeans3D"])
+    assert_grad_close("opacities", t["opacities"].grad.cpu().numpy(), rb["dopacity"][:, None])
+    if pb.D:
+        assert_grad_close("language_feature_precomp", t["language_feature_precomp"].grad.cpu().numpy(), rb["dlang"])

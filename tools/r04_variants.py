@@ -49,41 +49,53 @@ V = {
          "                    const float om = 1.f - al;\n                    T = T * __builtin_amdgcn_rcpf(om);",
          "                    const float dot = dv[k];\n                    const float al = fminf(0.99f, BWD_OP(k) * G);\n"
          "                    const float om = 1.f - al;\n                    T = T * __builtin_amdgcn_rcpf(om);")],
-    # candidate: stage padded with INT_MAX positions -> no k < kn test per candidate in phase 1
-    "fullgrp": [
-        ("struct WaveStageG {\n    float4 A[80];\n    float4 B[80];\n    uint32_t gid[80];\n};",
-         "struct WaveStageG {\n    float4 A[96];\n    float4 B[96];\n    uint32_t gid[96];\n};"),
-        ("    for (int e = lane; e < 80; e += 64) {\n        st.A[e] = make_float4(0.f, 0.f, 0.f, 0.f);",
-         "    for (int e = lane; e < 96; e += 64) {\n        st.A[e] = make_float4(0.f, 0.f, 0.f, 0.f);"),
-        ("            n = carry + stage_candidates_geo_rec(st, carry, valid, gid, p, pm.bx, pm.by, Ac, Bc);",
-         "            n = carry + stage_candidates_geo_rec(st, carry, valid, gid, p, pm.bx, pm.by, Ac, Bc);\n"
-         "            if (lane < 16) reinterpret_cast<float*>(&st.B[n + lane])[3] = __int_as_float(0x7fffffff);\n"
-         "            wave_lds_fence();"),
-        ("                const bool cj = (k < kn_u) && (__float_as_int(B.w) < last) && !(power > 0.0f);",
-         "                const bool cj = (__float_as_int(B.w) < last) && !(power > 0.0f);")],
 }
-# fullgrp + the conic pre-scaled by -log2e/2 (power in base 2: 7 VALU instead of 10) (timing)
-V["p1lite"] = [
-    (V["fullgrp"][0][0], "struct WaveStageG {\n    float4 A[96];\n    float4 B[96];\n    float4 Q[96];\n    uint32_t gid[96];\n};"),
-    (V["fullgrp"][1][0], "    for (int e = lane; e < 96; e += 64) {\n        st.Q[e] = make_float4(0.f, 0.f, 0.f, 0.f);\n"
-                         "        st.A[e] = make_float4(0.f, 0.f, 0.f, 0.f);"),
-    V["fullgrp"][2],
-    ("        st.B[r] = make_float4(B.x, B.y, B.z, __int_as_float(pos));\n        st.gid[r] = gid;\n    }\n    wave_lds_fence();\n"
-     "    return __popcll(m);\n}\n\n// Feature c",
-     "        st.B[r] = make_float4(B.x, B.y, B.z, __int_as_float(pos));\n"
-     f"        st.Q[r] = make_float4(-0.5f * {LOG2E} * A.z, -{LOG2E} * A.w, -0.5f * {LOG2E} * B.x, 0.f);\n"
-     "        st.gid[r] = gid;\n    }\n    wave_lds_fence();\n    return __popcll(m);\n}\n\n// Feature c"),
-    ("                const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);\n"
-     "                const bool cj = (k < kn_u) && (__float_as_int(B.w) < last) && !(power > 0.0f);\n"
-     "                // G = 0 for a non-candidate pair: alpha - 1/255 is then far below the band\n"
-     "                const float G = cj ? __builtin_amdgcn_exp2f(power * LSR_LOG2E) : 0.f;",
-     "                const float4 Q = st.Q[g0 + k];\n                const float dx = A.x - pfx, dy = A.y - pfy;\n"
-     "                const float p2 = fmaf(dx, fmaf(Q.x, dx, Q.y * dy), (Q.z * dy) * dy);\n"
-     "                const bool cj = (__float_as_int(B.w) < last) && !(p2 > 0.0f);\n"
-     "                const float G = cj ? __builtin_amdgcn_exp2f(p2) : 0.f;")]
+# candidate: the ML forward's gathered language slices (A operand) loaded one 4-candidate step ahead
+V["fwdpf"] = [(
+    """            for (int q0 = 0; q0 < n; q0 += 4) {
+                if (wave_ballot(!done) == 0) break;
+                // A operand: language channel 16 nb + li of candidate q0 + lg
+                // (0 past the chunk) -- from the staged rows, or (SF) gathered
+                float av[MLB];
+#pragma unroll
+                for (int nb = 0; nb < MLB; nb++) {
+                    // MLM: channels past D (a language set wider than D) read 0
+                    const int ch = 16 * nb + li;
+                    float fa;
+                    if constexpr (SF)
+                        fa = a.lang[(size_t)st.gid[min(q0 + lg, n - 1)] * D + (MLM ? min(ch, D - 1) : ch)];
+                    else
+                        fa = Fs[(q0 + lg) * (F4 * 4) + 3 + ch];
+                    av[nb] = ((q0 + lg < n) & (!MLM || ch < D)) ? fa : 0.f;
+                }""",
+    """            auto a_op = [&](int q, float (&o)[MLB]) {
+#pragma unroll
+                for (int nb = 0; nb < MLB; nb++) {
+                    const int ch = 16 * nb + li;
+                    float fa;
+                    if constexpr (SF)
+                        fa = a.lang[(size_t)st.gid[min(q + lg, n - 1)] * D + (MLM ? min(ch, D - 1) : ch)];
+                    else
+                        fa = Fs[(q + lg) * (F4 * 4) + 3 + ch];
+                    o[nb] = ((q + lg < n) & (!MLM || ch < D)) ? fa : 0.f;
+                }
+            };
+            float avn[MLB];
+            if (n > 0) a_op(0, avn);
+            for (int q0 = 0; q0 < n; q0 += 4) {
+                if (wave_ballot(!done) == 0) break;
+                float av[MLB];
+#pragma unroll
+                for (int nb = 0; nb < MLB; nb++) av[nb] = avn[nb];
+                if (q0 + 4 < n) a_op(q0 + 4, avn);""")]
+
+# baseline: no per-block candidate lists (the backward re-stages from the tile lists)
+V["nolst"] = [("    uint8_t* p = (uint8_t*)lb;\n    ra.listA = (float4*)p;",
+               "    uint8_t* p = (uint8_t*)lb;\n    return;\n    ra.listA = (float4*)p;", "lsr_api.hip")]
+
 # diagnostic: per-phase s_memtime census (tools/bwd_stamps.py)
-V["stamps"] = [('#include "lsr_internal.h"\n\n#ifndef LSR_BWD_SPLAT_PF',
-                '#define LSR_BWD_STAMPS 1\n#include "lsr_internal.h"\n\n#ifndef LSR_BWD_SPLAT_PF')]
+V["stamps"] = [('#include "lsr_internal.h"\n\n#include <type_traits>',
+                '#define LSR_BWD_STAMPS 1\n#include "lsr_internal.h"\n\n#include <type_traits>')]
 
 
 def build(name):
