@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 7
+#define LSR_ABI_VERSION 8
 
 enum {
     LSR_OK = 0,
@@ -303,6 +303,19 @@ int lsr_knn_dist2(const float* points, int64_t N, float* out, lsr_alloc_fn alloc
 
 const char* lsr_strerror(int code);
 int lsr_abi_version(void);
+
+/* Process-wide options.  LSR_OPT_BIN_MODE picks the forward's tile binning:
+ * LSR_BIN_SORTED_TILES scatters (depth, id) keys into the tile buckets and
+ * sorts each bucket; LSR_BIN_ORDERED radix-sorts the Gaussians by depth once
+ * and places every bucket's instances in that order (no bucket sort);
+ * LSR_BIN_AUTO (default) takes the ordered mode from ~3M Gaussians up.  Both
+ * produce the identical point_list.  LSR_EINVAL for an unknown option/value. */
+#define LSR_OPT_BIN_MODE 1
+#define LSR_BIN_AUTO 0
+#define LSR_BIN_SORTED_TILES 1
+#define LSR_BIN_ORDERED 2
+int lsr_set_option(int option, int64_t value);
+int lsr_get_option(int option, int64_t* value);
 
 /* Dense language channel sets compiled into this build (ascending; D is
  * rounded up to the next set).  Returns the largest supported D. */

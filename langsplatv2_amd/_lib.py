@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LSR_LIB", os.path.join(_HERE, "liblsr.so"))
 
 LSR_OK = 0
+LSR_EINVAL = 1
 LSR_ENONFINITE = 6
 LSR_ELISTS = 7
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_GRAD, LSR_BUF_DECODE, LSR_BUF_KNN, LSR_BUF_LOSS = 0, 1, 2, 3, 4, 5, 6
@@ -126,7 +127,7 @@ EXPORTS = ("lsr_forward", "lsr_backward", "lsr_mark_visible", "lsr_quick_decode"
            "lsr_quick_decode_prepare", "lsr_quick_decode_run", "lsr_topk_code_forward",
            "lsr_topk_code_backward", "lsr_topk_code_backward_sparse", "lsr_knn_dist2", "lsr_lang_loss_forward", "lsr_lang_loss_backward", "lsr_adam_step", "lsr_sh_grad_from_views", "lsr_strerror",
            "lsr_abi_version", "lsr_max_lang_dim", "lsr_profile_enable", "lsr_profile_stages", "lsr_profile_reset",
-           "lsr_profile_query")
+           "lsr_profile_query", "lsr_set_option", "lsr_get_option")
 
 _lib = None
 
@@ -196,6 +197,10 @@ def load(path: str | None = None):
     lib.lsr_profile_query.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
     lib.lsr_profile_query.restype = ctypes.c_int
+    lib.lsr_set_option.argtypes = [ctypes.c_int, ctypes.c_int64]
+    lib.lsr_set_option.restype = ctypes.c_int
+    lib.lsr_get_option.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
+    lib.lsr_get_option.restype = ctypes.c_int
     if path is None:
         _lib = lib
     return lib
@@ -205,6 +210,23 @@ def check(rc: int, what: str):
     if rc != LSR_OK:
         msg = load().lsr_strerror(rc).decode()
         raise RuntimeError(f"{what} failed: {msg} (code {rc})")
+
+
+LSR_OPT_BIN_MODE = 1
+BIN_MODES = {"auto": 0, "sorted_tiles": 1, "ordered": 2}
+
+
+def set_bin_mode(mode: str) -> str:
+    """Select the forward's tile binning process-wide (lsr_set_option
+    LSR_OPT_BIN_MODE): "sorted_tiles", "ordered" or "auto"; returns the
+    previous mode.  Both modes produce the same point_list."""
+    if mode not in BIN_MODES:
+        raise ValueError(f"bin mode must be one of {sorted(BIN_MODES)}")
+    lib = load()
+    prev = ctypes.c_int64(0)
+    check(lib.lsr_get_option(LSR_OPT_BIN_MODE, ctypes.byref(prev)), "lsr_get_option")
+    check(lib.lsr_set_option(LSR_OPT_BIN_MODE, BIN_MODES[mode]), "lsr_set_option")
+    return {v: k for k, v in BIN_MODES.items()}[prev.value]
 
 
 def profile_enable(on: bool = True):

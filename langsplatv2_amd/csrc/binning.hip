@@ -19,7 +19,7 @@
 // (tile_keep, lsr_device.h); a dropped instance has alpha < 1/255 at every
 // pixel of its tile, so no output changes (the oracle checks both lists
 // render identically: tests/test_oracle.py).  cfg3: 8.25 M -> 4.73 M.
-#include "lsr_internal.h"
+#include "bin_common.h"
 
 #include <algorithm>
 
@@ -288,28 +288,6 @@ hipError_t launch_scatter(const Cam& c, int P, const uint8_t* geom, const int32_
 // fixed by the per-tile sort.
 
 
-// Screen bands: each block owns a band of `rows` tile rows, so a block's LDS
-// histogram covers rows * gx tiles (<= LSR_BAND_LDS bytes) and several blocks
-// stay resident per CU at any resolution; a Gaussian's rect is clipped to the
-// band (each band re-reads the chunk's 20-B records, cheap next to the
-// instance work).
-#ifndef LSR_BAND_LDS
-#define LSR_BAND_LDS 32768
-#endif
-#ifndef LSR_COUNT_XCD
-#define LSR_COUNT_XCD 1   // chunk-major count grid: cfg5 bin_count 0.627 -> 0.604 ms (cfg3 ±0)
-#endif
-struct Band {
-    int ty0, ty1, t0, nt;
-    __device__ Band(const Cam& c, int rows, int band)
-    {
-        ty0 = band * rows;
-        ty1 = min(c.gy, ty0 + rows);
-        t0 = ty0 * c.gx;
-        nt = (ty1 - ty0) * c.gx;
-    }
-};
-
 // Load-balanced expansion of the kept instances.  Lane l of a wave owns
 // Gaussian i0 + l: its cull box clipped to the band, h_l rows.  The wave's
 // rows are numbered by an exclusive scan of h_l and taken 64 at a time
@@ -349,16 +327,6 @@ __device__ __forceinline__ int wave_spans_stage(WaveSpans& ws, int h, int bx0, i
     if (lane == 63) ws.rpre[64] = s;
     wave_lds_fence();
     return __shfl(s, 63, 64);
-}
-
-// largest o in [0, 64) with pre[o] <= k (pre non-decreasing, pre[64] > k)
-__device__ __forceinline__ int wave_search(const int* pre, int k)
-{
-    int o = 0;
-#pragma unroll
-    for (int step = 32; step >= 1; step >>= 1)
-        if (pre[o + step] <= k) o += step;
-    return o;
 }
 
 // Row entry e of the staged wave: its owner (returned), band row yr and kept
@@ -426,44 +394,6 @@ struct SpanWalk {
     }
 };
 
-// One Gaussian's binning inputs (radius, the two splat records, depth),
-// loaded one wave iteration ahead of their use (LSR_BIN_PF): the walk of
-// iteration k runs while iteration k + 1's records are in flight, instead of
-// every iteration waiting for a dependent radius -> record gather.  Lanes
-// past the chunk read Gaussian g1 - 1 (a valid address) and get radius 0.
-struct BinRec {
-    int r;
-    float4 A, B;
-    float depth;
-    __device__ __forceinline__ void load(const uint8_t* geom, int P, int g1, const int32_t* __restrict__ radii, int i,
-                                         bool with_depth)
-    {
-        const GeomLayout L = geom_layout(P);
-        const int q = min(i, g1 - 1);
-        const int rr = radii[q];
-        A = ((const float4*)(geom + L.splatA))[q];
-        B = ((const float4*)(geom + L.splatB))[q];
-        depth = with_depth ? ((const float*)(geom + L.depth))[q] : 0.f;
-        r = i < g1 ? rr : 0;
-    }
-};
-
-// Lane's Gaussian -> its cull box clipped to the band: columns [x0, x1),
-// first row y0 (band-relative); returns the row count (0 if none).
-__device__ __forceinline__ int band_box(const Cam& c, const Band& bd, const BinRec& g, int& x0, int& x1, int& y0)
-{
-    x0 = x1 = y0 = 0;
-    if (g.r <= 0) return 0;
-    int y1;
-    get_rect(g.A.x, g.A.y, g.r, c.gx, c.gy, x0, y0, x1, y1);
-    cull_box(g.A.x, g.A.y, g.A.z, g.A.w, g.B.x, g.B.z, x0, y0, x1, y1);
-    y0 = max(y0, bd.ty0);
-    y1 = min(y1, bd.ty1);
-    const int h = (y1 > y0 && x1 > x0) ? y1 - y0 : 0;
-    y0 -= bd.ty0;
-    return h;
-}
-
 // Stage the lane's Gaussian for the span walk; returns the wave's row total.
 __device__ __forceinline__ int stage_gaussian(WaveSpans& ws, const Cam& c, const Band& bd, const BinRec& g)
 {
@@ -476,7 +406,7 @@ template <int BB>
 __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int rows, int S,
                                                          const uint8_t* __restrict__ geom,
                                                          const int32_t* __restrict__ radii, uint32_t* __restrict__ table,
-                                                         uint32_t* __restrict__ cls_cnt)
+                                                         uint32_t* __restrict__ cls_cnt, const uint32_t* __restrict__ order)
 {
     extern __shared__ uint32_t hist[];
     __shared__ WaveSpans wss[BB / 64];
@@ -499,10 +429,10 @@ __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int r
     const int lane = threadIdx.x & 63;
     const int g0 = blk * chunk, g1 = min(P, g0 + chunk);
     BinRec nx;
-    if (g0 < g1) nx.load(geom, P, g1, radii, g0 + (threadIdx.x & ~63) + lane, false);
+    if (g0 < g1) nx.load(geom, P, g1, radii, g0 + (threadIdx.x & ~63) + lane, false, order);
     for (int i0 = g0 + (threadIdx.x & ~63); i0 < g1; i0 += BB) {
         const BinRec cur = nx;
-        nx.load(geom, P, g1, radii, i0 + BB + lane, false);
+        nx.load(geom, P, g1, radii, i0 + BB + lane, false, order);
         const int R = stage_gaussian(ws, c, bd, cur);
         // every row entry adds its kept range [sx0, sx1) to the histogram as
         // a difference (+1 at sx0, -1 at sx1 inside the row): two LDS atomics
@@ -804,8 +734,8 @@ static int bin_band_rows(const Cam& c)
 #ifndef LSR_SCATTER_MERGE
 #define LSR_SCATTER_MERGE 0
 #endif
-static int scatter_merge(int P) { return LSR_SCATTER_MERGE > 0 ? LSR_SCATTER_MERGE : (P >= (4 << 20) ? 4 : 1); }
-static int bin_scatter_rows(const Cam& c)
+int scatter_merge(int P) { return LSR_SCATTER_MERGE > 0 ? LSR_SCATTER_MERGE : (P >= (4 << 20) ? 4 : 1); }
+int bin_scatter_rows(const Cam& c)
 {
     if (LSR_SCATTER_ROWS > 0) return std::max(1, std::min(c.gy, LSR_SCATTER_ROWS));
     return std::max(1, std::min(c.gy, LSR_SCATTER_LDS / (4 * c.gx)));
@@ -815,7 +745,7 @@ static int bin_scatter_rows(const Cam& c)
 // bin_count 0.070 -> 0.061 ms: the LDS histogram's clear and flush loops
 // halve), 8 waves from 4M up (16 measured slower at cfg5: count 0.60 -> 0.66,
 // scatter 0.98 -> 1.11 ms).
-static int bin_block(int P) { return P >= (4 << 20) ? 512 : 1024; }
+int bin_block(int P) { return P >= (4 << 20) ? 512 : 1024; }
 
 int bin_blocks(int P, const Cam& c, int& chunk)
 {
@@ -839,7 +769,8 @@ bool bin_privatised_ok(const Cam& c) { return (size_t)c.gx * 4 <= LSR_BAND_LDS &
 
 hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t* geom, const int32_t* radii,
                             uint32_t* table, uint32_t* tile_cnt, uint32_t* tile_start, uint64_t* tpart,
-                            uint32_t* cls_cnt, uint32_t* cls_list, uint64_t* host_slot, uint32_t seq, hipStream_t st)
+                            uint32_t* cls_cnt, uint32_t* cls_list, uint64_t* host_slot, uint32_t seq, hipStream_t st,
+                            const uint32_t* order)
 {
     const int T = c.gx * c.gy;
     const int rows = bin_band_rows(c);
@@ -854,9 +785,9 @@ hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t
     }
     if (B > 0) {
         if (bin_block(P) == 1024)
-            k_bin_count<1024><<<grid, 1024, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt);
+            k_bin_count<1024><<<grid, 1024, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt, order);
         else
-            k_bin_count<512><<<grid, 512, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt);
+            k_bin_count<512><<<grid, 512, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt, order);
         BinPublish pb{tpart, cls_cnt + LSR_TICKET_WORD, tile_start + T, host_slot, seq};
         const int G = (T + TBL_TILES - 1) / TBL_TILES, Tp = table_stride(T);
         if (B <= 16 * TBL_RPT)

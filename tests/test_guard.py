@@ -16,7 +16,22 @@ def test_status_codes_have_text():
     lib = _lib.load()
     assert b"non-finite" in lib.lsr_strerror(_lib.LSR_ENONFINITE).lower()
     assert b"binning lists" in lib.lsr_strerror(_lib.LSR_ELISTS).lower()
-    assert lib.lsr_abi_version() == 7
+    assert lib.lsr_abi_version() == 8
+
+
+def test_bin_mode_option_roundtrip():
+    """lsr_set_option / lsr_get_option (host-only: no GPU needed)."""
+    import ctypes
+    lib = _lib.load()
+    prev = _lib.set_bin_mode("ordered")
+    v = ctypes.c_int64(-1)
+    assert lib.lsr_get_option(_lib.LSR_OPT_BIN_MODE, ctypes.byref(v)) == 0 and v.value == 2
+    assert _lib.set_bin_mode("sorted_tiles") == "ordered"
+    assert _lib.set_bin_mode(prev) == "sorted_tiles"
+    assert lib.lsr_set_option(_lib.LSR_OPT_BIN_MODE, 3) == _lib.LSR_EINVAL
+    assert lib.lsr_set_option(12345, 0) == _lib.LSR_EINVAL
+    with pytest.raises(ValueError):
+        _lib.set_bin_mode("bogus")
 
 
 def _render(case, dev, debug, poison=None):

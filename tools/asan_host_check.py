@@ -95,7 +95,7 @@ assert lib.lsr_adam_step(None, None, None, None, -1, 0.1, 0.9, 0.999, 1e-8, 0.0,
 calls += 9
 # pure host code: stage-name parsing (random strings), profiling tables, versions
 names = ["preprocess", "scan_tiles", "bin_count", "scan_tile_counts", "bin_scatter", "tile_sort", "render_fwd",
-         "grad_zero", "render_bwd", "preprocess_bwd"]
+         "grad_zero", "render_bwd", "preprocess_bwd", "depth_order"]
 for _ in range(2000):
     parts = [rng.choice(names + ["", "x", "render", "render_bwdx", "a" * rng.randint(0, 300)]) for _ in
              range(rng.randint(0, 6))]
@@ -115,9 +115,21 @@ ms = (ctypes.c_double * 16)()
 cl = (ctypes.c_int64 * 16)()
 for k in (0, 1, 5, 10, 16):
     n = lib.lsr_profile_query(nm, ms, cl, k)
-    assert n == min(k, 10), (k, n)
+    assert n == min(k, len(names)), (k, n)
     calls += 1
 lib.lsr_profile_enable(0)
+# process-wide options: valid modes round-trip, anything else is rejected
+lib.lsr_set_option.argtypes = [ctypes.c_int, ctypes.c_int64]
+lib.lsr_get_option.argtypes = [ctypes.c_int, ctypes.c_void_p]
+v = ctypes.c_int64(-1)
+for mode in (2, 1, 0):
+    assert lib.lsr_set_option(1, mode) == 0
+    assert lib.lsr_get_option(1, ctypes.byref(v)) == 0 and v.value == mode
+    calls += 2
+for opt, val in ((1, 3), (1, -1), (0, 0), (77, 1)):
+    assert lib.lsr_set_option(opt, val) != 0
+    calls += 1
+assert lib.lsr_get_option(1, None) != 0
 for code in range(-3, 10):
     assert lib.lsr_strerror(code)
     calls += 1
