@@ -1,6 +1,9 @@
 """A/B timing of liblsr variants in ONE process: each variant's library is
 loaded under its own name and the cfg3 fwd+bwd stage times are measured in
-interleaved rounds (cdna guide §5.4 rule 24).  Usage: python tools/ab.py name=path.so ..."""
+interleaved rounds (cdna guide §5.4 rule 24).  Usage: python tools/ab.py name=path.so[#binmode] ...
+(binmode: auto / sorted_tiles / ordered, set through lsr_set_option before each of the variant's rounds;
+LSR_CFG selects the BASELINE config, default 3)."""
+import ctypes
 import os
 import statistics
 import sys
@@ -14,7 +17,8 @@ from langsplatv2_amd.scenes import CONFIGS, make_camera, make_gaussians  # noqa:
 import bench  # noqa: E402
 
 variants = [a.split("=", 1) for a in sys.argv[1:]]
-libs = {name: _lib.load(path) for name, path in variants}
+modes = {name: _lib.BIN_MODES[path.split("#", 1)[1]] if "#" in path else None for name, path in variants}
+libs = {name: _lib.load(path.split("#", 1)[0]) for name, path in variants}
 cfg = CONFIGS[int(os.environ.get("LSR_CFG", "3"))]
 D = int(os.environ.get("LSR_D", cfg["lang_dim"]))
 FWD_ONLY = not cfg["backward"]
@@ -29,8 +33,12 @@ dc = torch.randn(3, cfg["H"], cfg["W"], device=dev)
 dl = torch.randn(D, cfg["H"], cfg["W"], device=dev)
 
 
-def run(lib, steps):
+def run(name, steps):
+    lib = libs[name]
     _lib._lib = lib
+    if modes[name] is not None:
+        lib.lsr_set_option.argtypes = [ctypes.c_int, ctypes.c_int64]
+        assert lib.lsr_set_option(_lib.LSR_OPT_BIN_MODE, modes[name]) == 0
     lib.lsr_profile_reset()
     lib.lsr_profile_enable(1)
     for _ in range(steps):
@@ -50,10 +58,10 @@ def run(lib, steps):
 
 res = {name: [] for name, _ in variants}
 for name, _ in variants:
-    run(libs[name], 3)
+    run(name, 3)
 for rnd in range(5):
     for name, _ in variants:
-        res[name].append(run(libs[name], 5))
+        res[name].append(run(name, 5))
 for name, _ in variants:
     stages = res[name][0].keys()
     med = {k: statistics.median(x[k] for x in res[name]) for k in stages}
