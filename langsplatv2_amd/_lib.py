@@ -197,10 +197,11 @@ def load(path: str | None = None):
     lib.lsr_profile_query.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
     lib.lsr_profile_query.restype = ctypes.c_int
-    lib.lsr_set_option.argtypes = [ctypes.c_int, ctypes.c_int64]
-    lib.lsr_set_option.restype = ctypes.c_int
-    lib.lsr_get_option.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
-    lib.lsr_get_option.restype = ctypes.c_int
+    if hasattr(lib, "lsr_set_option"):   # (A/B builds of older sources lack the options)
+        lib.lsr_set_option.argtypes = [ctypes.c_int, ctypes.c_int64]
+        lib.lsr_set_option.restype = ctypes.c_int
+        lib.lsr_get_option.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
+        lib.lsr_get_option.restype = ctypes.c_int
     if path is None:
         _lib = lib
     return lib

@@ -907,7 +907,9 @@ __device__ __forceinline__ int quick_code_raw(const WaveRawQ<DT == 2 ? 8 : 4>& r
 // record, rgb, weight row and index row land at slot l of each array (an LDS-
 // DMA writes wave-uniform M0 + lane x size).  One asm block walks M0 through
 // the arrays (raw's layout is fixed by the static_asserts below); the weight
-// and index row parts are the immediate offsets of one address each.  (The
+// and index row parts are the immediate offsets of one address each.  The
+// immediate offset applies to the LDS destination as well (M0 + offset + 16
+// lane), so M0 steps to each array's base minus that offset.  (The
 // __builtin_amdgcn_global_load_lds form crashes ROCm 7.2's SIFixSGPRCopies in
 // this kernel, and per-call M0 constants spilled SGPRs.)  The caller waits with
 // s_waitcnt vmcnt before reading raw.
@@ -930,11 +932,11 @@ __device__ __forceinline__ void quick_dma12(WaveRawQ<QB>& raw, const RenderArgs&
                      LSR_GLDS(1024, "global_load_lds_dwordx4 %[pB], off")
                      LSR_GLDS(1024, "global_load_lds_dwordx3 %[pR], off")
                      LSR_GLDS(768, "global_load_lds_dwordx4 %[pW], off")
-                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pW], off offset:16")
-                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pW], off offset:32")
-                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off")
-                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off offset:16")
-                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off offset:32")
+                     LSR_GLDS(1008, "global_load_lds_dwordx4 %[pW], off offset:16")
+                     LSR_GLDS(1008, "global_load_lds_dwordx4 %[pW], off offset:32")
+                     LSR_GLDS(1056, "global_load_lds_dwordx4 %[pQ], off")
+                     LSR_GLDS(1008, "global_load_lds_dwordx4 %[pQ], off offset:16")
+                     LSR_GLDS(1008, "global_load_lds_dwordx4 %[pQ], off offset:32")
                      "s_mov_b32 m0, %[keep]"
                      : [keep] "=&s"(keep)
                      : [base] "s"(base), [pA] "v"(pA), [pB] "v"(pB), [pR] "v"(pR), [pW] "v"(pW), [pQ] "v"(pQ)
@@ -945,14 +947,14 @@ __device__ __forceinline__ void quick_dma12(WaveRawQ<QB>& raw, const RenderArgs&
                      LSR_GLDS(1024, "global_load_lds_dwordx4 %[pB], off")
                      LSR_GLDS(1024, "global_load_lds_dwordx3 %[pR], off")
                      LSR_GLDS(768, "global_load_lds_dwordx4 %[pW], off")
-                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pW], off offset:16")
-                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pW], off offset:32")
-                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off")
-                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off offset:16")
-                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off offset:32")
-                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off offset:48")
-                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off offset:64")
-                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pQ], off offset:80")
+                     LSR_GLDS(1008, "global_load_lds_dwordx4 %[pW], off offset:16")
+                     LSR_GLDS(1008, "global_load_lds_dwordx4 %[pW], off offset:32")
+                     LSR_GLDS(1056, "global_load_lds_dwordx4 %[pQ], off")
+                     LSR_GLDS(1008, "global_load_lds_dwordx4 %[pQ], off offset:16")
+                     LSR_GLDS(1008, "global_load_lds_dwordx4 %[pQ], off offset:32")
+                     LSR_GLDS(1008, "global_load_lds_dwordx4 %[pQ], off offset:48")
+                     LSR_GLDS(1008, "global_load_lds_dwordx4 %[pQ], off offset:64")
+                     LSR_GLDS(1008, "global_load_lds_dwordx4 %[pQ], off offset:80")
                      "s_mov_b32 m0, %[keep]"
                      : [keep] "=&s"(keep)
                      : [base] "s"(base), [pA] "v"(pA), [pB] "v"(pB), [pR] "v"(pR), [pW] "v"(pW), [pQ] "v"(pQ)

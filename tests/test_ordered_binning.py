@@ -60,9 +60,9 @@ def test_ordered_big_tiles_and_empty(gpu, oracle_lib, bin_mode):
 
 
 def test_ordered_backward_vs_sorted_tiles(gpu, bin_mode):
-    """Same lists => the backward (and the block lists it reads) are the same
-    computation: gradients bit-identical between the modes."""
-    from harness import run_gpu_fwd_bwd
+    """Same lists => the same forward (bit-identical) and the same backward
+    computation (equal up to the order of the gradient atomics: GRAD_RTOL)."""
+    from harness import assert_grad_close, run_gpu_fwd_bwd
     case = make_case(**CASES["sh3_lang16_ragged"])
     rng = np.random.default_rng(2)
     H, W = case["cam"]["H"], case["cam"]["W"]
@@ -73,8 +73,10 @@ def test_ordered_backward_vs_sorted_tiles(gpu, bin_mode):
     bin_mode("ordered")
     b = run_gpu_fwd_bwd(case, gpu, dcol, dlang)
     for k in a:
-        if k.startswith("grad_") or k in ("color", "lang"):
+        if k in ("color", "lang", "radii"):
             np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+        elif k.startswith("grad_"):
+            assert_grad_close(k, b[k], a[k])
 
 
 @pytest.mark.slow
