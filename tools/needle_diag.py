@@ -46,3 +46,32 @@ for t in tiles:
             py, px = ty * 16 + y, tx * 16 + x
             print(f"   px ({px},{py}) gpu {g[:, y, x]} uncull {u[:, y, x]} cull {c[:, y, x]}"
                   f" T gpu {got['final_T'][py, px]} uncull {ref_u['final_T'][py, px]}")
+
+# records: GPU vs oracle for the visible Gaussians
+vis = culled0["radii"] > 0
+for k in ("xy", "conic_opacity", "depth"):
+    a, b = got[k][vis], culled0[k][vis]
+    bad = np.nonzero((a != b).reshape(a.shape[0], -1).any(1))[0]
+    print(k, "mismatching Gaussians:", len(bad), "of", int(vis.sum()))
+    for i in bad[:3]:
+        print("   gpu", a[i], "oracle", b[i])
+# the pair behind the first mismatching pixel: which Gaussians are in that tile's list, their power at the pixel
+t = None
+for tt in tiles:
+    tx, ty = tt % gx, tt // gx
+    sl = (slice(None), slice(ty * 16, ty * 16 + 16), slice(tx * 16, tx * 16 + 16))
+    if (got["color"][sl] != ref_c["color"][sl]).any():
+        t = tt
+        ys, xs = np.nonzero((got["color"][sl] != ref_c["color"][sl]).any(0))
+        py, px = ty * 16 + ys[0], tx * 16 + xs[0]
+        break
+if t is not None:
+    r = culled0["ranges"][t]
+    ids = culled0["point_list"][r[0]:r[1]]
+    f = np.float32
+    for i in ids[:8]:
+        x, y = got["xy"][i]
+        ca, cb, cc, o = got["conic_opacity"][i]
+        dx, dy = f(x) - f(px), f(y) - f(py)
+        p = f(-0.5) * (f(ca * dx) * dx + f(f(cc * dy) * dy)) - f(f(cb * dx) * dy)
+        print(f"   id {i} xy {x},{y} conic {ca:.6g},{cb:.6g},{cc:.6g} o {o:.4g} power@({px},{py}) ~ {p:.6g}")
