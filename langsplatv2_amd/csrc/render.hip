@@ -884,7 +884,7 @@ template <int QB>
 struct WaveRawQ {
     float4 A[64];
     float4 B[64];
-    float rgb[64 * 3];                  // 12-B DMA: lane l at 12 l
+    float rgb[3][64];                   // channel c of lane l (three 4-B DMAs)
     float4 W[3][64];                    // weight row part p (4 weights) of lane l
     uint4 Q[3 * QB / 4][64];            // index row bytes [16 p, 16 p + 16) of lane l
 };
@@ -909,7 +909,9 @@ __device__ __forceinline__ int quick_code_raw(const WaveRawQ<DT == 2 ? 8 : 4>& r
 // the arrays (raw's layout is fixed by the static_asserts below); the weight
 // and index row parts are the immediate offsets of one address each.  The
 // immediate offset applies to the LDS destination as well (M0 + offset + 16
-// lane), so M0 steps to each array's base minus that offset.  (The
+// lane), so M0 steps to each array's base minus that offset.  The colour
+// goes as three 4-B DMAs (one channel plane each): a dwordx3 LDS-DMA does not
+// land at 12 x lane (measured: wrong colours with the 12-B layout).  (The
 // __builtin_amdgcn_global_load_lds form crashes ROCm 7.2's SIFixSGPRCopies in
 // this kernel, and per-call M0 constants spilled SGPRs.)  The caller waits with
 // s_waitcnt vmcnt before reading raw.
@@ -930,8 +932,10 @@ __device__ __forceinline__ void quick_dma12(WaveRawQ<QB>& raw, const RenderArgs&
         asm volatile("s_mov_b32 %[keep], m0\n\t"
                      "s_mov_b32 m0, %[base]\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[pA], off\n\t"
                      LSR_GLDS(1024, "global_load_lds_dwordx4 %[pB], off")
-                     LSR_GLDS(1024, "global_load_lds_dwordx3 %[pR], off")
-                     LSR_GLDS(768, "global_load_lds_dwordx4 %[pW], off")
+                     LSR_GLDS(1024, "global_load_lds_dword %[pR], off")
+                     LSR_GLDS(252, "global_load_lds_dword %[pR], off offset:4")
+                     LSR_GLDS(252, "global_load_lds_dword %[pR], off offset:8")
+                     LSR_GLDS(264, "global_load_lds_dwordx4 %[pW], off")
                      LSR_GLDS(1008, "global_load_lds_dwordx4 %[pW], off offset:16")
                      LSR_GLDS(1008, "global_load_lds_dwordx4 %[pW], off offset:32")
                      LSR_GLDS(1056, "global_load_lds_dwordx4 %[pQ], off")
@@ -945,8 +949,10 @@ __device__ __forceinline__ void quick_dma12(WaveRawQ<QB>& raw, const RenderArgs&
         asm volatile("s_mov_b32 %[keep], m0\n\t"
                      "s_mov_b32 m0, %[base]\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[pA], off\n\t"
                      LSR_GLDS(1024, "global_load_lds_dwordx4 %[pB], off")
-                     LSR_GLDS(1024, "global_load_lds_dwordx3 %[pR], off")
-                     LSR_GLDS(768, "global_load_lds_dwordx4 %[pW], off")
+                     LSR_GLDS(1024, "global_load_lds_dword %[pR], off")
+                     LSR_GLDS(252, "global_load_lds_dword %[pR], off offset:4")
+                     LSR_GLDS(252, "global_load_lds_dword %[pR], off offset:8")
+                     LSR_GLDS(264, "global_load_lds_dwordx4 %[pW], off")
                      LSR_GLDS(1008, "global_load_lds_dwordx4 %[pW], off offset:16")
                      LSR_GLDS(1008, "global_load_lds_dwordx4 %[pW], off offset:32")
                      LSR_GLDS(1056, "global_load_lds_dwordx4 %[pQ], off")
@@ -1018,7 +1024,7 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
             const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             st.A[r] = A;
             st.B[r] = make_float4(B.x, B.y, B.z, __int_as_float((int)(idx - rs) + 1));
-            st.C[r] = make_float4(raw.rgb[3 * lane], raw.rgb[3 * lane + 1], raw.rgb[3 * lane + 2], 0.f);
+            st.C[r] = make_float4(raw.rgb[0][lane], raw.rgb[1][lane], raw.rgb[2][lane], 0.f);
             st.Wt[r][0] = raw.W[0][lane];
             st.Wt[r][1] = raw.W[1][lane];
             st.Wt[r][2] = raw.W[2][lane];
@@ -1745,6 +1751,8 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             }
             BWD_STAMP(2);
             // dot[k][p] of the group's candidates on MFMA: (16 x C) . (C x 64)
+            float dv[16];
+            (void)dv;
             if constexpr (!LO) {
                 f32x4 acc[4];
 #pragma unroll
@@ -1755,9 +1763,18 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                     for (int pb = 0; pb < 4; pb++)
                         acc[pb] = BWD_MFMA(af[t], dotB[t][pb], acc[pb]);
 #pragma unroll
-                for (int pb = 0; pb < 4; pb++)
-#pragma unroll
-                    for (int r = 0; r < 4; r++) sDU[(4 * lg + r) * GS + pb * 16 + li] = acc[pb][r];
+                for (int r = 0; r < 4; r++) {
+                    uint32_t x0 = __float_as_uint(acc[0][r]), x1 = __float_as_uint(acc[1][r]);
+                    uint32_t x2 = __float_as_uint(acc[2][r]), x3 = __float_as_uint(acc[3][r]);
+                    auto s02 = __builtin_amdgcn_permlane32_swap(x0, x2, false, false);
+                    auto s13 = __builtin_amdgcn_permlane32_swap(x1, x3, false, false);
+                    auto s01 = __builtin_amdgcn_permlane16_swap(s02[0], s13[0], false, false);
+                    auto s23 = __builtin_amdgcn_permlane16_swap(s02[1], s13[1], false, false);
+                    dv[0 + r] = __uint_as_float(s01[0]);
+                    dv[4 + r] = __uint_as_float(s01[1]);
+                    dv[8 + r] = __uint_as_float(s23[0]);
+                    dv[12 + r] = __uint_as_float(s23[1]);
+                }
             }
             wave_lds_fence();
             BWD_STAMP(3);
@@ -1780,7 +1797,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
                     const float G = Gr[k];
-                    const float dot = sDU[k * GS + lane];
+                    const float dot = dv[k];
                     const float al = fminf(0.99f, BWD_OP(k) * G);
                     const float om = 1.f - al;
                     const float rcp = __builtin_amdgcn_rcpf(om);
@@ -1794,7 +1811,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
 #pragma unroll
                 for (int k = 0; k < 16; k++) {
                     const float G = Gr[k];
-                    const float dot = sDU[k * GS + lane];
+                    const float dot = dv[k];
                     const float al = fminf(0.99f, BWD_OP(k) * G);
                     const float om = 1.f - al;
                     T = T * __builtin_amdgcn_rcpf(om);

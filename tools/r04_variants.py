@@ -25,30 +25,6 @@ V = {
         "            return (float)(off & 1023) * 1e-3f;\n        };")],
     # (probe) backward without the 1/255 error-band lane collection
     "noband": [("                near_m |= lanes_abs_lt(d, 2e-8f);", "")],
-    # candidate: the dot product's MFMA results transposed with permlane swaps instead of through LDS
-    "dotperm": [
-        ("            // dot[k][p] of the group's candidates on MFMA: (16 x C) . (C x 64)\n            if constexpr (!LO) {",
-         "            // dot[k][p] of the group's candidates on MFMA: (16 x C) . (C x 64)\n            float dv[16];\n            (void)dv;\n            if constexpr (!LO) {"),
-        ("#pragma unroll\n                for (int pb = 0; pb < 4; pb++)\n#pragma unroll\n"
-         "                    for (int r = 0; r < 4; r++) sDU[(4 * lg + r) * GS + pb * 16 + li] = acc[pb][r];\n            }",
-         "#pragma unroll\n                for (int r = 0; r < 4; r++) {\n"
-         "                    uint32_t x0 = __float_as_uint(acc[0][r]), x1 = __float_as_uint(acc[1][r]);\n"
-         "                    uint32_t x2 = __float_as_uint(acc[2][r]), x3 = __float_as_uint(acc[3][r]);\n"
-         "                    auto s02 = __builtin_amdgcn_permlane32_swap(x0, x2, false, false);\n"
-         "                    auto s13 = __builtin_amdgcn_permlane32_swap(x1, x3, false, false);\n"
-         "                    auto s01 = __builtin_amdgcn_permlane16_swap(s02[0], s13[0], false, false);\n"
-         "                    auto s23 = __builtin_amdgcn_permlane16_swap(s02[1], s13[1], false, false);\n"
-         "                    dv[0 + r] = __uint_as_float(s01[0]);\n                    dv[4 + r] = __uint_as_float(s01[1]);\n"
-         "                    dv[8 + r] = __uint_as_float(s23[0]);\n                    dv[12 + r] = __uint_as_float(s23[1]);\n"
-         "                }\n            }"),
-        ("                    const float dot = sDU[k * GS + lane];\n                    const float al = fminf(0.99f, BWD_OP(k) * G);\n"
-         "                    const float om = 1.f - al;\n                    const float rcp",
-         "                    const float dot = dv[k];\n                    const float al = fminf(0.99f, BWD_OP(k) * G);\n"
-         "                    const float om = 1.f - al;\n                    const float rcp"),
-        ("                    const float dot = sDU[k * GS + lane];\n                    const float al = fminf(0.99f, BWD_OP(k) * G);\n"
-         "                    const float om = 1.f - al;\n                    T = T * __builtin_amdgcn_rcpf(om);",
-         "                    const float dot = dv[k];\n                    const float al = fminf(0.99f, BWD_OP(k) * G);\n"
-         "                    const float om = 1.f - al;\n                    T = T * __builtin_amdgcn_rcpf(om);")],
 }
 # candidate: the ML forward's gathered language slices (A operand) loaded one 4-candidate step ahead
 V["fwdpf"] = [(
