@@ -303,13 +303,9 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
     auto note = [&](bool ok, int j) {
         if constexpr (ZERO) {
             const uint64_t mk = wave_ballot(ok);
-            const uint32_t lo = (uint32_t)mk, hi = (uint32_t)(mk >> 32);
-            uint32_t keep;   // lane select through M0 (one SGPR operand per VOP3: the value)
-            asm volatile("s_mov_b32 %[keep], m0\n\ts_mov_b32 m0, %[j]\n\t"
-                         "v_writelane_b32 %[d], %[lo], m0\n\tv_writelane_b32 %[e], %[hi], m0\n\t"
-                         "s_mov_b32 m0, %[keep]"
-                         : [d] "+v"(mlo), [e] "+v"(mhi), [keep] "=&s"(keep)
-                         : [lo] "s"(lo), [hi] "s"(hi), [j] "s"(j));
+            const bool mine = lane == j;
+            mlo = mine ? (uint32_t)mk : mlo;
+            mhi = mine ? (uint32_t)(mk >> 32) : mhi;
         }
     };
     uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
