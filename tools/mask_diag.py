@@ -42,7 +42,7 @@ LM = lb[offM + 16 * 8:offM + 16 * 8 + 4 * M * 8].view(np.uint64)
 saved = node.saved_tensors
 image = saved[-1]
 N = t["means3D"].shape[0]
-dec = layout.decode({2: image, 1: saved[-2], 0: saved[-3]}, N, W, H, M)
+dec = {k: v.cpu().numpy() for k, v in layout.decode({2: image, 1: saved[-2], 0: saved[-3]}, N, W, H, M).items()}
 ts = dec["ranges"][:, 0].astype(np.int64)
 ncon = dec["n_contrib"]
 f = np.float32
