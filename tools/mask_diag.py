@@ -70,7 +70,7 @@ for tile in range(T):
             p = f(-0.5) * (f(A[2]) * dx * dx + f(B[0]) * dy * dy) - f(A[3]) * dx * dy
             al = np.minimum(f(0.99), f(B[1]) * np.exp(p.astype(np.float64)).astype(f))
             want = inside & (p <= 0) & (al >= 1 / 255) & (pos < nc)
-            got = (int(LM[base + e]) >> ls) & 1
+            got = (np.uint64(LM[base + e]) >> ls.astype(np.uint64)) & np.uint64(1)
             diff = np.nonzero(want != got.astype(bool))[0]
             tot += 1
             if len(diff):
