@@ -1310,13 +1310,13 @@ __device__ __forceinline__ uint64_t lanes_abs_lt(float v, float bound)
     return m;
 }
 
-// x in the lanes of mask m, 0 elsewhere: one v_cndmask on the SGPR-pair mask
-// (a uniform 64-bit value used as the lane condition directly).
+// x in the lanes of mask m, 0 elsewhere: the uniform 64-bit mask used as the
+// lane condition directly (inverse ballot: one v_cndmask on the SGPR pair; the
+// compiler sees the SGPR read and covers the SALU-write -> VALU-mask-read
+// hazard, which a hand-written v_cndmask in inline asm did not: wrong lanes).
 __device__ __forceinline__ float lanes_select(uint64_t m, float x)
 {
-    float r;
-    asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(x), "s"(m));
-    return r;
+    return __builtin_amdgcn_inverse_ballot_w64(m) ? x : 0.f;
 }
 
 // Per-wave LDS staging of one chunk's candidate geometry (no feature rows).
