@@ -634,15 +634,13 @@ static GradWs grad_ws_layout(int P, int Dd, bool geom, bool lang, bool lang_alig
     return w;
 }
 
-// The backward's per-block candidate lists (RenderArgs::listA/B/lcount/listM):
-// A and B arrays of 4 M entries (block b = 4 tile + sub owns [4 tile_start +
-// sub n_tile, + n_tile)), the 4 T per-block counts, and the per-entry
-// contribution masks (8 B, after 16 leading zero entries: the backward's
-// scalar loads of a 16-candidate window may start before entry 0).
+// The backward's per-block candidate lists (RenderArgs::listA/B/lcount): A and
+// B arrays of 4 M entries (block b = 4 tile + sub owns [4 tile_start + sub n_tile,
+// + n_tile)), then the 4 T per-block counts.
 static size_t block_lists_bytes(size_t M, size_t T)
 {
     if (M == 0 || T == 0) return 0;
-    return 2 * align256(4 * M * 16) + align256(4 * T * 4) + align256((4 * M + 16) * 8);
+    return 2 * align256(4 * M * 16) + align256(4 * T * 4);
 }
 static void set_block_lists(RenderArgs& ra, void* lb, size_t M)
 {
@@ -650,7 +648,6 @@ static void set_block_lists(RenderArgs& ra, void* lb, size_t M)
     ra.listA = (float4*)p;
     ra.listB = (float4*)(p + align256(4 * M * 16));
     ra.lcount = (uint32_t*)(p + 2 * align256(4 * M * 16));
-    ra.listM = (uint64_t*)(p + 2 * align256(4 * M * 16) + align256(4 * (size_t)ra.cam.gx * ra.cam.gy * 4)) + 16;
 }
 
 int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, lsr_alloc_fn alloc, void* ctx,

@@ -104,8 +104,6 @@ struct RenderArgs {
     float4* listA = nullptr;   // the candidate's splat record A {x, y, conic.a, conic.b}
     float4* listB = nullptr;   // {conic.c, opacity, id bits, 0-based tile-list position bits}
     uint32_t* lcount = nullptr;
-    uint64_t* listM = nullptr;  // per entry: the block's pixels (lanes) the candidate contributed to
-                                // in the forward; 16 zero entries precede listM[0]
 };
 hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st);
 

@@ -285,29 +285,15 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
     // ZERO (a backward is pending): the staged candidates also go to this
     // block's list for the backward (RenderArgs::listA), nst entries so far;
     // (mlast, nlast, blast): the last chunk's mask, entries before it, its start
-    // listM: per entry, the 64-bit mask of the block's pixels the candidate
-    // contributed to (built per chunk in mlo / mhi: lane j holds candidate j's)
     ListSink ls;
     uint32_t nst = 0, nlast = 0, blast = rs;
     uint64_t mlast = 0;
-    uint64_t* lmask = nullptr;
-    uint32_t mlo = 0u, mhi = 0u;
     if constexpr (ZERO) {
         if (a.listA) {
             ls.A = a.listA + (size_t)4 * rs + (size_t)wt.sub * (re - rs);
             ls.B = a.listB + (size_t)4 * rs + (size_t)wt.sub * (re - rs);
-            lmask = a.listM + (size_t)4 * rs + (size_t)wt.sub * (re - rs);
         }
     }
-    // candidate j's contributing lanes -> lane j of (mlo, mhi) (j uniform, < 64)
-    auto note = [&](bool ok, int j) {
-        if constexpr (ZERO) {
-            const uint64_t mk = wave_ballot(ok);
-            const bool mine = lane == j;
-            mlo = mine ? (uint32_t)mk : mlo;
-            mhi = mine ? (uint32_t)(mk >> 32) : mhi;
-        }
-    };
     uint32_t next_gid = (rs + lane < re) ? a.point_list[rs + lane] : 0u;
     // SPF: a chunk's ids are loaded two chunks ahead and its records one chunk
     // ahead, issued after the current chunk's feature loads: the staging then
@@ -350,7 +336,6 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
             nlast = nst;
             blast = base;
             nst += (uint32_t)n;
-            mlo = mhi = 0u;
         }
         // Two instances per iteration, branch-free per lane: a lane that
         // skips an instance (exponent cut, alpha < 1/255, saturated or done)
@@ -424,7 +409,6 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                     T = ok ? test_T : T;
                     lastj = ok ? q0 + k : lastj;
                     s4[k] = aT;
-                    if (q0 + k < n) note(ok, q0 + k);
                 }
                 // transpose (lane group, candidate): lane (li, lg) then holds
                 // candidate lg's aT at block pixel 16 pb + li in s4[pb]
@@ -497,7 +481,6 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 }
                 T = ok0 ? test_T : T;
                 lastj = ok0 ? j0 : lastj;
-                note(ok0, j0);
             }
             {
                 const float test_T = T * (1.0f - al1);
@@ -521,12 +504,9 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                 }
                 T = ok1 ? test_T : T;
                 lastj = ok1 ? j1 : lastj;
-                if (two) note(ok1, j1);
             }
         }
         if (lastj >= 0) last = (uint32_t)(base - rs) + 1u + st.src[lastj];
-        if constexpr (ZERO)
-            if (lmask && lane < n) lmask[ls.pos + lane] = ((uint64_t)mhi << 32) | mlo;
         wave_lds_fence();
     }
     if constexpr (ZERO) {
@@ -1310,15 +1290,6 @@ __device__ __forceinline__ uint64_t lanes_abs_lt(float v, float bound)
     return m;
 }
 
-// x in the lanes of mask m, 0 elsewhere: the uniform 64-bit mask used as the
-// lane condition directly (inverse ballot: one v_cndmask on the SGPR pair; the
-// compiler sees the SGPR read and covers the SALU-write -> VALU-mask-read
-// hazard, which a hand-written v_cndmask in inline asm did not: wrong lanes).
-__device__ __forceinline__ float lanes_select(uint64_t m, float x)
-{
-    return __builtin_amdgcn_inverse_ballot_w64(m) ? x : 0.f;
-}
-
 // Per-wave LDS staging of one chunk's candidate geometry (no feature rows).
 // 80 entries: up to 15 candidates carried over from the previous chunk + 64.
 // B.w holds the candidate's tile-list position (int bits) once staged: the
@@ -1443,10 +1414,8 @@ __device__ __forceinline__ void dot_features(const RenderArgs& a, uint32_t gid, 
             af[4 * r + 2] = v.z;
             af[4 * r + 3] = v.w;
         }
-        // lane group 3 repeats blue: its B operand (dL/dout row 3 of the colour
-        // step) is 0, so the product is 0 with no select -- a select here would
-        // make the compiler wait for this gather before phase 1
-        af[NL / 4] = a.rgb[3 * (size_t)gid + min(lg, 2)];
+        const float c = a.rgb[3 * (size_t)gid + min(lg, 2)];
+        af[NL / 4] = lg < 3 ? c : 0.f;
     } else {
 #pragma unroll
         for (int t = 0; t < KS; t++) af[t] = feature_at<NL>(a, gid, 4 * t + lg);
@@ -1575,9 +1544,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
     // LST: entries [lbase, lbase + cnt) of the block's list, back to front
     const uint32_t lcnt = LST ? a.lcount[4 * wt.tile + wt.sub] : 0u;
     const size_t lbase = LST ? (size_t)4 * rs + (size_t)wt.sub * (a.tile_start[wt.tile + 1] - rs) : 0;
-    // the masks through the constant address space: scalar loads (read-only here)
-    const __attribute__((address_space(4))) uint64_t* const lmask =
-        (const __attribute__((address_space(4))) uint64_t*)(uintptr_t)(LST ? a.listM + lbase : nullptr);
     if constexpr (!LST) {
         gid1 = pl_at(wmax - 1 - lane);
         if constexpr (SPF) {
@@ -1745,21 +1711,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             // as a lane mask (scalar ORs), not per-lane flags.
             uint64_t near_m = 0u;
             const int kn_u = __builtin_amdgcn_readfirstlane(kn);   // uniform: scalar compares below
-            // LST: the forward's contribution masks of the group's candidates
-            // (scalar loads; candidate k = entry e0 - k; none past the group)
-            uint64_t mk[16];
-            if constexpr (LST) {
-                // the window of entries e0 - 15 .. e0 in two 64-B scalar loads (the
-                // list buffer has 16 entries before entry 0), then the ones past
-                // the group zeroed with scalar selects
-                const int e0 = (int)lcnt - 1 - (c0 + g0);
-                const auto* w = lmask + (e0 - 15);
-                uint64_t win[16];
-#pragma unroll
-                for (int i = 0; i < 16; i++) win[i] = w[i];
-#pragma unroll
-                for (int k = 0; k < 16; k++) mk[k] = k < kn_u ? win[15 - k] : 0ull;
-            }
             // candidate li's opacity in lane li: phase 2 takes candidate k's
             // from lane k (v_readlane) instead of a broadcast LDS read per k
             const int opl = __float_as_int(SB[g0 + li].y);
@@ -1767,17 +1718,6 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             // GREG: G stays in registers from phase 1 to phase 2 (no LDS round trip)
             float Gr[16];
             (void)Gr;
-            if constexpr (LST) {
-                // the forward's decisions (alpha >= 1/255, not terminated) are the
-                // masks: G where the pair contributed, else 0; no tests here
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    const float4 A = SA[g0 + k];
-                    const float cc = SB[g0 + k].x;
-                    const float power = splat_power(A.z, A.w, cc, A.x - pfx, A.y - pfy);
-                    Gr[k] = lanes_select(mk[k], __builtin_amdgcn_exp2f(power * LSR_LOG2E));
-                }
-            } else {
 #pragma unroll
             for (int k = 0; k < 16; k++) {
                 const float4 A = SA[g0 + k];
@@ -1790,8 +1730,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                 near_m |= lanes_abs_lt(d, 2e-8f);
                 Gr[k] = d >= 0.f ? G : 0.f;
             }
-            }
-            if (!LST && near_m != 0u) {
+            if (near_m != 0u) {
                 // the 1/255 decision must be the forward's: lanes inside the fast
                 // exp's error band re-evaluate with the forward's exp (rare)
 #pragma unroll
@@ -1801,7 +1740,7 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
                     const float4 A = SA[j];
                     const float4 B = SB[j];
                     const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
-                    const bool cj = (__float_as_int(B.w) < last) & !(power > 0.0f) & !(power < B.z);
+                    const bool cj = (__float_as_int(B.w) < last) & !(power > 0.0f) & (LST || !(power < B.z));
                     const float af2 = fminf(0.99f, B.y * __builtin_amdgcn_exp2f(power * LSR_LOG2E));
                     if (cj & (fabsf(af2 - (1.0f / 255.0f)) < 2e-8f)) {
                         const float G = expf_det(power);
