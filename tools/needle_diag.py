@@ -55,23 +55,36 @@ for k in ("xy", "conic_opacity", "depth"):
     print(k, "mismatching Gaussians:", len(bad), "of", int(vis.sum()))
     for i in bad[:3]:
         print("   gpu", a[i], "oracle", b[i])
-# the pair behind the first mismatching pixel: which Gaussians are in that tile's list, their power at the pixel
-t = None
+# the pair behind the first mismatching pixels: the Gaussian the GPU blended (colour / 0.99) and the
+# forward's operations on it, in float32 with fmaf emulated through float64 (exact product)
+col = case["g"]["colors_precomp"].numpy()
+f32 = np.float32
+
+
+def fmaf(a, b, c):
+    return f32(np.float64(a) * np.float64(b) + np.float64(c))
+
+
+shown = 0
 for tt in tiles:
     tx, ty = tt % gx, tt // gx
     sl = (slice(None), slice(ty * 16, ty * 16 + 16), slice(tx * 16, tx * 16 + 16))
-    if (got["color"][sl] != ref_c["color"][sl]).any():
-        t = tt
-        ys, xs = np.nonzero((got["color"][sl] != ref_c["color"][sl]).any(0))
-        py, px = ty * 16 + ys[0], tx * 16 + xs[0]
-        break
-if t is not None:
-    r = culled0["ranges"][t]
+    ys, xs = np.nonzero((got["color"][sl] != ref_c["color"][sl]).any(0))
+    if not len(ys):
+        continue
+    py, px = ty * 16 + ys[0], tx * 16 + xs[0]
+    c = got["color"][:, py, px]
+    r = culled0["ranges"][tt]
     ids = culled0["point_list"][r[0]:r[1]]
-    f = np.float32
-    for i in ids[:8]:
-        x, y = got["xy"][i]
-        ca, cb, cc, o = got["conic_opacity"][i]
-        dx, dy = f(x) - f(px), f(y) - f(py)
-        p = f(-0.5) * (f(ca * dx) * dx + f(f(cc * dy) * dy)) - f(f(cb * dx) * dy)
-        print(f"   id {i} xy {x},{y} conic {ca:.6g},{cb:.6g},{cc:.6g} o {o:.4g} power@({px},{py}) ~ {p:.6g}")
+    best = min(ids, key=lambda i: float(np.abs(col[i] * 0.99 - c).sum()))
+    x, y = got["xy"][best]
+    ca, cb, cc, o = got["conic_opacity"][best]
+    dx, dy = f32(f32(x) - f32(px)), f32(f32(y) - f32(py))
+    inner = fmaf(f32(ca * dx), dx, f32(f32(cc * dy) * dy))
+    p = fmaf(f32(-0.5), inner, -f32(f32(cb * dx) * dy))
+    print(f"px ({px},{py}) gpu colour {c} -> id {best} colour*0.99 {col[best] * 0.99} in-list pos "
+          f"{int(np.nonzero(ids == best)[0][0])}/{len(ids)} xy ({x},{y}) conic ({ca!r},{cb!r},{cc!r}) o {o!r}"
+          f" dx {dx!r} dy {dy!r} inner {inner!r} power {p!r}")
+    shown += 1
+    if shown >= 4:
+        break
