@@ -43,13 +43,17 @@ __device__ __forceinline__ float expf_det(float x)
 
 // Two expf_det at once on packed f32 (v_pk_fma/add/mul: each half rounds
 // exactly as the scalar instruction), bitwise equal to expf_det for
-// x >= -87.  No range guard: the render loops only consume exponents of
-// pairs that passed the power >= cut test, i.e. x in [-5.6, 0]; lanes outside
-// are discarded (their alpha is never selected).
+// x >= -87.  Below, x is clamped to -87 (one v_med3_f32 per half): the result is then
+// ~1e-38 where expf_det returns 0, and every caller rejects both (alpha <
+// 1/255), so the decisions are expf_det's.  The clamp is needed: a staged
+// 8x8 block of a needle splat (2D condition number 1e5+) holds pixels with
+// power of -100 .. -1000, where n = round(x log2 e) < -127 wraps the exponent
+// bits below to a huge positive scale (alpha 0.99 far off the needle).
 typedef float lsr_f32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t lsr_u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ lsr_f32x2 expf_det2(lsr_f32x2 x)
 {
+    x = lsr_f32x2{__builtin_amdgcn_fmed3f(x.x, -87.0f, 1.0e30f), __builtin_amdgcn_fmed3f(x.y, -87.0f, 1.0e30f)};
     const lsr_f32x2 t = __builtin_elementwise_fma(x, lsr_f32x2{1.44269504088896341f, 1.44269504088896341f},
                                                   lsr_f32x2{12582912.0f, 12582912.0f});
     const lsr_f32x2 n = t - lsr_f32x2{12582912.0f, 12582912.0f};
