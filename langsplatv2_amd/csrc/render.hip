@@ -1694,36 +1694,14 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
         constexpr int SGS = LST ? 4 : 1;   // word stride of the id array
         BWD_STAMP(1);
 
-        // FPF: the dot product's feature gathers run one group ahead inside the
-        // chunk (the next group's ids are in the stage already): a group's
-        // gather then has the previous group's phases 1-3 and rows to land,
-        // instead of phase 1 alone (census: the wait for it was most of
-        // "feat + phase 1")
-        // (D <= 16: at D = 32 the 9 extra registers cross 168 VGPRs, 2 waves/SIMD)
-        constexpr bool FPF = LST && !LO && NL <= 16;
-        float afn[KS];
-        (void)afn;
-        if constexpr (FPF) {
-            const int kn0 = min(16, nfull);
-            dot_features<NL, VEC>(a, SG[SGS * (li < kn0 ? li : 0)], lg, afn);
-        }
         for (int g0 = 0; g0 < nfull; g0 += 16) {
             const int kn = min(16, nfull - g0);
             BWD_COUNT(9);
             // A fragments of the dot product: feature 4t+lg of candidate g0+li,
-            // gathered now (FPF: one group earlier), consumed after phase 1
+            // gathered now, consumed after phase 1
             if constexpr (!LO) {
-                if constexpr (FPF) {
-#pragma unroll
-                    for (int t = 0; t < KS; t++) af[t] = afn[t];
-                    if (g0 + 16 < nfull) {
-                        const int kn2 = min(16, nfull - g0 - 16);
-                        dot_features<NL, VEC>(a, SG[SGS * (g0 + 16 + (li < kn2 ? li : 0))], lg, afn);
-                    }
-                } else {
-                    const uint32_t gi = SG[SGS * (g0 + (li < kn ? li : 0))];
-                    dot_features<NL, VEC>(a, gi, lg, af);
-                }
+                const uint32_t gi = SG[SGS * (g0 + (li < kn ? li : 0))];
+                dot_features<NL, VEC>(a, gi, lg, af);
             }
             // phase 1: G of the 16 candidates (0 where the pair does not
             // contribute), independent across candidates; straight-line code.

@@ -69,34 +69,6 @@ V["fwdpf"] = [(
 V["nolst"] = [("    uint8_t* p = (uint8_t*)lb;\n    ra.listA = (float4*)p;",
                "    uint8_t* p = (uint8_t*)lb;\n    return;\n    ra.listA = (float4*)p;", "lsr_api.hip")]
 
-# (probe) phase 1 reads one candidate's record for all 16 (no per-candidate LDS latency)
-V["p1onerec"] = [("""                const float4 A = SA[g0 + k];
-                const float4 B = SB[g0 + k];
-                const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
-                const bool cj = (k < kn_u) && (__float_as_int(B.w) < last) && !(power > 0.0f);""",
-                  """                const float4 A = SA[g0];
-                const float4 B = SB[g0];
-                const float power = splat_power(A.z, A.w, B.x, A.x - pfx + (float)k, A.y - pfy);
-                const bool cj = (k < kn_u) && (__float_as_int(B.w) < last) && !(power > 0.0f);""")]
-# (probe) phase 1 without the exponential
-V["p1noexp"] = [("""                const float G = cj ? __builtin_amdgcn_exp2f(power * LSR_LOG2E) : 0.f;
-                const float d = fminf(0.99f, B.y * G) - (1.0f / 255.0f);
-                near_m |= lanes_abs_lt(d, 2e-8f);""",
-                 """                const float G = cj ? fmaf(power, 0.01f, 1.0f) : 0.f;
-                const float d = fminf(0.99f, B.y * G) - (1.0f / 255.0f);
-                near_m |= lanes_abs_lt(d, 2e-8f);""")]
-# (probe) no phase 1 at all
-V["p1none"] = [("""                const float4 A = SA[g0 + k];
-                const float4 B = SB[g0 + k];
-                const float power = splat_power(A.z, A.w, B.x, A.x - pfx, A.y - pfy);
-                const bool cj = (k < kn_u) && (__float_as_int(B.w) < last) && !(power > 0.0f);
-                // G = 0 for a non-candidate pair: alpha - 1/255 is then far below the band
-                const float G = cj ? __builtin_amdgcn_exp2f(power * LSR_LOG2E) : 0.f;
-                const float d = fminf(0.99f, B.y * G) - (1.0f / 255.0f);
-                near_m |= lanes_abs_lt(d, 2e-8f);
-                Gr[k] = d >= 0.f ? G : 0.f;""",
-                """                Gr[k] = (k < kn_u) && (k < last) ? 0.01f * (float)(k + 1) : 0.f;""")]
-
 # diagnostic: per-phase s_memtime census (tools/bwd_stamps.py)
 V["stamps"] = [('#include "lsr_internal.h"\n\n#include <type_traits>',
                 '#define LSR_BWD_STAMPS 1\n#include "lsr_internal.h"\n\n#include <type_traits>')]
