@@ -249,8 +249,11 @@ __device__ __forceinline__ void zero_backward_accumulators(const RenderArgs& a)
 // measured slower than the VALU blend and is not launched.)
 // MLM (with ML): D below the language set's width NL (masked channels);
 // otherwise D == NL is a compile-time constant (fewer registers).
+// the D = 16 ML form at 6 waves / SIMD (80 VGPRs): its blend is latency bound
+template <int NL, bool ML>
+constexpr int fwd_waves() { return (ML && NL == 16) ? 6 : 1; }
 template <int NL, bool ZERO = false, bool ML = false, bool MLM = false>
-__global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(fwd_waves<NL, ML>()))) k_render_fwd(RenderArgs a)
 {
     if constexpr (ZERO) zero_backward_accumulators(a);
     constexpr int C = 3 + NL;
@@ -362,7 +365,10 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                         fa = Fs[(q0 + lg) * (F4 * 4) + 3 + ch];
                     av[nb] = ((q0 + lg < n) & (!MLM || ch < D)) ? fa : 0.f;
                 }
+                // al[k]: the pair's alpha where it is blended (the lane not done,
+                // exponent <= 0, alpha >= 1/255), else 0; cm[k] the lanes of al != 0
                 float al[4];
+                bool cm[4];
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
                     const int j0 = q0 + 2 * h, e = j0 >> 1;
@@ -375,40 +381,66 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderArgs a)
                     const f32x2 EX = expf_det2(P);
                     const float a0 = fminf(0.99f, OP.x * EX.x), a1 = fminf(0.99f, OP.y * EX.y);
                     // no exponent-cut test: below the cut the 1/255 test rejects the pair
-                    al[2 * h] = ((j0 < n) & !(P.x > 0.0f) & !(a0 < 1.0f / 255.0f)) ? a0 : 0.f;
-                    al[2 * h + 1] = ((j0 + 1 < n) & !(P.y > 0.0f) & !(a1 < 1.0f / 255.0f)) ? a1 : 0.f;
+                    const bool c0 = (j0 < n) & !done & !(P.x > 0.0f) & !(a0 < 1.0f / 255.0f);
+                    const bool c1 = (j0 + 1 < n) & !done & !(P.y > 0.0f) & !(a1 < 1.0f / 255.0f);
+                    al[2 * h] = c0 ? a0 : 0.f;
+                    al[2 * h + 1] = c1 ? a1 : 0.f;
+                    cm[2 * h] = c0;
+                    cm[2 * h + 1] = c1;
                 }
-                // the serial recurrence (the legacy loop's, one candidate at a time)
+                // the serial recurrence.  T never increases, so if no lane's
+                // transmittance after the 4 candidates (computed as if none
+                // terminated) is below 1e-4, none terminated: then a lane with
+                // al = 0 gets aT = 0 and T unchanged with no selects and no
+                // termination tests.  Otherwise (rare) the group runs the legacy
+                // ok0 / term / ok logic.  Bitwise the legacy result either way.
                 float s4[4];
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const float alk = al[k];
-                    const float test_T = T * (1.0f - alk);
-                    const bool ok0 = (alk != 0.f) & !done;
-                    const bool term = ok0 & (test_T < 0.0001f);
-                    done = done | term;
-                    const bool ok = ok0 & !term;
-                    const float aT = ok ? alk * T : 0.f;
-                    // rgb; past the chunk a staged row's (aT = 0 there)
+                // candidate k's rgb (past the chunk a staged row's: aT = 0 there)
+                auto rgb_of = [&](int k) -> float3 {
                     const int kk = min(q0 + k, n - 1);
-                    float f0, f1, f2;
                     if constexpr (SF) {   // the line staged with the candidate
                         const float4 f = st.R[kk];
-                        f0 = f.x;
-                        f1 = f.y;
-                        f2 = f.z;
+                        return make_float3(f.x, f.y, f.z);
                     } else {
                         const float4 f = st.F[kk * F4];
-                        f0 = f.x;
-                        f1 = f.y;
-                        f2 = f.z;
+                        return make_float3(f.x, f.y, f.z);
                     }
-                    acc[0] = fmaf(f0, aT, acc[0]);
-                    acc[1] = fmaf(f1, aT, acc[1]);
-                    acc[2] = fmaf(f2, aT, acc[2]);
-                    T = ok ? test_T : T;
-                    lastj = ok ? q0 + k : lastj;
-                    s4[k] = aT;
+                };
+                // transmittance before each candidate, assuming no termination
+                float Tk[5];
+                Tk[0] = T;
+#pragma unroll
+                for (int k = 0; k < 4; k++) Tk[k + 1] = Tk[k] * (1.0f - al[k]);
+                if (wave_ballot(Tk[4] < 0.0001f) == 0u) {
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const float aT = al[k] * Tk[k];
+                        const float3 f = rgb_of(k);
+                        acc[0] = fmaf(f.x, aT, acc[0]);
+                        acc[1] = fmaf(f.y, aT, acc[1]);
+                        acc[2] = fmaf(f.z, aT, acc[2]);
+                        lastj = cm[k] ? q0 + k : lastj;
+                        s4[k] = aT;
+                    }
+                    T = Tk[4];
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const float alk = al[k];
+                        const float test_T = T * (1.0f - alk);
+                        const bool ok0 = (alk != 0.f) & !done;
+                        const bool term = ok0 & (test_T < 0.0001f);
+                        done = done | term;
+                        const bool ok = ok0 & !term;
+                        const float aT = ok ? alk * T : 0.f;
+                        const float3 f = rgb_of(k);
+                        acc[0] = fmaf(f.x, aT, acc[0]);
+                        acc[1] = fmaf(f.y, aT, acc[1]);
+                        acc[2] = fmaf(f.z, aT, acc[2]);
+                        T = ok ? test_T : T;
+                        lastj = ok ? q0 + k : lastj;
+                        s4[k] = aT;
+                    }
                 }
                 // transpose (lane group, candidate): lane (li, lg) then holds
                 // candidate lg's aT at block pixel 16 pb + li in s4[pb]
