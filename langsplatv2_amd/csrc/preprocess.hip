@@ -99,16 +99,11 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
         }
         o = in.opacities[i];
         if constexpr (SH16) {
-            if (shrow) {   // the row staged in LDS by the caller (k_preprocess_sh16)
+            const float4* src = reinterpret_cast<const float4*>(in.shs) + (size_t)i * 12;
 #pragma unroll
-                for (int k = 0; k < 48; k++) sh[k] = shrow[k];
-            } else {
-                const float4* src = reinterpret_cast<const float4*>(in.shs) + (size_t)i * 12;
-#pragma unroll
-                for (int k = 0; k < 12; k++) {
-                    const float4 v = src[k];
-                    sh[4 * k] = v.x; sh[4 * k + 1] = v.y; sh[4 * k + 2] = v.z; sh[4 * k + 3] = v.w;
-                }
+            for (int k = 0; k < 12; k++) {
+                const float4 v = src[k];
+                sh[4 * k] = v.x; sh[4 * k + 1] = v.y; sh[4 * k + 2] = v.z; sh[4 * k + 3] = v.w;
             }
         }
         // keep the loads here: the compiler otherwise sinks them past the
@@ -216,35 +211,13 @@ __global__ void __launch_bounds__(256) k_preprocess(Cam c, lsr_inputs in, uint8_
     preprocess_one<SH16, COV>(c, in, geom, radii, i, nullptr);
 }
 
-// SH16 with the 64 rows of a wave staged through LDS by coalesced float4 loads
-// (stage_sh_rows, as the backward's k_preprocess_bwd_sh16) instead of 12
-// lane-strided float4 loads per thread.
-template <bool COV>
-__global__ void __launch_bounds__(64) k_preprocess_sh16(Cam c, lsr_inputs in, uint8_t* __restrict__ geom,
-                                                        int32_t* __restrict__ radii)
-{
-    __shared__ float shl[64 * LSR_SH_ROW];
-    const int b0 = blockIdx.x * 64, lane = threadIdx.x;
-    const int cnt = min(64, in.P - b0);
-    stage_sh_rows(shl, in.shs, b0, cnt, lane);
-    __syncthreads();
-    if (lane < cnt) preprocess_one<true, COV>(c, in, geom, radii, b0 + lane, shl + lane * LSR_SH_ROW);
-}
-
-#ifndef LSR_PRE_STAGE
-#define LSR_PRE_STAGE 1
-#endif
 hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, int32_t* radii, hipStream_t st)
 {
     if (in.P == 0) return hipSuccess;
     const bool sh16 = in.shs && in.max_coeffs == 16 && ((uintptr_t)in.shs % 16 == 0);
     const bool cov = in.cov3D_precomp != nullptr;
     const dim3 g((in.P + 255) / 256);
-    if (LSR_PRE_STAGE && sh16 && !in.colors_precomp) {
-        const dim3 g64((in.P + 63) / 64);
-        if (cov) k_preprocess_sh16<true><<<g64, 64, 0, st>>>(c, in, geom, radii);
-        else k_preprocess_sh16<false><<<g64, 64, 0, st>>>(c, in, geom, radii);
-    } else if (sh16 && cov) k_preprocess<true, true><<<g, 256, 0, st>>>(c, in, geom, radii);
+    if (sh16 && cov) k_preprocess<true, true><<<g, 256, 0, st>>>(c, in, geom, radii);
     else if (sh16) k_preprocess<true, false><<<g, 256, 0, st>>>(c, in, geom, radii);
     else if (cov) k_preprocess<false, true><<<g, 256, 0, st>>>(c, in, geom, radii);
     else k_preprocess<false, false><<<g, 256, 0, st>>>(c, in, geom, radii);
