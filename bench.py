@@ -130,6 +130,8 @@ def pmc_traffic(stage, prefix="r"):
     return int(sum(v["traffic_bytes"] for v in ks)), os.path.relpath(files[-1], ROOT)
 
 
+ROOF_EVERY = 4   # timed-region steps per event-bracketed launch of the roofline kernel
+
 STAGE_KERNEL = {"render_bwd": "k_render_bwd_mf", "render_fwd": "k_render_fwd", "preprocess": "k_preprocess",
                 "preprocess_bwd": "k_preprocess_bwd", "bin_scatter": "k_bin_scatter", "bin_count": "k_bin_count",
                 "tile_sort": "k_tile_sort"}
@@ -357,7 +359,8 @@ def main_forward_replicas(args, world, rank, dev) -> int:
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        _lib.profile_enable(i % ROOF_EVERY == 0)   # as in the training bench
         step()
     torch.cuda.synchronize()
     if world > 1:
@@ -528,7 +531,10 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        # the dominant kernel is bracketed by events on every ROOF_EVERY-th step
+        # of the timed region (each bracket idles the stream a few us)
+        _lib.profile_enable(i % ROOF_EVERY == 0)
         step()
     torch.cuda.synchronize()
     if world > 1:
