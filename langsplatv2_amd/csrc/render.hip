@@ -1333,13 +1333,21 @@ struct WaveStageG {
 };
 
 // LST: the block's candidate list (written by the forward, RenderArgs::listA/B)
-// copied into LDS by LDS-DMA, 64 entries per chunk, two buffers (the next
-// chunk lands while this one is processed).  B = {conic.c, opacity, id bits,
-// 0-based position bits}.
+// copied into LDS by LDS-DMA, one 16-candidate group per chunk, two buffers
+// (the next chunk lands while this one is processed).  B = {conic.c, opacity,
+// id bits, 0-based position bits}.  16-entry chunks keep the D = 16 kernel's
+// LDS at 10240 B, which with <= 128 VGPRs (amdgpu_waves_per_eu(4) below) lets
+// 4 waves per SIMD reside instead of 3 (64-entry chunks: 12096 B): backward
+// 0.503 -> 0.469 ms at cfg3.
+#define LSR_LST_CHUNK 16
 struct WaveStageL {
-    float4 A[128];
-    float4 B[128];
+    float4 A[2 * LSR_LST_CHUNK];
+    float4 B[2 * LSR_LST_CHUNK];
 };
+// waves per SIMD the MFMA backward is compiled for: 4 for the list-driven
+// D = 16 kernel (the headline's), the launch-bounds floor otherwise
+template <int NL, bool LD, bool LST>
+constexpr int bwd_waves() { return (LST && LD && NL == 16) ? 4 : LSR_MF_WAVES; }
 
 // LDS-DMA of one 16-B row part per lane: lane l's bytes land at lds + 16 l (an
 // LDS-DMA writes wave-uniform M0 + lane x size).  Inline asm with M0 saved and
@@ -1486,7 +1494,7 @@ __device__ unsigned long long g_bwd_stamps[16];
 // gathers, no block tests, no compaction; the list chunks arrive by LDS-DMA one
 // chunk ahead.  The same candidates in the same order: results unchanged.
 template <int NL, bool LO = false, bool LD = false, bool SP = false, bool LST = false>
-__global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArgs b)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_waves<NL, LD, LST>()))) k_render_bwd_mf(RenderBwdArgs b)
 {
     static_assert(!(LST && SP), "the sparse-input backward follows the quick forward (no lists)");
     static_assert(!LO || NL > 0, "language-only backward needs D > 0");
@@ -1591,13 +1599,16 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
             st.gid[e] = 0u;
         }
     }
-    // LST: chunk c0's entries lbase + lcnt - 1 - (c0 + lane) -> stl buffer `off`
-    // (lanes past the list copy entry 0: finite, and past the group's end)
+    // LST: chunk c0's entries lbase + lcnt - 1 - (c0 + lane) -> stl buffer `off`,
+    // lanes < LSR_LST_CHUNK (lanes past the list copy entry 0: finite, and
+    // past the group's end)
     auto list_dma = [&](int c0, int off) {
         const int e = (int)lcnt - 1 - (c0 + lane);
         const size_t src = lbase + (size_t)(e >= 0 ? e : 0);
-        glds16(a.listA + src, stl.A + off);
-        glds16(a.listB + src, stl.B + off);
+        if (lane < LSR_LST_CHUNK) {
+            glds16(a.listA + src, stl.A + off);
+            glds16(a.listB + src, stl.B + off);
+        }
     };
 
     float dr0 = 0.f, dr1 = 0.f, dr2 = 0.f;   // the lane's own pixel's RGB dL/dout (0 outside the image)
@@ -1679,26 +1690,28 @@ __global__ void __launch_bounds__(64, LSR_MF_WAVES) k_render_bwd_mf(RenderBwdArg
         sBc[lane] = dr2;
     }
     // LST: a chunk's DMA is waited for with vmcnt(N), N = a lower bound of the
-    // VMEM operations the previous (full, 4-group) chunk issued after it -- its
-    // buffer atomics, GRL x 4 per group (unconditional, never merged; the
+    // VMEM operations the previous (full, one-group) chunk issued after it --
+    // its buffer atomics, GRL x 4 per group (unconditional, never merged; the
     // feature gathers are not counted) -- so the wait does not drain them
     constexpr int OPG = GRL * 4;
-    constexpr int CHUNK_OPS = 4 * OPG < 63 ? 4 * OPG : 63;
+    constexpr int CGR = LSR_LST_CHUNK / 16;   // groups per list chunk
+    constexpr int CHUNK_OPS = CGR * OPG < 63 ? CGR * OPG : 63;
+    constexpr int CH = LST ? LSR_LST_CHUNK : 64;   // candidates per chunk
     if constexpr (LST) list_dma(0, 0);
     BWD_STAMP(0);
     const int cend = LST ? (int)lcnt : wmax;
-    for (int c0 = 0; c0 < cend; c0 += 64) {
+    for (int c0 = 0; c0 < cend; c0 += CH) {
         int n, nfull;
         const float4* SA;
         const float4* SB;
         const uint32_t* SG;
         BWD_COUNT(8);
         if constexpr (LST) {
-            const int off = (c0 >> 6 & 1) * 64;
+            const int off = (c0 / CH & 1) * CH;
             if (c0 == 0 || !buf_atom) wait_vmcnt<0>();
             else wait_vmcnt<CHUNK_OPS>();
-            if (c0 + 64 < cend) list_dma(c0 + 64, 64 - off);
-            n = nfull = min(64, cend - c0);
+            if (c0 + CH < cend) list_dma(c0 + CH, CH - off);
+            n = nfull = min(CH, cend - c0);
             SA = stl.A + off;
             SB = stl.B + off;
             SG = reinterpret_cast<const uint32_t*>(stl.B + off) + 2;   // B.z, stride 4 words
