@@ -138,14 +138,17 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #endif
 template <int NL>
 constexpr bool fwd_sfeat() { return LSR_FWD_SFEAT > 0 && NL >= LSR_FWD_SFEAT; }
+// SF (the ML form) holds NE = 68 entries: up to 3 candidates of a partial
+// group carried over from the previous chunk + 64 (with their list positions).
 template <int F4, bool SF>
 struct WaveStageP {
-    f32x2 X[32], Y[32], CA[32], CB[32], CC[32], OP[32];
+    static constexpr int NE = SF ? 68 : 64;
+    f32x2 X[NE / 2], Y[NE / 2], CA[NE / 2], CB[NE / 2], CC[NE / 2], OP[NE / 2];
     float4 F[SF ? 1 : 64 * F4];
-    uint32_t gid[SF ? 64 : 1];
-    float4 R[SF ? 64 : 1];   // SF: the candidates' RGB (read by the ML blend as one broadcast line)
-    uint8_t src[64];   // the staging lane (position = chunk base + src + 1): 192 B less LDS than
-                       // the positions themselves, so 6 instead of 5 waves/SIMD at D = 16
+    uint32_t gid[SF ? NE : 1];
+    float4 R[SF ? NE : 1];   // SF: the candidates' RGB (read by the ML blend as one broadcast line)
+    uint32_t pos[SF ? NE : 1];   // SF: the entry's 1-based list position
+    uint8_t src[SF ? 1 : 64];    // !SF: the staging lane (position = chunk base + src + 1)
 };
 
 // The backward's per-block candidate list (RenderArgs::listA/B): with LST the
@@ -162,8 +165,11 @@ template <int NL, int F4, bool LST = false>
 __device__ __forceinline__ int stage_candidates_p_rec(WaveStageP<F4, fwd_sfeat<NL>()>& st, bool valid, uint32_t gid,
                                                       int pos, int bx, int by, float4 A, float4 B,
                                                       const float* __restrict__ rgb, const float* __restrict__ lang,
-                                                      int D, const ListSink& ls = ListSink(), uint64_t* mo = nullptr)
+                                                      int D, const ListSink& ls = ListSink(), uint64_t* mo = nullptr,
+                                                      int off = 0)
 {
+    constexpr bool SF = fwd_sfeat<NL>();
+    constexpr int NE = WaveStageP<F4, SF>::NE;
     const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), bx, by) &&
                     block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, bx, by);
     const uint64_t m = wave_ballot(ok);
@@ -177,19 +183,24 @@ __device__ __forceinline__ int stage_candidates_p_rec(WaveStageP<F4, fwd_sfeat<N
                 ls.B[ls.pos + r] = make_float4(B.x, B.y, __uint_as_float(gid), __int_as_float(pos - 1));
             }
         }
-        float* base = reinterpret_cast<float*>(&st) + (r & 1);
-        const int e = (r >> 1) * 2;
-        base[0 * 64 + e] = A.x;
-        base[1 * 64 + e] = A.y;
-        base[2 * 64 + e] = A.z;
-        base[3 * 64 + e] = A.w;
-        base[4 * 64 + e] = B.x;
-        base[5 * 64 + e] = B.y;
-        st.src[r] = (uint8_t)(threadIdx.x & 63);
-        if constexpr (fwd_sfeat<NL>()) {
-            st.gid[r] = gid;
-            st.R[r] = make_float4(rgb[3 * (size_t)gid], rgb[3 * (size_t)gid + 1], rgb[3 * (size_t)gid + 2], 0.f);
-        } else
+        // entry i = off + r (SF: after the carried entries)
+        const int i = off + r;
+        float* base = reinterpret_cast<float*>(&st) + (i & 1);
+        const int e = (i >> 1) * 2;
+        base[0 * NE + e] = A.x;
+        base[1 * NE + e] = A.y;
+        base[2 * NE + e] = A.z;
+        base[3 * NE + e] = A.w;
+        base[4 * NE + e] = B.x;
+        base[5 * NE + e] = B.y;
+        if constexpr (SF) {
+            st.pos[i] = (uint32_t)pos;
+            st.gid[i] = gid;
+            st.R[i] = make_float4(rgb[3 * (size_t)gid], rgb[3 * (size_t)gid + 1], rgb[3 * (size_t)gid + 2], 0.f);
+        } else {
+            st.src[r] = (uint8_t)(threadIdx.x & 63);
+        }
+        if constexpr (!SF)
             stage_features<NL, F4>(&st.F[r * F4], rgb, lang, D, gid);
     }
     wave_lds_fence();
@@ -201,14 +212,14 @@ __device__ __forceinline__ int stage_candidates_p(WaveStageP<F4, fwd_sfeat<NL>()
                                                   int by, const float4* __restrict__ splatA,
                                                   const float4* __restrict__ splatB, const float* __restrict__ rgb,
                                                   const float* __restrict__ lang, int D, const ListSink& ls = ListSink(),
-                                                  uint64_t* mo = nullptr)
+                                                  uint64_t* mo = nullptr, int off = 0)
 {
     float4 A = make_float4(0.f, 0.f, 0.f, 0.f), B = A;
     if (valid) {
         A = splatA[gid];
         B = splatB[gid];
     }
-    return stage_candidates_p_rec<NL, F4, LST>(st, valid, gid, pos, bx, by, A, B, rgb, lang, D, ls, mo);
+    return stage_candidates_p_rec<NL, F4, LST>(st, valid, gid, pos, bx, by, A, B, rgb, lang, D, ls, mo, off);
 }
 
 // The backward's accumulators (RenderArgs::zero; lsr_fwd_out.grad_ws): a
@@ -311,6 +322,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(fwd_wav
         A1 = a.splatA[next_gid];
         B1 = a.splatB[next_gid];
     }
+    // ML: a partial group (carry < 4 entries) waits in the stage for the next
+    // chunk's candidates, so every group but the list's last is full: the
+    // blend's per-group work is paid per 4 candidates, not per chunk remainder.
+    // The blend is per candidate in list order either way (bit-identical).
+    int carry = 0;
     for (uint32_t base = rs; base < re; base += 64) {
         if (wave_ballot(!done) == 0) break;
         const uint32_t idx = base + lane;
@@ -322,7 +338,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(fwd_wav
         if constexpr (FSPF) {
             const float4 Ac = A1, Bc = B1;
             n = stage_candidates_p_rec<NL, F4, ZERO>(st, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, Ac, Bc, a.rgb,
-                                                     a.lang, D, ls, &mchunk);
+                                                     a.lang, D, ls, &mchunk, ML ? carry : 0);
             next_gid = next_gid2;
             A1 = a.splatA[next_gid];
             B1 = a.splatB[next_gid];
@@ -332,7 +348,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(fwd_wav
         } else {
             next_gid = (idx + 64 < re) ? a.point_list[idx + 64] : 0u;
             n = stage_candidates_p<NL, F4, ZERO>(st, valid, gid, (int)(idx - rs) + 1, pm.bx, pm.by, a.splatA,
-                                                 a.splatB, a.rgb, a.lang, D, ls, &mchunk);
+                                                 a.splatB, a.rgb, a.lang, D, ls, &mchunk, ML ? carry : 0);
         }
         if constexpr (ZERO) {
             mlast = mchunk;
@@ -349,7 +365,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(fwd_wav
         if constexpr (ML) {
             const int lg = lane >> 4, li = lane & 15;
             const float* const Fs = reinterpret_cast<const float*>(st.F);
-            for (int q0 = 0; q0 < n; q0 += 4) {
+            n += carry;   // the stage's entries: carried + this chunk's
+            // full groups only, except in the list's last chunk
+            const int nproc = (base + 64 >= re) ? n : (n & ~3);
+            int q0 = 0;
+            for (; q0 < nproc; q0 += 4) {
                 if (wave_ballot(!done) == 0) break;
                 // A operand: language channel 16 nb + li of candidate q0 + lg
                 // (0 past the chunk) -- from the staged rows, or (SF) gathered
@@ -466,6 +486,30 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(fwd_wav
                     for (int nb = 0; nb < MLB; nb++)
                         mlacc[nb][pb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[nb], s4[pb], mlacc[nb][pb], 0, 0, 0);
             }
+            if constexpr (SF) {
+                if (lastj >= 0) last = st.pos[lastj];
+                lastj = -1;
+                // the partial group's entries [q0, n) -> [0, carry) (q0 >= 4 when
+                // they move: no overlap; a wave's LDS accesses complete in order)
+                carry = n - q0;
+                if (q0 > 0 && carry > 0) {
+                    if (lane < carry) {
+                        const int i = q0 + lane;
+                        float* fb = reinterpret_cast<float*>(&st);
+                        constexpr int NE = WaveStageP<F4, SF>::NE;
+                        float v[6];
+#pragma unroll
+                        for (int f = 0; f < 6; f++) v[f] = fb[f * NE + i];
+                        const uint32_t pv = st.pos[i], gv = st.gid[i];
+                        const float4 rv = st.R[i];
+#pragma unroll
+                        for (int f = 0; f < 6; f++) fb[f * NE + lane] = v[f];
+                        st.pos[lane] = pv;
+                        st.gid[lane] = gv;
+                        st.R[lane] = rv;
+                    }
+                }
+            }
         } else
         for (int j0 = 0; j0 < n; j0 += 2) {
             if (wave_ballot(!done) == 0) break;
@@ -538,7 +582,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(fwd_wav
                 lastj = ok1 ? j1 : lastj;
             }
         }
-        if (lastj >= 0) last = (uint32_t)(base - rs) + 1u + st.src[lastj];
+        if constexpr (!ML) {
+            if (lastj >= 0) last = (uint32_t)(base - rs) + 1u + st.src[lastj];
+        }
         wave_lds_fence();
     }
     if constexpr (ZERO) {
