@@ -26,6 +26,21 @@ dev = torch.device("cuda:0")
 cam = make_camera(cfg["W"], cfg["H"])
 g0 = make_gaussians(cfg["N"], cam, seed=0, sh_degree=3, lang_dim=D)
 keys = ("means3D", "shs", "opacities", "scales", "rotations", "language_feature_precomp")
+if os.environ.get("LSR_SPATIAL"):
+    # layout probe: the same Gaussians in a spatial order (3-D Morton code of the
+    # means, 10 bits per axis) instead of the generator's random order
+    m = g0["means3D"].double()
+    lo, hi = m.min(0).values, m.max(0).values
+    q = ((m - lo) / (hi - lo).clamp_min(1e-12) * 1023).long().clamp(0, 1023)
+
+    def spread(v):
+        out = torch.zeros_like(v)
+        for b in range(10):
+            out |= ((v >> b) & 1) << (3 * b)
+        return out
+    code = spread(q[:, 0]) | (spread(q[:, 1]) << 1) | (spread(q[:, 2]) << 2)
+    perm = torch.argsort(code)
+    g0 = {k: (v[perm] if isinstance(v, torch.Tensor) and v.shape[:1] == perm.shape else v) for k, v in g0.items()}
 g = {k: g0[k].to(dev).requires_grad_(True) for k in keys}
 g["means2D"] = torch.zeros_like(g["means3D"], requires_grad=True)
 r = GaussianRasterizer(bench.settings(cam, dev, 3, True))
