@@ -85,6 +85,28 @@ def test_backward_vs_oracle(name, gpu, oracle_lib):
         assert_grad_close("language_feature_precomp", got["grad_language_feature_precomp"], rb["dlang"])
 
 
+@pytest.mark.parametrize("N", [1, 5, 16, 23, 40, 70])
+def test_block_list_chunk_boundaries(N, gpu, oracle_lib):
+    """One 16x16 tile (four 8x8 blocks) at D = 16: the backward reads each
+    block's candidate list in chunks of one 16-candidate group
+    (render.hip LSR_LST_CHUNK) with a counted DMA wait, so list lengths below,
+    at and across multiples of 16 (and a lone candidate) must give the
+    oracle's gradients."""
+    case = make_case(N=N, W=16, H=16, sh_degree=None, lang_dim=16, seed=40 + N)
+    pb = oracle_problem(case)
+    ref = oracle_lib.forward(pb)
+    rng = np.random.default_rng(2)
+    dcol = rng.standard_normal((3, 16, 16)).astype(np.float32)
+    dlang = rng.standard_normal((16, 16, 16)).astype(np.float32)
+    rb = oracle_lib.backward(pb, ref, dcol, dlang)
+    got = run_gpu_fwd_bwd(case, gpu, dcol, dlang)
+    np.testing.assert_array_equal(got["color"], ref["color"])
+    assert_grad_close("means2D", got["grad_means2D"], rb["dmean2D"])
+    assert_grad_close("opacities", got["grad_opacities"], rb["dopacity"][:, None])
+    assert_grad_close("colors_precomp", got["grad_colors_precomp"], rb["dcolor"])
+    assert_grad_close("language_feature_precomp", got["grad_language_feature_precomp"], rb["dlang"])
+
+
 @pytest.mark.parametrize("name", ["sh3_lang16_ragged", "rgb_lang3", "cov_precomp_lang8", "lang64_feature_mode",
                                   "yaw_sh3_lang32"])
 def test_language_only_backward(name, gpu, oracle_lib):
