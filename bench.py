@@ -217,35 +217,47 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline(cam, gcpu, D):
+def cpu_baseline(cam, gcpu, D, cfg_name="cfg3", backward=True, tile_sample=None):
     """The oracle (oracle/lsr_oracle.c: the naive per-pixel serial blend, per-tile loops) on
-    the host's cores, the WHOLE frame: preprocess + binning (single-threaded in the oracle),
-    render forward over all tiles on `threads` OpenMP threads, render backward on the same
-    threads (fp64 atomic accumulation) + preprocess backward.  kind "port": the reference's
-    CUDA rasterizer source is absent, this is its restatement."""
+    the host's cores, the WHOLE frame (or, with `tile_sample`, that many seeded tiles, the
+    render time scaled by T / sample -- flagged extrapolated): preprocess + binning
+    (single-threaded in the oracle), render forward over the tiles on `threads` OpenMP
+    threads, and with `backward` the render backward on the same threads (fp64 atomic
+    accumulation) + preprocess backward.  kind "port": the reference's CUDA rasterizer
+    source is absent, this is its restatement."""
     from oracle import oracle as O
     O.build()
     threads = host_threads()
     pb = O.Problem(cam, gcpu)
+    T = pb.gx * pb.gy
+    tiles = None
+    if tile_sample is not None and tile_sample < T:
+        tiles = np.sort(np.random.default_rng(0).choice(T, size=tile_sample, replace=False)).astype(np.int32)
+    scale = T / len(tiles) if tiles is not None else 1.0
     rng = np.random.default_rng(0)
     dcol = rng.standard_normal((3, pb.H, pb.W)).astype(np.float32)
     dlang = rng.standard_normal((pb.D, pb.H, pb.W)).astype(np.float32) if pb.D else None
     t0 = time.perf_counter()
     O.forward(pb, nthreads=threads, tiles=np.zeros(0, np.int32))   # preprocess + binning only
     t1 = time.perf_counter()
-    f = O.forward(pb, nthreads=threads)
+    f = O.forward(pb, nthreads=threads, tiles=tiles)
     t2 = time.perf_counter()
-    O.backward(pb, f, dcol, dlang, nthreads=threads)
+    if backward:
+        O.backward(pb, f, dcol, dlang, tiles=tiles, nthreads=threads)
     t3 = time.perf_counter()
     t_pre_bin = t1 - t0
-    t_fwd = t2 - t1
-    t_bwd = t3 - t2
+    # the render part of the forward (after preprocess + binning) scales with the tiles
+    t_fwd = t_pre_bin + (t2 - t1 - t_pre_bin) * scale
+    t_bwd = (t3 - t2) * scale
     t_frame = t_fwd + t_bwd
+    what = "whole" if tiles is None else f"{len(tiles)} of {T} tiles (x{scale:.1f}, extrapolated) of the"
     return dict(value=round(1.0 / t_frame, 5), unit="frames/s", cores=threads, kind="port",
                 cpu_model=cpu_model(), host_cpus=os.cpu_count(),
-                sample=f"whole cfg3 frame, oracle/lsr_oracle.c on {threads} OpenMP threads: forward {t_fwd:.2f}s "
-                       f"(of which preprocess + binning {t_pre_bin:.2f}s, single-threaded), backward {t_bwd:.2f}s "
-                       f"(render bwd on {threads} threads + preprocess bwd)",
+                sample=f"{what} {cfg_name} frame, oracle/lsr_oracle.c on {threads} OpenMP threads: forward {t_fwd:.2f}s "
+                       f"(of which preprocess + binning {t_pre_bin:.2f}s, single-threaded)"
+                       + (f", backward {t_bwd:.2f}s (render bwd on {threads} threads + preprocess bwd)" if backward else
+                          ", forward only"),
+                extrapolated=tiles is not None,
                 seconds_per_frame=round(t_frame, 3), stages_s=dict(preprocess_binning=round(t_pre_bin, 3),
                                                                   forward=round(t_fwd, 3), backward=round(t_bwd, 3)))
 
@@ -340,31 +352,44 @@ def dry_run(world, rank, config=3) -> int:
 # --config 3: the headline (BASELINE metric) — fwd+bwd, views sharded, RCCL gradient exchange.
 # --config 5: BASELINE configs[4] — forward only, replicas only (every rank renders its own
 #             view of the replicated 5M-Gaussian scene; no data-path collective).
-CONFIG_MODES = {3: "fwd+bwd, views sharded + RCCL all-reduce of gradients",
+CONFIG_MODES = {1: "fwd+bwd, views sharded + gradient all-reduce (BASELINE configs[0], plumbing size)",
+                2: "forward only, replicas (no collective)",
+                3: "fwd+bwd, views sharded + RCCL all-reduce of gradients",
                 5: "forward only, replicas (no collective)"}
+FWD_METRIC = {2: "frames/s fwd @ 100k Gaussians 800x800 3+3ch (BASELINE configs[1], replicas)",
+              5: "frames/s fwd @ 5M Gaussians 4K 3+32ch (BASELINE configs[4], replicas)"}
+FWD_WORKLOAD = {2: "BASELINE cfg2: 100k Gaussians, 800x800, RGB colours + 3 language channels, forward only; "
+                   "1 view per GPU, replicas (no collective)",
+                5: "BASELINE cfg5: 5M Gaussians, 3840x2160, SH deg 3 + 32 dense language channels, "
+                   "forward only; 1 view per GPU, replicas (no collective)"}
+# CPU-baseline tile sample per forward config (None = the whole frame; cfg5's whole
+# frame would take minutes of oracle time on the box's 16 threads)
+FWD_CPU_TILES = {2: None, 5: 256}
 
 
 def main_forward_replicas(args, world, rank, dev) -> int:
-    """BASELINE configs[4]: 5M Gaussians, 3840x2160, SH degree 3 + 32 dense language
-    channels, forward only; one view per rank (yaw within +-20 degrees), Gaussians replicated,
-    nothing exchanged.  value = frames rendered by all ranks / max-over-ranks time."""
+    """The forward-only BASELINE configs: configs[1] (cfg2: 100k Gaussians, 800x800, RGB
+    colours + 3 language channels) and configs[4] (cfg5: 5M Gaussians, 3840x2160, SH degree 3
+    + 32 dense language channels); one view per rank (yaw within +-20 degrees), Gaussians
+    replicated, nothing exchanged.  value = frames rendered by all ranks / max-over-ranks
+    time."""
     cfg = CONFIGS[args.config]
     N, W, H, D, deg = cfg["N"], cfg["W"], cfg["H"], cfg["lang_dim"], cfg["sh_degree"]
     yaw = dp.rank_yaw(rank, world)
     cam0 = make_camera(W, H)
     cam = make_camera(W, H, yaw_deg=yaw)
     gcpu = make_gaussians(N, cam0, seed=0, sh_degree=deg, lang_dim=D)
-    keys = ("means3D", "shs", "opacities", "scales", "rotations", "language_feature_precomp")
+    keys = [k for k in ("means3D", "shs", "colors_precomp", "opacities", "scales", "rotations",
+                        "language_feature_precomp") if k in gcpu]
     g = {k: gcpu[k].to(dev) for k in keys}
     g["means2D"] = torch.zeros_like(g["means3D"])
-    rs = settings(cam, dev, deg, True)
+    rs = settings(cam, dev, deg or 0, D > 0)
     rast = GaussianRasterizer(rs)
+    kw = {k: g[k] for k in keys if k not in ("means3D", "opacities")}
 
     def step():
         with torch.no_grad():
-            return rast(means3D=g["means3D"], means2D=g["means2D"], opacities=g["opacities"], shs=g["shs"],
-                        language_feature_precomp=g["language_feature_precomp"], scales=g["scales"],
-                        rotations=g["rotations"])
+            return rast(means3D=g["means3D"], means2D=g["means2D"], opacities=g["opacities"], **kw)
 
     for _ in range(args.warmup):
         step()
@@ -400,18 +425,20 @@ def main_forward_replicas(args, world, rank, dev) -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)   # timing only, not on the data path
         elapsed = float(t.item())
     if rank == 0:
-        bytes_, info = algorithmic_bytes(g, rs, D, 48)
+        S = 3 * (deg + 1) ** 2 if deg is not None else 0
+        bytes_, info = algorithmic_bytes(g, rs, D, S)
         dom_ms = dom_ms_s / dom_calls if dom_calls else 0.0
         dom_gbps = bytes_[dom] / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
         step_ms = elapsed / args.steps * 1e3
         fwd_keys = ("preprocess", "bin_count", "scan_tile_counts", "bin_scatter", "tile_sort", "render_fwd")
-        traffic, traffic_src = pmc_traffic(dom, prefix="cfg5_r")
+        pre = f"cfg{args.config}_r"
+        traffic, traffic_src = pmc_traffic(dom, prefix=pre)
         # §8d charges every instance its 4C-byte feature row (M * 140 B at C = 35), which the
         # kernel re-reads from L2: the algorithmic rate exceeds the HBM peak, so the HBM
         # roofline here is the MEASURED traffic (PMC) over the launch time
         meas_gbps = traffic / (dom_ms * 1e-3) / 1e9 if (traffic and dom_ms > 0) else None
         out = {
-            "metric": "frames/s fwd @ 5M Gaussians 4K 3+32ch (BASELINE configs[4], replicas)",
+            "metric": FWD_METRIC[args.config],
             "value": round(world * args.steps / elapsed, 3),
             "unit": "frames/s",
             "n_gpus": world,
@@ -424,8 +451,7 @@ def main_forward_replicas(args, world, rank, dev) -> int:
             "dtype": "f32",
             "data": "synthetic (seeded; SURVEY.md §8d generator)",
             "config": {
-                "workload": "BASELINE cfg5: 5M Gaussians, 3840x2160, SH deg 3 + 32 dense language channels, "
-                            "forward only; 1 view per GPU, replicas (no collective)",
+                "workload": FWD_WORKLOAD[args.config],
                 "gaussians": N, "width": W, "height": H, "lang_dim": D, "sh_degree": deg,
                 "global_batch": world, "parallelism": f"replicas x{world}" if world > 1 else "single GPU",
             },
@@ -440,16 +466,19 @@ def main_forward_replicas(args, world, rank, dev) -> int:
                 "algorithmic_bytes_per_launch": int(bytes_[dom]),
                 "algorithmic_GBps": round(dom_gbps, 1),
                 "bytes_formula": "SURVEY.md §8d (bench.py:algorithmic_bytes)",
-                "note": "the §8d bytes charge every instance its 4C-byte feature row (M*4C, most of the bytes "
-                        "at C = 35), which the kernel re-reads from L2, so the algorithmic rate exceeds the "
-                        "HBM peak and is not an HBM fraction; the kernel is VALU/MFMA-issue bound (`issue`)",
-                "issue": pmc_issue(dom, prefix="cfg5_r"),
+                "note": "the §8d bytes charge every instance its 4C-byte feature row (M*4C), which the kernel "
+                        "re-reads from L2, so the algorithmic rate can exceed the HBM peak and is not an HBM "
+                        "fraction; the kernel is VALU/MFMA-issue bound (`issue`)",
+                "issue": pmc_issue(dom, prefix=pre),
                 "ms_per_launch": round(dom_ms, 4), "launches_timed": dom_calls,
             },
             "stages_ms": {k: round(v, 4) for k, v in per_stage.items()},
             "stage_bytes": {k: int(bytes_[k]) for k in fwd_keys if k in bytes_},
             "workload_stats": info,
         }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(cam, gcpu, D, cfg_name=f"cfg{args.config}", backward=False,
+                                               tile_sample=FWD_CPU_TILES[args.config])
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
@@ -462,8 +491,9 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=3, choices=[3, 5],
-                    help="3: BASELINE cfg3 fwd+bwd (the headline); 5: BASELINE cfg5 forward-only replicas")
+    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 5],
+                    help="3: BASELINE cfg3 fwd+bwd (the headline); 1: BASELINE cfg1 fwd+bwd (1k Gaussians, "
+                         "128x128, RGB); 2 / 5: BASELINE cfg2 / cfg5 forward-only replicas")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fwd-1mpix", action="store_true")
     ap.add_argument("--no-quick", action="store_true")
@@ -486,7 +516,7 @@ def main() -> int:
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     _lib.load()
-    if args.config == 5:
+    if args.config in (2, 5):
         return main_forward_replicas(args, world, rank, dev)
 
     cfg = CONFIGS[args.config]
@@ -496,34 +526,36 @@ def main() -> int:
     cam0 = make_camera(W, H)
     cam = make_camera(W, H, yaw_deg=yaw)
     gcpu = make_gaussians(N, cam0, seed=0, sh_degree=deg, lang_dim=D)
-    leaf_keys = ("means3D", "shs", "opacities", "scales", "rotations", "language_feature_precomp")
+    leaf_keys = tuple(k for k in ("means3D", "shs", "colors_precomp", "opacities", "scales", "rotations",
+                                  "language_feature_precomp") if k in gcpu)
     g = {k: gcpu[k].to(dev).requires_grad_(True) for k in leaf_keys}
     g["means2D"] = torch.zeros_like(g["means3D"], requires_grad=True)
     leaves = [g[k] for k in leaf_keys]
     inputs = leaves + [g["means2D"]]
     gen = torch.Generator(device="cpu").manual_seed(1 + rank)
     dcolor = torch.randn((3, H, W), generator=gen).to(dev)
-    dlang = torch.randn((D, H, W), generator=gen).to(dev)
-    rs = settings(cam, dev, deg, True)
+    dlang = torch.randn((D, H, W), generator=gen).to(dev) if D else None
+    rs = settings(cam, dev, deg or 0, D > 0)
     rast = GaussianRasterizer(rs)
+    kw = {k: g[k] for k in leaf_keys if k not in ("means3D", "opacities")}
+    outs_of = (lambda c, l: [c, l]) if D else (lambda c, l: [c])
+    grads_in = [dcolor, dlang] if D else [dcolor]
     exch = dp.ViewShardedExchange(leaves, with_stats=True, names=leaf_keys) if world > 1 else None
     xev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
     xms = [0.0, 0]
 
     def step(timed_exchange=False):
-        color, lang, radii = rast(means3D=g["means3D"], means2D=g["means2D"], opacities=g["opacities"],
-                                  shs=g["shs"], language_feature_precomp=g["language_feature_precomp"],
-                                  scales=g["scales"], rotations=g["rotations"])
+        color, lang, radii = rast(means3D=g["means3D"], means2D=g["means2D"], opacities=g["opacities"], **kw)
         if exch is None:
-            return torch.autograd.grad([color, lang], inputs, [dcolor, dlang])
+            return torch.autograd.grad(outs_of(color, lang), inputs, grads_in)
         # gradients land in the all-reduce buckets; the language bucket's all-reduce
         # starts on a side stream as soon as the render backward has finished it
         with exch.sink():
-            grads = torch.autograd.grad([color, lang], inputs, [dcolor, dlang])
+            grads = torch.autograd.grad(outs_of(color, lang), inputs, grads_in)
         if timed_exchange:
             xev[0].record()
         red, _, _ = exch.finish(grads[-1], radii, grads[:-1], campos=rs.campos, means3D=g["means3D"].detach(),
-                                sh_degree=deg)
+                                sh_degree=deg or 0)
         if timed_exchange:
             xev[1].record()
             xev[1].synchronize()
@@ -579,15 +611,17 @@ def main() -> int:
         value = frames / elapsed
         with torch.no_grad():
             gd = {k: v.detach() for k, v in g.items()}
-            bytes_, info = algorithmic_bytes(gd, rs, D, 48)
+            bytes_, info = algorithmic_bytes(gd, rs, D, 3 * (deg + 1) ** 2 if deg is not None else 0)
         dom_ms = dom_ms_s / dom_calls if dom_calls else 0.0
         dom_gbps = bytes_[dom] / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
-        traffic, traffic_src = pmc_traffic(dom)
+        pre = "r" if args.config == 3 else f"cfg{args.config}_r"
+        traffic, traffic_src = pmc_traffic(dom, prefix=pre)
         step_ms = elapsed / args.steps * 1e3
         kernel_ms = sum(v["ms_per_launch"] for v in per_stage.values())
         total_bytes = sum(bytes_.values())
         out = {
-            "metric": METRIC,
+            "metric": METRIC if args.config == 3 else
+            "frames/s fwd+bwd @ 1k Gaussians 128x128 RGB (BASELINE configs[0]); ms_per_step = its fwd+bwd time",
             "value": round(value, 3),
             "unit": "frames/s",
             "n_gpus": world,
@@ -601,7 +635,9 @@ def main() -> int:
             "data": "synthetic (seeded; SURVEY.md §8d generator)",
             "config": {
                 "workload": "BASELINE cfg3: 1M Gaussians, 1920x1080, SH deg 3 + 16 dense language channels, "
-                            "fwd+bwd, all inputs require grad; 1 view per GPU",
+                            "fwd+bwd, all inputs require grad; 1 view per GPU" if args.config == 3 else
+                            "BASELINE cfg1: 1k Gaussians, 128x128, RGB colours_precomp, fwd+bwd, all inputs "
+                            "require grad; 1 view per GPU",
                 "gaussians": N, "width": W, "height": H, "lang_dim": D, "sh_degree": deg,
                 "global_batch": world, "parallelism": f"dp{world} (views sharded, RCCL all-reduce of grads)"
                 if world > 1 else "single GPU",
@@ -630,9 +666,9 @@ def main() -> int:
                 "ms_per_launch": round(dom_ms, 4),
                 "launches_timed": dom_calls,
                 # the kernel is issue/latency-bound, not HBM-bound: its SQ-counter roofline
-                "issue": pmc_issue(dom),
+                "issue": pmc_issue(dom, prefix=pre),
                 # and its writes are memory-side atomics: their rate's floor
-                "atomics": atomic_floor("render_bwd_mf", dom_ms) if dom == "render_bwd" else None,
+                "atomics": atomic_floor("render_bwd_mf", dom_ms, prefix=pre) if dom == "render_bwd" else None,
             },
             "hbm_step": {"algorithmic_bytes": int(total_bytes),
                          "GBps_over_kernels": round(total_bytes / (kernel_ms * 1e-3) / 1e9, 1) if kernel_ms else 0,
@@ -642,12 +678,12 @@ def main() -> int:
             "stage_bytes": {k: int(v) for k, v in bytes_.items()},
             "workload_stats": info,
         }
-        if world == 1 and not args.no_fwd_1mpix:
+        if world == 1 and not args.no_fwd_1mpix and args.config == 3:
             out["fwd_fps_1mpix"] = round(fwd_fps({k: v.detach() for k, v in g.items()}, dev, deg, D), 1)
-        if world == 1 and not args.no_quick:
+        if world == 1 and not args.no_quick and args.config == 3:
             out["quick_1mpix"] = quick_fps(N, dev)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(cam, gcpu, D)
+            out["cpu_baseline"] = cpu_baseline(cam, gcpu, D, cfg_name=f"cfg{args.config}")
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -308,9 +308,15 @@ int lsr_abi_version(void);
  * LSR_BIN_SORTED_TILES scatters (depth, id) keys into the tile buckets and
  * sorts each bucket; LSR_BIN_ORDERED radix-sorts the Gaussians by depth once
  * and places every bucket's instances in that order (no bucket sort);
- * LSR_BIN_AUTO (default) takes the ordered mode from ~3M Gaussians up.  Both
- * produce the identical point_list.  LSR_EINVAL for an unknown option/value. */
+ * LSR_BIN_AUTO (default) currently always takes the sorted tiles (the ordered
+ * mode measured slower at every size; it is opt-in only).  Both produce the
+ * identical point_list.  LSR_OPT_LISTS_MAX_MB (default 2048): a forward with a
+ * backward pending writes the backward's per-block candidate lists (128 B per
+ * tile instance) only while they fit this many MiB; above it the backward
+ * re-stages from the tile lists (identical results).  LSR_EINVAL for an
+ * unknown option/value. */
 #define LSR_OPT_BIN_MODE 1
+#define LSR_OPT_LISTS_MAX_MB 2
 #define LSR_BIN_AUTO 0
 #define LSR_BIN_SORTED_TILES 1
 #define LSR_BIN_ORDERED 2

@@ -230,6 +230,20 @@ def set_bin_mode(mode: str) -> str:
     return {v: k for k, v in BIN_MODES.items()}[prev.value]
 
 
+LSR_OPT_LISTS_MAX_MB = 2
+
+
+def set_lists_max_mb(mb: int) -> int:
+    """Budget (MiB) for the backward's per-block candidate lists a training
+    forward writes (lsr_set_option LSR_OPT_LISTS_MAX_MB, default 2048); above
+    it the backward re-stages from the tile lists.  Returns the previous value."""
+    lib = load()
+    prev = ctypes.c_int64(0)
+    check(lib.lsr_get_option(LSR_OPT_LISTS_MAX_MB, ctypes.byref(prev)), "lsr_get_option")
+    check(lib.lsr_set_option(LSR_OPT_LISTS_MAX_MB, int(mb)), "lsr_set_option")
+    return int(prev.value)
+
+
 def profile_enable(on: bool = True):
     load().lsr_profile_enable(1 if on else 0)
 

@@ -313,10 +313,12 @@ class _RasterizeGaussians(torch.autograd.Function):
                          "cov3D_precomp": id(cov3Ds_precomp)}
         ctx.dims = dims
         # each 8x8 block's candidate list, written by the forward render for the
-        # backward (lsr_fwd_out.lists; read only, kept for every backward of this graph)
-        ctx.lists = bufs.get(_lib.LSR_BUF_LISTS)
+        # backward (lsr_fwd_out.lists; read only, kept for every backward of this
+        # graph).  Saved like the binning buffers, so autograd frees it with the
+        # graph after the backward (unless retain_graph) instead of holding it for
+        # as long as an output's grad_fn lives
         ctx.save_for_backward(*saved, radii, bufs[_lib.LSR_BUF_GEOM], bufs[_lib.LSR_BUF_BINNING],
-                              bufs[_lib.LSR_BUF_IMAGE])
+                              bufs[_lib.LSR_BUF_IMAGE], bufs.get(_lib.LSR_BUF_LISTS))
         ctx.mark_non_differentiable(radii)
         # backward handles None upstream gradients itself; without this autograd
         # zero-fills a gradient for the int radii output every step
@@ -326,7 +328,7 @@ class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad_color, grad_lang, _grad_radii):
         rs = ctx.raster_settings
-        (means3D, opac, sh, col, sc, rot, cov, lang, qw, qi, radii, geom, binning, image) = ctx.saved_tensors
+        (means3D, opac, sh, col, sc, rot, cov, lang, qw, qi, radii, geom, binning, image, lists) = ctx.saved_tensors
         N, M, D, K = ctx.dims
         dev = means3D.device
         lib = _lib.load()
@@ -348,8 +350,8 @@ class _RasterizeGaussians(torch.autograd.Function):
                           _ptr(qw) if quick else None, _ptr(qi) if quick else None)
         bin_ = _lib.BwdIn(geom.data_ptr(), binning.data_ptr(), image.data_ptr(), ctx.num_rendered, radii.data_ptr(),
                           grad_color.data_ptr(), _ptr(gl))
-        if ctx.lists is not None:
-            bin_.lists = ctx.lists.data_ptr()
+        if lists is not None:
+            bin_.lists = lists.data_ptr()
         ws = ctx.grad_ws
         ctx.grad_ws = None   # a second backward (retain_graph) clears its own
         if ws is not None:

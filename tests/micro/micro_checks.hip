@@ -163,3 +163,58 @@ extern "C" int micro_mfma_order(int R, int seed, int specials, long long* counts
     (void)hipFree(dD);
     return 0;
 }
+
+// The render backward's fast exponential (v_exp_f32 of power * log2 e, render.hip
+// k_render_bwd_mf phase 1) against the deterministic expf_det the forward and
+// the oracle use, EXHAUSTIVELY over every float power in [lo, 0]: the largest
+// relative difference |e_hw - e_det| / e_det.  The backward's alpha band
+// (2e-8 around 1/255) must exceed it.
+__global__ void k_exp_band(uint32_t b0, uint32_t b1, unsigned int* maxrel_bits, unsigned long long* count)
+{
+    const uint32_t stride = gridDim.x * blockDim.x;
+    float mx = 0.f;
+    unsigned long long n = 0;
+    for (uint32_t b = b0 + blockIdx.x * blockDim.x + threadIdx.x; b <= b1 && b >= b0; b += stride) {
+        const float x = __uint_as_float(b);
+        const float eh = __builtin_amdgcn_exp2f(x * 1.4426950408889634f);
+        const float ed = lsr::expf_det(x);
+        if (ed > 0.f) {
+            const float r = fabsf(eh - ed) / ed;
+            mx = fmaxf(mx, r);
+            n++;
+        }
+        if (b > 0xffffffffu - stride) break;
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        mx = fmaxf(mx, __shfl_xor(mx, d, 64));
+        n += __shfl_xor(n, d, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(maxrel_bits, __float_as_uint(mx));
+        atomicAdd(count, n);
+    }
+}
+
+// out[0] = max relative difference over powers in [lo, -0.0], out[1] = values tested
+extern "C" int micro_exp_band(float lo, double* out)
+{
+    unsigned int* dm = nullptr;
+    unsigned long long* dn = nullptr;
+    if (hipMalloc(&dm, 4) != hipSuccess || hipMalloc(&dn, 8) != hipSuccess) return 2;
+    (void)hipMemset(dm, 0, 4);
+    (void)hipMemset(dn, 0, 8);
+    uint32_t b1;
+    std::memcpy(&b1, &lo, 4);
+    k_exp_band<<<2048, 256>>>(0x80000000u, b1, dm, dn);
+    unsigned int m = 0;
+    unsigned long long n = 0;
+    if (hipMemcpy(&m, dm, 4, hipMemcpyDeviceToHost) != hipSuccess) return 2;
+    if (hipMemcpy(&n, dn, 8, hipMemcpyDeviceToHost) != hipSuccess) return 2;
+    float mf;
+    std::memcpy(&mf, &m, 4);
+    out[0] = mf;
+    out[1] = (double)n;
+    (void)hipFree(dm);
+    (void)hipFree(dn);
+    return 0;
+}

@@ -53,3 +53,13 @@ def test_config5_forward_replicas_dry_run():
     assert j["yaws"] == [-20.0, 20.0]
     p1 = _run(["--dry-run"])
     assert _last_json(p1.stdout)["config"] == 3
+
+
+def test_config1_and_config2_dry_run():
+    """BASELINE configs[0] (cfg1: fwd+bwd) and configs[1] (cfg2: forward-only
+    replicas) are bench.py lines too."""
+    for cfg, mode in ((1, "fwd+bwd"), (2, "replicas")):
+        p = _run(["--config", str(cfg), "--dry-run"])
+        assert p.returncode == 0, p.stderr[-2000:]
+        j = _last_json(p.stdout)
+        assert j["config"] == cfg and mode in j["mode"]

@@ -99,3 +99,38 @@ def test_forward_prepares_zeroed_workspace():
             assert int(torch.count_nonzero(lang[:N * D * 4])) == 0, req
     *_, ws = rasterizer._run_forward(*args, grad_request=0)
     assert ws is None
+
+
+def _grads_once(case, seed=7):
+    from diff_gaussian_rasterization import GaussianRasterizer
+    rs = settings_for(case, DEV)
+    t = gpu_inputs(case, DEV, requires_grad=True)
+    kw = {k: t[k] for k in ("shs", "colors_precomp", "scales", "rotations", "language_feature_precomp") if k in t}
+    color, lang, _ = GaussianRasterizer(raster_settings=rs)(means3D=t["means3D"], means2D=t["means2D"],
+                                                            opacities=t["opacities"], **kw)
+    gen = torch.Generator(device=DEV).manual_seed(seed)
+    outs, grads = [color], [torch.randn(color.shape, device=DEV, generator=gen)]
+    if lang.numel():
+        outs.append(lang)
+        grads.append(torch.randn(lang.shape, device=DEV, generator=gen))
+    torch.autograd.backward(outs, grads)
+    torch.cuda.synchronize()
+    return {k: v.grad.detach().cpu().numpy() for k, v in t.items() if isinstance(v, torch.Tensor) and v.grad is not None}
+
+
+@pytest.mark.parametrize("lang_dim", [16, 0])
+def test_lists_budget_zero_falls_back_to_restaging(lang_dim):
+    """LSR_OPT_LISTS_MAX_MB: with no budget the forward writes no
+    per-block lists and the backward re-stages from the tile lists; the
+    gradients are the same sums (GRAD_RTOL: atomics arrival order)."""
+    from langsplatv2_amd import _lib
+    case = make_case(N=4000, W=160, H=128, sh_degree=3, lang_dim=lang_dim, seed=6)
+    a = _grads_once(case)
+    prev = _lib.set_lists_max_mb(0)
+    try:
+        b = _grads_once(case)
+    finally:
+        assert _lib.set_lists_max_mb(prev) == 0
+    assert set(a) == set(b) and "means3D" in a
+    for k in a:
+        assert_grad_close(k, a[k], b[k])

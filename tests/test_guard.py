@@ -80,7 +80,7 @@ def test_debug_list_check_catches_bad_ids(gpu, tmp_path, monkeypatch):
     case = make_case(N=2000, W=96, H=80, sh_degree=3, lang_dim=16, seed=0)
     t, (color, lang, radii) = _render(case, gpu, True)
     node = color.grad_fn                       # the autograd ctx of the rasterizer call
-    binning = node.saved_tensors[-2]           # (..., radii, geom, binning, image)
+    binning = node.saved_tensors[-3]           # (..., radii, geom, binning, image, lists)
     pl_off = layout.bin_layout(int(node.num_rendered))["point_list"]
     # through .data: the saved tensor's version counter stays, as a kernel's stray write would leave it
     binning.data[pl_off:pl_off + 4].view(torch.int32)[0] = 10 ** 8      # id far past P

@@ -46,3 +46,27 @@ def test_mfma_f32_is_an_in_order_fmaf_chain(micro, specials):
     if specials:
         assert spec > tot // 4          # the special operands are really exercised
     assert fwd == tot, f"MFMA != fmaf chain k=0..3 on {tot - fwd} of {tot} (reverse order matches {rev})"
+
+
+def test_fast_exp_inside_the_backward_alpha_band(micro):
+    """The render backward evaluates G with the hardware v_exp_f32 (power * log2 e)
+    and re-takes the alpha >= 1/255 decision with expf_det (the forward's, the
+    oracle's) for every lane whose alpha is within 2e-8 of 1/255 (render.hip,
+    k_render_bwd_mf phase 1).  That is exact only if the two exponentials differ
+    by less than 2e-8 * 255 = 5.1e-6 relative wherever alpha can reach 1/255:
+    powers >= ln(1/255) - ln(opacity), i.e. >= -5.55 for opacities <= 1
+    (sigmoid-activated); -8 leaves room for opacities up to e^2.5.  Checked over
+    EVERY float power in [-8, 0] (1.09e9 values) against a bound of half the
+    band.  (Over [-87, 0] the product power * log2 e rounds to 2^-24 of 125 and
+    the difference reaches 3.9e-6: still inside, with less margin.)"""
+    micro.micro_exp_band.argtypes = [ctypes.c_float, ctypes.POINTER(ctypes.c_double)]
+    out = (ctypes.c_double * 2)()
+    assert micro.micro_exp_band(-8.0, out) == 0
+    band_rel = 2e-8 * 255.0
+    print(f"max relative |exp_hw - expf_det| / expf_det = {out[0]:.3e} over {int(out[1])} powers; "
+          f"backward band {band_rel:.2e} relative")
+    assert out[1] > 1.0e9   # every float in [-8, 0]
+    assert 0.0 < out[0] < 0.5 * band_rel
+    out87 = (ctypes.c_double * 2)()
+    assert micro.micro_exp_band(-87.0, out87) == 0
+    assert out87[0] < band_rel
