@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 8
+#define LSR_ABI_VERSION 9   /* 9 (r05): LSR_OPT_LISTS_MAX_MB; LSR_BIN_ORDERED removed */
 
 enum {
     LSR_OK = 0,
@@ -305,16 +305,14 @@ const char* lsr_strerror(int code);
 int lsr_abi_version(void);
 
 /* Process-wide options.  LSR_OPT_BIN_MODE picks the forward's tile binning:
- * LSR_BIN_SORTED_TILES scatters (depth, id) keys into the tile buckets and
- * sorts each bucket; LSR_BIN_ORDERED radix-sorts the Gaussians by depth once
- * and places every bucket's instances in that order (no bucket sort);
- * LSR_BIN_AUTO (default) currently always takes the sorted tiles (the ordered
- * mode measured slower at every size; it is opt-in only).  Both produce the
- * identical point_list.  LSR_OPT_LISTS_MAX_MB (default 2048): a forward with a
- * backward pending writes the backward's per-block candidate lists (128 B per
- * tile instance) only while they fit this many MiB; above it the backward
- * re-stages from the tile lists (identical results).  LSR_EINVAL for an
- * unknown option/value. */
+ * LSR_BIN_SORTED_TILES (= LSR_BIN_AUTO, the default) scatters (depth, id) keys
+ * into the tile buckets and sorts each bucket.  (ABI <= 8's LSR_BIN_ORDERED, a
+ * depth-ordered mode measured slower at every size, is no longer built: the
+ * value is rejected with LSR_EINVAL.)  LSR_OPT_LISTS_MAX_MB (default 2048): a
+ * forward with a backward pending writes the backward's per-block candidate
+ * lists (128 B per tile instance) only while they fit this many MiB; above it
+ * the backward re-stages from the tile lists (identical results).  LSR_EINVAL
+ * for an unknown option/value. */
 #define LSR_OPT_BIN_MODE 1
 #define LSR_OPT_LISTS_MAX_MB 2
 #define LSR_BIN_AUTO 0

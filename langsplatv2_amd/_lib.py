@@ -214,13 +214,13 @@ def check(rc: int, what: str):
 
 
 LSR_OPT_BIN_MODE = 1
-BIN_MODES = {"auto": 0, "sorted_tiles": 1, "ordered": 2}
+BIN_MODES = {"auto": 0, "sorted_tiles": 1}
 
 
 def set_bin_mode(mode: str) -> str:
     """Select the forward's tile binning process-wide (lsr_set_option
-    LSR_OPT_BIN_MODE): "sorted_tiles", "ordered" or "auto"; returns the
-    previous mode.  Both modes produce the same point_list."""
+    LSR_OPT_BIN_MODE): "sorted_tiles" or "auto" (the same: one mode is built);
+    returns the previous mode."""
     if mode not in BIN_MODES:
         raise ValueError(f"bin mode must be one of {sorted(BIN_MODES)}")
     lib = load()

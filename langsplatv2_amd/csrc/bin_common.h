@@ -1,4 +1,4 @@
-// bin_common.h — pieces shared by the binning kernels (binning.hip, order.hip).
+// bin_common.h — pieces shared by the binning kernels (binning.hip).
 #pragma once
 #include "lsr_internal.h"
 
@@ -45,13 +45,12 @@ struct BinRec {
     int r;
     float4 A, B;
     float depth;
-    uint32_t id;   // the Gaussian (through `order` when given: position i of the depth order)
+    uint32_t id;   // the Gaussian
     __device__ __forceinline__ void load(const uint8_t* geom, int P, int g1, const int32_t* __restrict__ radii, int i,
-                                         bool with_depth, const uint32_t* __restrict__ order = nullptr)
+                                         bool with_depth)
     {
         const GeomLayout L = geom_layout(P);
-        const int qi = min(i, g1 - 1);
-        const int q = order ? (int)order[qi] : qi;
+        const int q = min(i, g1 - 1);
         id = (uint32_t)q;
         const int rr = radii[q];
         A = ((const float4*)(geom + L.splatA))[q];

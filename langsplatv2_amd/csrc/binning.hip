@@ -406,7 +406,7 @@ template <int BB>
 __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int rows, int S,
                                                          const uint8_t* __restrict__ geom,
                                                          const int32_t* __restrict__ radii, uint32_t* __restrict__ table,
-                                                         uint32_t* __restrict__ cls_cnt, const uint32_t* __restrict__ order)
+                                                         uint32_t* __restrict__ cls_cnt)
 {
     extern __shared__ uint32_t hist[];
     __shared__ WaveSpans wss[BB / 64];
@@ -429,10 +429,10 @@ __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int r
     const int lane = threadIdx.x & 63;
     const int g0 = blk * chunk, g1 = min(P, g0 + chunk);
     BinRec nx;
-    if (g0 < g1) nx.load(geom, P, g1, radii, g0 + (threadIdx.x & ~63) + lane, false, order);
+    if (g0 < g1) nx.load(geom, P, g1, radii, g0 + (threadIdx.x & ~63) + lane, false);
     for (int i0 = g0 + (threadIdx.x & ~63); i0 < g1; i0 += BB) {
         const BinRec cur = nx;
-        nx.load(geom, P, g1, radii, i0 + BB + lane, false, order);
+        nx.load(geom, P, g1, radii, i0 + BB + lane, false);
         const int R = stage_gaussian(ws, c, bd, cur);
         // every row entry adds its kept range [sx0, sx1) to the histogram as
         // a difference (+1 at sx0, -1 at sx1 inside the row): two LDS atomics
@@ -769,8 +769,7 @@ bool bin_privatised_ok(const Cam& c) { return (size_t)c.gx * 4 <= LSR_BAND_LDS &
 
 hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t* geom, const int32_t* radii,
                             uint32_t* table, uint32_t* tile_cnt, uint32_t* tile_start, uint64_t* tpart,
-                            uint32_t* cls_cnt, uint32_t* cls_list, uint64_t* host_slot, uint32_t seq, hipStream_t st,
-                            const uint32_t* order)
+                            uint32_t* cls_cnt, uint32_t* cls_list, uint64_t* host_slot, uint32_t seq, hipStream_t st)
 {
     const int T = c.gx * c.gy;
     const int rows = bin_band_rows(c);
@@ -785,9 +784,9 @@ hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t
     }
     if (B > 0) {
         if (bin_block(P) == 1024)
-            k_bin_count<1024><<<grid, 1024, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt, order);
+            k_bin_count<1024><<<grid, 1024, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt);
         else
-            k_bin_count<512><<<grid, 512, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt, order);
+            k_bin_count<512><<<grid, 512, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt);
         BinPublish pb{tpart, cls_cnt + LSR_TICKET_WORD, tile_start + T, host_slot, seq};
         const int G = (T + TBL_TILES - 1) / TBL_TILES, Tp = table_stride(T);
         if (B <= 16 * TBL_RPT)

@@ -53,10 +53,9 @@ struct Status {
 // when enabled, each stage is bracketed by two events recorded on the
 // caller's stream; lsr_profile_query sums their elapsed times.
 enum Stage { ST_PRE, ST_SCAN, ST_DUP, ST_SCAN_T, ST_SCATTER, ST_SORT, ST_RENDER, ST_GZERO, ST_RENDER_BWD,
-             ST_PRE_BWD, ST_ORDER, ST_N };
+             ST_PRE_BWD, ST_N };
 const char* kStageNames[ST_N] = {"preprocess", "scan_tiles", "bin_count", "scan_tile_counts", "bin_scatter",
-                                 "tile_sort", "render_fwd", "grad_zero", "render_bwd", "preprocess_bwd",
-                                 "depth_order"};
+                                 "tile_sort", "render_fwd", "grad_zero", "render_bwd", "preprocess_bwd"};
 
 // Process-wide (the autograd engine runs backward on its own thread, and the
 // caller enables timing on its thread), thread-safe: the switch and mask are
@@ -462,28 +461,22 @@ int lsr_sh_grad_from_views(int64_t N, int M, int sh_degree, const float* means3D
 
 int lsr_abi_version(void) { return LSR_ABI_VERSION; }
 
-// Process-wide options (lsr_set_option).  LSR_OPT_BIN_MODE: which tile binning
-// the forward runs (binning.hip sorted tiles / order.hip ordered).
-#ifndef LSR_BIN_ORDERED_MIN_P
-#define LSR_BIN_ORDERED_MIN_P (1 << 30)   // LSR_BIN_AUTO: ordered from this many Gaussians up (pending measurement)
-#endif
+// Process-wide options (lsr_set_option).  LSR_OPT_BIN_MODE: the forward's tile
+// binning; one mode is built (binning.hip: scatter into tile buckets + per-tile
+// sort).  The depth-ordered mode of round 4 (order.hip) measured slower at every
+// size (cfg5 scatter 4.55 vs 0.84 ms) and was removed in round 5.
 static std::atomic<int64_t> g_bin_mode{LSR_BIN_AUTO};
 // LSR_OPT_LISTS_MAX_MB: the backward's per-block candidate lists (128 B per
 // instance of capacity) are written only while they fit this budget; above it
 // the backward re-stages its candidates from the tile lists (same results,
 // measured 2.8 % slower at cfg3).  cfg3: 0.6 GB; cfg5 (M = 60 M): 7.7 GB -> off.
 static std::atomic<int64_t> g_lists_max_mb{2048};
-static bool bin_ordered(int P)
-{
-    const int64_t m = g_bin_mode.load(std::memory_order_relaxed);
-    return m == LSR_BIN_ORDERED || (m == LSR_BIN_AUTO && P >= LSR_BIN_ORDERED_MIN_P);
-}
 
 int lsr_set_option(int option, int64_t value)
 {
     switch (option) {
         case LSR_OPT_BIN_MODE:
-            if (value != LSR_BIN_AUTO && value != LSR_BIN_SORTED_TILES && value != LSR_BIN_ORDERED) return LSR_EINVAL;
+            if (value != LSR_BIN_AUTO && value != LSR_BIN_SORTED_TILES) return LSR_EINVAL;
             g_bin_mode.store(value, std::memory_order_relaxed);
             return LSR_OK;
         case LSR_OPT_LISTS_MAX_MB:
@@ -680,21 +673,18 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
 
     const GeomLayout GL = geom_layout((size_t)P);
     const ImageLayout IL = image_layout(NPIX, (size_t)T);
-    // privatised binning needs a B x T table (tail of the image workspace);
-    // the ordered mode also the depth sort's workspace after it
+    // privatised binning needs a B x T table (tail of the image workspace)
     const bool priv = P > 0 && bin_privatised_ok(c);
-    const bool ordered = priv && bin_ordered(P);
     int chunk = 0;
     const int B = priv ? bin_blocks(P, c, chunk) : 0;
     const size_t table_bytes = priv ? align256((size_t)B * table_stride(T) * 4) : 0;
-    const size_t order_bytes = ordered ? depth_order_layout(P).total : 0;
     uint8_t* geom = (uint8_t*)alloc(ctx, GL.total, LSR_BUF_GEOM);
-    uint8_t* img = (uint8_t*)alloc(ctx, IL.total + table_bytes + order_bytes, LSR_BUF_IMAGE);
+    uint8_t* img = (uint8_t*)alloc(ctx, IL.total + table_bytes, LSR_BUF_IMAGE);
     if (!geom || !img) return LSR_ENOMEM;
     out->geom = geom;
     out->geom_bytes = GL.total;
     out->image = img;
-    out->image_bytes = IL.total + table_bytes + order_bytes;
+    out->image_bytes = IL.total + table_bytes;
     uint32_t* table = (uint32_t*)(img + IL.total);
     uint32_t* tile_cnt = (uint32_t*)(img + IL.tile_cnt);
     uint32_t* tile_start = (uint32_t*)(img + IL.tile_start);
@@ -709,19 +699,12 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     HostSlot& hs = host_slot();
     if (!hs.word) return LSR_EHIP;
     const uint32_t seq = ++hs.seq;
-    const uint32_t* order = nullptr;
-    if (ordered) {
-        // 2a. the Gaussians sorted by depth (order.hip): the count and scatter
-        // below walk chunks of that order, and the tile lists come out sorted
-        StageScope sc(ST_ORDER, st);
-        LSR_HIP(launch_depth_order(P, geom, out->radii, img + IL.total + table_bytes, &order, st));
-    }
     if (priv) {
         // 2. per-block tile histograms -> column scan -> tile starts; M = total
         {
             StageScope sc(ST_DUP, st);
             LSR_HIP(launch_bin_count(c, P, chunk, B, geom, out->radii, table, tile_cnt, tile_start, tpart, cls_cnt,
-                                     cls_list, hs.dev, seq, st, order));
+                                     cls_list, hs.dev, seq, st));
         }
         {
             StageScope sc(ST_SCAN_T, st);
@@ -767,11 +750,7 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     }
     out->binning = bin;
     out->binning_bytes = bin_cap;
-    if (ordered) {
-        StageScope sc(ST_SCATTER, st);
-        LSR_HIP(launch_bin_scatter_ord(c, P, chunk, B, geom, out->radii, order, table, tile_start,
-                                       (uint32_t*)(bin + BL.point_list), st));
-    } else if (priv) {
+    if (priv) {
         StageScope sc(ST_SCATTER, st);
         LSR_HIP(launch_bin_scatter(c, P, chunk, B, geom, out->radii, table, tile_start, (uint64_t*)(bin + BL.keys),
                                    st));
@@ -791,7 +770,7 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
                                (uint64_t*)(bin + BL.keys), st));
     }
     LSR_DEBUG_SYNC(s, st, "scatter");
-    if (!ordered) {
+    {
         StageScope sc(ST_SORT, st);
         LSR_HIP(launch_tile_sort(T, tile_start, (uint64_t*)(bin + BL.keys), (uint32_t*)(bin + BL.point_list), cls_cnt,
                                  cls_list, priv ? host_cls : nullptr, st));

@@ -80,11 +80,8 @@ __device__ __forceinline__ bool wave_any(bool b) { return __builtin_amdgcn_ballo
 // Wait for the wave's outstanding LDS operations; the memory clobber keeps
 // the compiler from moving LDS accesses across it (wave-private LDS staging
 // needs no workgroup barrier).
-#ifdef LSR_LDS_NOWAIT   // experiment: compiler-only ordering (a wave's LDS operations execute in issue order)
-__device__ __forceinline__ void wave_lds_fence() { asm volatile("" ::: "memory"); }
-#else
+// (tools/variants/lds_nowait.patch: the compiler-only form, -0.8 % render_bwd, not taken)
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-#endif
 
 // float -> int truncating + saturating; NaN -> 0 (matches oracle f2i).
 __device__ __forceinline__ int f2i(float v)

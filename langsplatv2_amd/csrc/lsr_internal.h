@@ -45,11 +45,9 @@ int bin_blocks(int P, const Cam& c, int& chunk);
 bool bin_privatised_ok(const Cam& c);
 // count + column scan + group-level tile scan; publishes M (and the sort
 // class counts) to host_slot like launch_publish_total
-// order: null, or the depth order (order.hip) whose chunks the blocks count
 hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t* geom, const int32_t* radii,
                             uint32_t* table, uint32_t* tile_cnt, uint32_t* tile_start, uint64_t* tpart,
-                            uint32_t* cls_cnt, uint32_t* cls_list, uint64_t* host_slot, uint32_t seq, hipStream_t st,
-                            const uint32_t* order = nullptr);
+                            uint32_t* cls_cnt, uint32_t* cls_list, uint64_t* host_slot, uint32_t seq, hipStream_t st);
 int bin_scatter_rows(const Cam& c);
 int scatter_merge(int P);
 int bin_block(int P);
@@ -61,18 +59,6 @@ hipError_t launch_bin_scatter(const Cam& c, int P, int chunk, int B, const uint8
 hipError_t launch_tile_sort(int T, const uint32_t* tile_start, uint64_t* keys, uint32_t* point_list,
                             uint32_t* cls_cnt, uint32_t* cls_list, const uint32_t* host_cnt, hipStream_t st);
 
-// order.hip: the ordered binning mode (Gaussians radix-sorted by depth, the
-// tile lists placed in that order: no per-tile sort)
-struct DepthOrderLayout {
-    size_t kA, kB, vA, vB, hist, part, total;
-};
-DepthOrderLayout depth_order_layout(int P);
-// *order <- the P Gaussian ids by (depth bits, id), invisible ones last (in ws)
-hipError_t launch_depth_order(int P, const uint8_t* geom, const int32_t* radii, uint8_t* ws, const uint32_t** order,
-                              hipStream_t st);
-hipError_t launch_bin_scatter_ord(const Cam& c, int P, int chunk, int B, const uint8_t* geom, const int32_t* radii,
-                                  const uint32_t* order, const uint32_t* table, const uint32_t* tile_start,
-                                  uint32_t* point_list, hipStream_t st);
 
 // render.hip
 struct RenderArgs {

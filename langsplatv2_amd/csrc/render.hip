@@ -272,6 +272,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(fwd_wav
     constexpr bool SF = fwd_sfeat<NL>();
     static_assert(!ML || NL == 16 || NL == 32 || NL == 64, "ML: whole 16-channel language blocks");
     static_assert(ML || !SF, "scalar feature rows (D >= LSR_FWD_SFEAT) feed the ML form only");
+    // the ML form's carried partial groups and `last` are kept in the SF stage
+    // (st.pos / st.gid / st.R); a build with ML but LDS-staged rows would drop them
+    static_assert(!ML || SF, "the ML carry logic needs the SF stage (LSR_FWD_SFEAT <= 16)");
     constexpr int MLB = ML ? NL / 16 : 1;   // ML: 16-channel output blocks
     __shared__ WaveStageP<F4, SF> st;
 
@@ -1514,23 +1517,6 @@ __device__ __forceinline__ void dot_features(const RenderArgs& a, uint32_t gid, 
 // requiring grad).  Then dL/dlang[j][c] = sum_p aT[j][p] dL/dout[c][p] is all
 // that is left: no dot products, no dL/dalpha recurrence, no moments, and the
 // rows go straight into the (N, D) output (b.grad_acc, b.VP = D).
-// Phase timing of the backward (diagnostic builds only, -DLSR_BWD_STAMPS):
-// per wave, s_memtime deltas summed per phase, added once per wave into
-// g_bwd_stamps (read by lsr_dbg_bwd_stamps).  Each stamp waits for the wave's
-// outstanding LDS operations (the counter read shares lgkmcnt), so phase
-// boundaries are slightly sharper than in the product build.
-#ifdef LSR_BWD_STAMPS
-__device__ unsigned long long g_bwd_stamps[16];
-#define BWD_STAMP_DECL unsigned long long st_acc[10] = {}; unsigned long long st_t = __builtin_amdgcn_s_memtime();
-#define BWD_STAMP(i) do { const unsigned long long _t = __builtin_amdgcn_s_memtime(); st_acc[i] += _t - st_t; st_t = _t; } while (0)
-#define BWD_COUNT(i) do { st_acc[i] += 1; } while (0)
-#define BWD_STAMP_FLUSH() do { if (threadIdx.x == 0) for (int _i = 0; _i < 10; _i++) atomicAdd(&g_bwd_stamps[_i + (threadIdx.x & 64)], st_acc[_i]); } while (0)
-#else
-#define BWD_STAMP_DECL
-#define BWD_STAMP(i) do {} while (0)
-#define BWD_COUNT(i) do {} while (0)
-#define BWD_STAMP_FLUSH() do {} while (0)
-#endif
 
 // SP (with LO): the language input is the quick path's sparse (weights,
 // codes) rows; the per-channel gradient rows are gathered at each Gaussian's
@@ -1612,7 +1598,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_wav
     const int last = inside ? (int)a.n_contrib[pix] : 0;
     const int wmax = wave_max_i(last);
     if (wmax == 0) return;
-    BWD_STAMP_DECL
     // Prologue order: the loads the first chunk's staging depends on (ids,
     // then records) are issued before the block's dL/dout fragments, so
     // waiting for them (vector-memory operations complete in issue order)
@@ -1739,19 +1724,22 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_wav
     // VMEM operations the previous (full, one-group) chunk issued after it --
     // its buffer atomics, GRL x 4 per group (unconditional, never merged; the
     // feature gathers are not counted) -- so the wait does not drain them
-    constexpr int OPG = GRL * 4;
+    // INVARIANT: the atomic loop below issues exactly GRL x 4
+    // unconditional buffer atomics per group (masked lanes get an out-of-range
+    // offset, never a branch), all after this chunk's DMA; the counted wait
+    // relies on it.  Change that loop and this count together.
+    constexpr int ATOMICS_PER_GROUP = GRL * 4;
+    constexpr int OPG = ATOMICS_PER_GROUP;
     constexpr int CGR = LSR_LST_CHUNK / 16;   // groups per list chunk
     constexpr int CHUNK_OPS = CGR * OPG < 63 ? CGR * OPG : 63;
     constexpr int CH = LST ? LSR_LST_CHUNK : 64;   // candidates per chunk
     if constexpr (LST) list_dma(0, 0);
-    BWD_STAMP(0);
     const int cend = LST ? (int)lcnt : wmax;
     for (int c0 = 0; c0 < cend; c0 += CH) {
         int n, nfull;
         const float4* SA;
         const float4* SB;
         const uint32_t* SG;
-        BWD_COUNT(8);
         if constexpr (LST) {
             const int off = (c0 / CH & 1) * CH;
             if (c0 == 0 || !buf_atom) wait_vmcnt<0>();
@@ -1783,11 +1771,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_wav
             SG = st.gid;
         }
         constexpr int SGS = LST ? 4 : 1;   // word stride of the id array
-        BWD_STAMP(1);
 
         for (int g0 = 0; g0 < nfull; g0 += 16) {
             const int kn = min(16, nfull - g0);
-            BWD_COUNT(9);
             // A fragments of the dot product: feature 4t+lg of candidate g0+li,
             // gathered now, consumed after phase 1
             if constexpr (!LO) {
@@ -1840,7 +1826,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_wav
                     }
                 }
             }
-            BWD_STAMP(2);
             // dot[k][p] of the group's candidates on MFMA: (16 x C) . (C x 64)
             float dv[16];
             (void)dv;
@@ -1868,7 +1853,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_wav
                 }
             }
             wave_lds_fence();
-            BWD_STAMP(3);
             // phase 2: the serial back-to-front recurrence per pixel.  S is the
             // colour accumulated behind the current instance (the upstream
             // "accum_rec" once the last contributor is folded in):
@@ -1912,7 +1896,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_wav
                 }
             }
             wave_lds_fence();
-            BWD_STAMP(4);
             // phase 3: language gradients on MFMA; RGB gradients and the six
             // pixel moments sum_p u {1, lx, ly, lx^2, lx ly, ly^2} on the VALU.
             // Lane (li, lg) reads candidate li's aT and u at pixel q = 4t + lg
@@ -2040,7 +2023,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_wav
                 gr[8] = C2;
             }
             wave_lds_fence();
-            BWD_STAMP(5);
             if constexpr (SP) {
                 // (slot, code) pairs: dL/dw[gid][m] += row[slot][idx[gid][m]]
                 const int K = a.K;
@@ -2079,7 +2061,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_wav
                     // buffer atomics: 32-bit offsets, and a lane with nothing
                     // to add gets an offset past the buffer (the range check
                     // drops it: tools/micro/buf_oob_atomic.hip) instead of an
-                    // exec-masked branch per atomic
+                    // exec-masked branch per atomic.  INVARIANT: exactly
+                    // ATOMICS_PER_GROUP = GRL x 4 of them, unconditionally (the
+                    // LST chunk wait above counts them as vmcnt operations)
+                    static_assert(ATOMICS_PER_GROUP == GRL * 4, "the LST wait counts these atomics");
 #pragma unroll
                     for (int h = 0; h < GRL; h++) {
                         const int f = 16 * h + li;
@@ -2119,7 +2104,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_wav
                 }
             }
             wave_lds_fence();
-            BWD_STAMP(6);
         }
         // carry the partial group to the front of the stage
         if constexpr (!LST) {
@@ -2131,9 +2115,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_wav
             }
         }
         wave_lds_fence();
-        BWD_STAMP(7);
     }
-    BWD_STAMP_FLUSH();
 }
 
 
@@ -2172,17 +2154,6 @@ hipError_t launch_render_bwd_lang_sparse(const RenderBwdArgs& b, hipStream_t st)
     return hipGetLastError();
 }
 
-#ifdef LSR_BWD_STAMPS
-}  // namespace lsr
-extern "C" int lsr_dbg_bwd_stamps(unsigned long long* out)
-{
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lsr::g_bwd_stamps), sizeof(unsigned long long) * 16) != hipSuccess)
-        return 3;
-    unsigned long long z[16] = {};
-    return hipMemcpyToSymbol(HIP_SYMBOL(lsr::g_bwd_stamps), z, sizeof(z)) == hipSuccess ? 0 : 3;
-}
-namespace lsr {
-#endif
 
 bool bwd_lang_direct(int D)
 {

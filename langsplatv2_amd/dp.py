@@ -39,9 +39,16 @@ sum up to fp32 summation order.  Per GPU the exchange moves
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
+
+
+def _debug() -> bool:
+    """LSR_DP_DEBUG=1: extra consistency checks in the exchange (they synchronise)."""
+    return os.environ.get("LSR_DP_DEBUG", "0") not in ("", "0")
 
 def rank_yaw(rank: int, world: int, spread_deg: float = 40.0) -> float:
     """Camera yaw of the view rank `rank` renders in the synthetic benchmark:
@@ -284,12 +291,23 @@ class ViewShardedExchange:
                 if g is not None and g.data_ptr() == v.data_ptr():
                     continue
                 if self.names[i] in used:
-                    # the backward wrote this bucket view itself: the view is the
-                    # gradient.  With loss.backward() inside `with ex.sink():`
-                    # AccumulateGrad keeps a COPY of the returned view as p.grad
-                    # (the sink holds a second reference), so `grads` may carry
-                    # that copy; packing it would race with an early all-reduce
-                    # already running on the view.
+                    # the backward wrote this bucket view itself.  `grads` may hold
+                    # a copy of it (loss.backward() inside `with ex.sink():` leaves
+                    # AccumulateGrad's copy in p.grad) or, when the leaf also gets
+                    # gradient through another path (a regulariser, a second use),
+                    # autograd's SUM: packing g is right in both cases
+                    # -- except on an early-bucket view whose all-reduce is already
+                    # in flight, where packing would race: there the
+                    # view must already be the whole gradient (checked with
+                    # LSR_DP_DEBUG=1).
+                    if g is None:
+                        continue
+                    if i in self.early_idx and self._early_work is not None:
+                        if _debug() and not torch.equal(g.reshape(v.shape), v):
+                            raise RuntimeError(f"finish: {self.names[i]} has gradient from outside the rasterizer, "
+                                               "but its early all-reduce already started")
+                        continue
+                    v.copy_(g.reshape(v.shape))
                     continue
                 if i in self.early_idx and self._early_work is not None:
                     # the early all-reduce is in flight on this view: packing it now would race

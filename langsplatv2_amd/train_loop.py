@@ -10,7 +10,7 @@ What it restates (reference file:line):
     points are `zeros_like(xyz, requires_grad=True) + 0` with retain_grad,
     the (1,) placeholder for the language input, SH evaluated by the rasterizer;
   * the loss (1 - lambda_dssim) L1 + lambda_dssim (1 - SSIM): train.py:166-168,
-    utils/loss_utils.py:18-75;
+    utils/loss_utils.py:18-71;
   * per-view bookkeeping: max_radii2D over the visibility filter and
     add_densification_stats (train.py:245-251, scene/gaussian_model.py:506-508);
   * the SH-degree ramp every 1000 iterations (train.py:135-136) and the
@@ -134,7 +134,7 @@ def _gauss_window(window_size: int, sigma: float, channel: int, like: torch.Tens
 
 
 def ssim(img1: torch.Tensor, img2: torch.Tensor, window_size: int = 11) -> torch.Tensor:
-    """utils/loss_utils.py:38-75 (11x11 Gaussian window, sigma 1.5, mean SSIM)."""
+    """utils/loss_utils.py:41-71 (ssim / _ssim: 11x11 Gaussian window, sigma 1.5, mean SSIM)."""
     c = img1.size(-3)
     w = _gauss_window(window_size, 1.5, c, img1)
     pad = window_size // 2

@@ -226,3 +226,55 @@ def _backward_pattern_worker(rank, world, port):
 
 def test_exchange_finish_after_backward_pattern_gloo_world2():
     mp.spawn(_backward_pattern_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def _multipath_worker(rank, world, port):
+    """a bucketed leaf that ALSO gets gradient from outside the
+    rasterizer (a regulariser): autograd hands finish() the SUM, while the
+    bucket view holds only the rasterizer's part.  finish() must pack the sum for
+    the main bucket; for an early-bucket view whose all-reduce is already in
+    flight it cannot, and LSR_DP_DEBUG=1 makes that an error instead of a silent
+    drop."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        names = ["means3D", "opacities", "language_feature_precomp"]
+        params = [torch.zeros(5, 3), torch.zeros(5, 1), torch.zeros(5, 16)]
+        ex = dp.ViewShardedExchange(params, with_stats=False, names=names)
+        g = torch.Generator().manual_seed(20 + rank)
+        local = [torch.randn(p.shape, generator=g) for p in params]
+        reg = [torch.randn(p.shape, generator=g) for p in params]
+        sink = ex.sink()
+        for nm, p, loc in zip(names, params, local):
+            sink.take(nm, tuple(p.shape), p.device, id(p)).copy_(loc)
+        # no early all-reduce started (e.g. the language input took no lang-ready
+        # callback): every view may be packed with autograd's sums
+        sums = [loc + rg for loc, rg in zip(local, reg)]
+        red, _, _ = ex.finish(None, None, sums)
+        exp = [torch.zeros_like(p) for p in params]
+        for r in range(world):
+            gr = torch.Generator().manual_seed(20 + r)
+            lo = [torch.randn(p.shape, generator=gr) for p in params]
+            rg = [torch.randn(p.shape, generator=gr) for p in params]
+            for i in range(3):
+                exp[i] += lo[i] + rg[i]
+        for i in range(3):
+            assert torch.allclose(red[i], exp[i], rtol=0, atol=1e-5), names[i]
+        # the early bucket in flight + a foreign contribution: an error in debug mode
+        sink = ex.sink()
+        for nm, p, loc in zip(names, params, local):
+            sink.take(nm, tuple(p.shape), p.device, id(p)).copy_(loc)
+        ex._on_lang_ready(sink)
+        assert ex._early_work is not None
+        os.environ["LSR_DP_DEBUG"] = "1"
+        with pytest.raises(RuntimeError, match="early all-reduce already started"):
+            ex.finish(None, None, sums)
+        ex._early_work.wait()
+        dist.barrier()
+    finally:
+        os.environ.pop("LSR_DP_DEBUG", None)
+        dist.destroy_process_group()
+
+
+def test_exchange_finish_packs_multipath_sums_gloo_world2():
+    mp.spawn(_multipath_worker, args=(2, _free_port()), nprocs=2, join=True)

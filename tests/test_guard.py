@@ -16,22 +16,26 @@ def test_status_codes_have_text():
     lib = _lib.load()
     assert b"non-finite" in lib.lsr_strerror(_lib.LSR_ENONFINITE).lower()
     assert b"binning lists" in lib.lsr_strerror(_lib.LSR_ELISTS).lower()
-    assert lib.lsr_abi_version() == 8
+    assert lib.lsr_abi_version() == 9
 
 
-def test_bin_mode_option_roundtrip():
-    """lsr_set_option / lsr_get_option (host-only: no GPU needed)."""
+def test_options_roundtrip():
+    """lsr_set_option / lsr_get_option (host-only: no GPU needed).  One binning
+    mode is built (sorted tiles; the round-4 ordered mode is rejected)."""
     import ctypes
     lib = _lib.load()
-    prev = _lib.set_bin_mode("ordered")
+    prev = _lib.set_bin_mode("sorted_tiles")
     v = ctypes.c_int64(-1)
-    assert lib.lsr_get_option(_lib.LSR_OPT_BIN_MODE, ctypes.byref(v)) == 0 and v.value == 2
-    assert _lib.set_bin_mode("sorted_tiles") == "ordered"
+    assert lib.lsr_get_option(_lib.LSR_OPT_BIN_MODE, ctypes.byref(v)) == 0 and v.value == 1
     assert _lib.set_bin_mode(prev) == "sorted_tiles"
+    assert lib.lsr_set_option(_lib.LSR_OPT_BIN_MODE, 2) == _lib.LSR_EINVAL      # LSR_BIN_ORDERED: removed
     assert lib.lsr_set_option(_lib.LSR_OPT_BIN_MODE, 3) == _lib.LSR_EINVAL
     assert lib.lsr_set_option(12345, 0) == _lib.LSR_EINVAL
     with pytest.raises(ValueError):
-        _lib.set_bin_mode("bogus")
+        _lib.set_bin_mode("ordered")
+    old = _lib.set_lists_max_mb(100)
+    assert old == 2048 and _lib.set_lists_max_mb(old) == 100
+    assert lib.lsr_set_option(_lib.LSR_OPT_LISTS_MAX_MB, -1) == _lib.LSR_EINVAL
 
 
 def _render(case, dev, debug, poison=None):

@@ -1,7 +1,7 @@
 """A/B timing of liblsr variants in ONE process: each variant's library is
 loaded under its own name and the cfg3 fwd+bwd stage times are measured in
 interleaved rounds (cdna guide §5.4 rule 24).  Usage: python tools/ab.py name=path.so[#binmode] ...
-(binmode: auto / sorted_tiles / ordered, set through lsr_set_option before each of the variant's rounds;
+(binmode: auto / sorted_tiles, set through lsr_set_option before each of the variant's rounds;
 LSR_CFG selects the BASELINE config, default 3)."""
 import ctypes
 import os

@@ -1,5 +1,7 @@
-"""Per-phase cycle census of k_render_bwd_mf (diagnostic variant built with
--DLSR_BWD_STAMPS: `make -C langsplatv2_amd/csrc variant NAME=stamps VFLAGS=-DLSR_BWD_STAMPS`).
+"""Per-phase cycle census of k_render_bwd_mf (diagnostic variant: the stamps
+live in tools/variants/bwd_stamps.patch, out of the product source --
+`python tools/variant.py stamps --patch tools/variants/bwd_stamps.patch`, then
+run this script on langsplatv2_amd/_build/var_stamps/liblsr.so).
 Runs cfg3 fwd+bwd a few times and prints, per phase, the s_memtime cycles summed
 over waves, per group and per chunk.  Usage: python tools/bwd_stamps.py [LIB]"""
 import ctypes

@@ -2,6 +2,7 @@
 sources stay free of experiment switches).
 
     python tools/variant.py NAME 'old text' 'new text' [file.hip] [-- 'old2' 'new2' [file2]] ...
+    python tools/variant.py NAME --patch tools/variants/X.patch [--patch ...] [-- 'old' 'new' ...]
 
 Each replacement must match exactly once in its file (default render.hip).
 Output: langsplatv2_amd/_build/var_NAME/liblsr.so (sources + objects under var_NAME/pkg) (load with tools/ab.py NAME=path)."""
@@ -32,6 +33,11 @@ def main():
     inc = os.path.join(dst, "include")
     shutil.copytree(os.path.join(ROOT, "include"), inc)
     for g in groups:
+        if g and g[0] == "--patch":
+            # a unified diff against langsplatv2_amd/csrc (a/langsplatv2_amd/csrc/<file>)
+            for pf in g[1::2]:
+                subprocess.run(["patch", "-s", "-p3", "-d", src, "-i", os.path.abspath(pf)], check=True)
+            continue
         old, new = g[0], g[1]
         fn = g[2] if len(g) > 2 else "render.hip"
         p = os.path.join(src, fn)
