@@ -237,17 +237,15 @@ def cpu_baseline(cam, gcpu, D, cfg_name="cfg3", backward=True, tile_sample=None)
     rng = np.random.default_rng(0)
     dcol = rng.standard_normal((3, pb.H, pb.W)).astype(np.float32)
     dlang = rng.standard_normal((pb.D, pb.H, pb.W)).astype(np.float32) if pb.D else None
-    t0 = time.perf_counter()
-    O.forward(pb, nthreads=threads, tiles=np.zeros(0, np.int32))   # preprocess + binning only
-    t1 = time.perf_counter()
-    f = O.forward(pb, nthreads=threads, tiles=tiles)
+    tf = {}
+    f = O.forward(pb, nthreads=threads, tiles=tiles, timings=tf)
     t2 = time.perf_counter()
     if backward:
         O.backward(pb, f, dcol, dlang, tiles=tiles, nthreads=threads)
     t3 = time.perf_counter()
-    t_pre_bin = t1 - t0
-    # the render part of the forward (after preprocess + binning) scales with the tiles
-    t_fwd = t_pre_bin + (t2 - t1 - t_pre_bin) * scale
+    t_pre_bin = tf["preprocess_binning"]
+    # the render part of the forward scales with the tiles (a sample: x T / sample)
+    t_fwd = t_pre_bin + tf["render"] * scale
     t_bwd = (t3 - t2) * scale
     t_frame = t_fwd + t_bwd
     what = "whole" if tiles is None else f"{len(tiles)} of {T} tiles (x{scale:.1f}, extrapolated) of the"

@@ -694,7 +694,13 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     uint32_t* cls_list = (uint32_t*)(img + IL.cls_list);
 
     // 1. preprocess
-    { StageScope sc(ST_PRE, st); LSR_HIP(launch_preprocess(c, *in, geom, out->radii, st)); }
+    {
+        // a pending geometry gradient: the preprocess also stores the SH colour
+        // Jacobian the preprocess backward needs (48 B instead of the 192-B SH row)
+        const bool jac = (out->grad_ws_request & LSR_GWS_GEOM) != 0 && !s->quick_render;
+        StageScope sc(ST_PRE, st);
+        LSR_HIP(launch_preprocess(c, *in, geom, out->radii, jac, st));
+    }
     LSR_DEBUG_SYNC(s, st, "preprocess");
     HostSlot& hs = host_slot();
     if (!hs.word) return LSR_EHIP;

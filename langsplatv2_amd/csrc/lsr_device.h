@@ -373,6 +373,7 @@ __device__ __forceinline__ bool block_overlap_exact(float x, float y, float ca, 
 {
     return rect_overlap_exact(x, y, ca, cb, cc, cut, bx, by, 7.f, 7.f);
 }
+
 // Binning's tile cull: can Gaussian (splat records A, B) contribute to any
 // pixel of tile (tx, ty)?  The exact cut-ellipse test on the whole 16x16 tile
 // (no clipping at the image border).  A rejected instance has alpha < 1/255 at
@@ -505,7 +506,7 @@ __device__ __forceinline__ uint32_t xor_lane_u32(uint32_t x)
 // ------------------------------------------------------------- layouts --
 // Geometry workspace (per Gaussian, SoA, every section 256-B aligned).
 struct GeomLayout {
-    size_t splatA, splatB, rgb, depth, tiles, offsets, clamped, scan_part, total;
+    size_t splatA, splatB, rgb, depth, tiles, offsets, clamped, scan_part, shjac, flags, total;
     // splatA = {x, y, conic.a, conic.b}; splatB = {conic.c, opacity, cut, extent bits}
 };
 
@@ -523,6 +524,11 @@ __host__ __device__ inline GeomLayout geom_layout(size_t N)
     L.offsets = o;  o += align256(N * 4);   // inclusive scan of tiles
     L.clamped = o;  o += align256(N * 4);   // 3-bit mask
     L.scan_part = o; o += align256(((N + 4095) / 4096 + 1) * 8);
+    // SH colour Jacobian d(RGB)/d(dir) (3 x float3 per Gaussian: ddx[0..2], ddy[0..2],
+    // ddz[0..2]), written by a forward with a geometry gradient pending and read by
+    // the preprocess backward instead of the 192-B SH row (preprocess.hip)
+    L.shjac = o;    o += align256(N * 36);
+    L.flags = o;    o += 256;               // [0] = 1: this forward wrote shjac
     L.total = o;
     return L;
 }

@@ -19,7 +19,7 @@ struct Cam {
 };
 
 // preprocess.hip
-hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, int32_t* radii, hipStream_t st);
+hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, int32_t* radii, bool jac, hipStream_t st);
 hipError_t launch_sh_grad_from_views(int64_t N, int M, int deg, const float* means3D, int R, const float* campos,
                                      const float* drgb, float* dL_dsh, hipStream_t st);
 hipError_t launch_preprocess_bwd(const Cam& c, const lsr_inputs& in, const uint8_t* geom, const int32_t* radii,

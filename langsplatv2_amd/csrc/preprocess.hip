@@ -50,9 +50,93 @@ __device__ __forceinline__ void stage_sh_rows(float* shl, const float* shs, int 
     for (int f = lane; f < cnt * 12; f += 64) put(f, src[f]);
 }
 
+// dRGB/dsh_k of the forward's SH evaluation (sh_channel) at direction
+// (x, y, z): the basis value multiplying coefficient k, same expressions as
+// preprocess_bwd_one's.
+__device__ __forceinline__ void sh_basis(int deg, float x, float y, float z, float (&bk)[16])
+{
+#pragma unroll
+    for (int k = 0; k < 16; k++) bk[k] = 0.f;
+    bk[0] = 0.28209479177387814f;
+    if (deg > 0) {
+        const float c1 = 0.4886025119029199f;
+        bk[1] = -c1 * y;
+        bk[2] = c1 * z;
+        bk[3] = -c1 * x;
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z;
+            const float xy = x * y, yz = y * z, xz = x * z;
+            bk[4] = LSR_C2_0 * xy;
+            bk[5] = LSR_C2_1 * yz;
+            bk[6] = LSR_C2_2 * (2.f * zz - xx - yy);
+            bk[7] = LSR_C2_3 * xz;
+            bk[8] = LSR_C2_4 * (xx - yy);
+            if (deg > 2) {
+                bk[9] = LSR_C3_0 * y * (3.f * xx - yy);
+                bk[10] = LSR_C3_1 * xy * z;
+                bk[11] = LSR_C3_2 * y * (4.f * zz - xx - yy);
+                bk[12] = LSR_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                bk[13] = LSR_C3_4 * x * (4.f * zz - xx - yy);
+                bk[14] = LSR_C3_5 * z * (xx - yy);
+                bk[15] = LSR_C3_6 * x * (xx - 3.f * yy);
+            }
+        }
+    }
+}
+
+// The view-factored SH gradient: one thread per Gaussian sums R views'
+// basis (x) dRGB products in view order and writes the (M,3) row once.
+// d(RGB_ch)/d(dir) of the SH colour (sh_channel) at the unit direction (x, y, z):
+// ddx/ddy/ddz[ch], the term order of upstream's backward.  Evaluated by the
+// forward when a geometry gradient is pending (stored in GeomLayout::shjac) or,
+// without that, by the preprocess backward from the SH row.
+template <typename SHV>
+__device__ __forceinline__ void sh_dir_jacobian(int deg, const SHV& sh, float x, float y, float z, float (&ddx)[3],
+                                                float (&ddy)[3], float (&ddz)[3])
+{
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) ddx[ch] = ddy[ch] = ddz[ch] = 0.f;
+#define S(k) sh[(k)*3 + ch]
+    if (deg > 0) {
+        const float c1 = 0.4886025119029199f;
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) {
+            ddx[ch] = -c1 * S(3);
+            ddy[ch] = -c1 * S(1);
+            ddz[ch] = c1 * S(2);
+        }
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z;
+            const float xy = x * y, yz = y * z, xz = x * z;
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) {
+                ddx[ch] += LSR_C2_0 * y * S(4) + LSR_C2_2 * 2.f * -x * S(6) + LSR_C2_3 * z * S(7) + LSR_C2_4 * 2.f * x * S(8);
+                ddy[ch] += LSR_C2_0 * x * S(4) + LSR_C2_1 * z * S(5) + LSR_C2_2 * 2.f * -y * S(6) + LSR_C2_4 * 2.f * -y * S(8);
+                ddz[ch] += LSR_C2_1 * y * S(5) + LSR_C2_2 * 2.f * 2.f * z * S(6) + LSR_C2_3 * x * S(7);
+            }
+            if (deg > 2) {
+#pragma unroll
+                for (int ch = 0; ch < 3; ch++) {
+                    ddx[ch] += LSR_C3_0 * S(9) * 3.f * 2.f * xy + LSR_C3_1 * S(10) * yz + LSR_C3_2 * S(11) * -2.f * xy +
+                               LSR_C3_3 * S(12) * -3.f * 2.f * xz + LSR_C3_4 * S(13) * (-3.f * xx + 4.f * zz - yy) +
+                               LSR_C3_5 * S(14) * 2.f * xz + LSR_C3_6 * S(15) * 3.f * (xx - yy);
+                    ddy[ch] += LSR_C3_0 * S(9) * 3.f * (xx - yy) + LSR_C3_1 * S(10) * xz +
+                               LSR_C3_2 * S(11) * (-3.f * yy + 4.f * zz - xx) + LSR_C3_3 * S(12) * -3.f * 2.f * yz +
+                               LSR_C3_4 * S(13) * -2.f * xy + LSR_C3_5 * S(14) * -2.f * yz +
+                               LSR_C3_6 * S(15) * -3.f * 2.f * xy;
+                    ddz[ch] += LSR_C3_1 * S(10) * xy + LSR_C3_2 * S(11) * 4.f * 2.f * yz +
+                               LSR_C3_3 * S(12) * 3.f * (2.f * zz - xx - yy) + LSR_C3_4 * S(13) * 4.f * 2.f * xz +
+                               LSR_C3_5 * S(14) * (xx - yy);
+                }
+            }
+        }
+    }
+#undef S
+}
+
 template <bool SH16, bool COV>
 __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& in, uint8_t* __restrict__ geom,
-                                               int32_t* __restrict__ radii, int i, const float* shrow)
+                                               int32_t* __restrict__ radii, int i, const float* shrow, bool jac)
 {
     const int N = in.P;
     const GeomLayout L = geom_layout(N);
@@ -182,6 +266,18 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
             const float* shg = in.shs + (size_t)i * in.max_coeffs * 3;
             for (int ch = 0; ch < 3; ch++) out[ch] = sh_channel(c.sh_degree, shg, ch, dir[0], dir[1], dir[2]);
         }
+        if (jac) {
+            // the backward's dRGB/d(dir), from the SH row already in registers: the
+            // preprocess backward then reads 48 B instead of the 192-B SH row
+            float ddx[3], ddy[3], ddz[3];
+            if constexpr (SH16) sh_dir_jacobian(c.sh_degree, sh, dir[0], dir[1], dir[2], ddx, ddy, ddz);
+            else sh_dir_jacobian(c.sh_degree, in.shs + (size_t)i * in.max_coeffs * 3, dir[0], dir[1], dir[2], ddx, ddy,
+                                 ddz);
+            float3* J = (float3*)(geom + L.shjac) + (size_t)3 * i;
+            J[0] = make_float3(ddx[0], ddx[1], ddx[2]);
+            J[1] = make_float3(ddy[0], ddy[1], ddy[2]);
+            J[2] = make_float3(ddz[0], ddz[1], ddz[2]);
+        }
         uint32_t m = 0;
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) {
@@ -204,23 +300,28 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
 
 template <bool SH16, bool COV>
 __global__ void __launch_bounds__(256) k_preprocess(Cam c, lsr_inputs in, uint8_t* __restrict__ geom,
-                                                    int32_t* __restrict__ radii)
+                                                    int32_t* __restrict__ radii, int jac)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) ((uint32_t*)(geom + geom_layout(in.P).flags))[0] = jac ? 1u : 0u;
     if (i >= in.P) return;
-    preprocess_one<SH16, COV>(c, in, geom, radii, i, nullptr);
+    preprocess_one<SH16, COV>(c, in, geom, radii, i, nullptr, jac != 0);
 }
 
-hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, int32_t* radii, hipStream_t st)
+// jac: a geometry gradient is pending -- store the SH colour Jacobian for the
+// preprocess backward (SH inputs only)
+hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, int32_t* radii, bool jac,
+                             hipStream_t st)
 {
     if (in.P == 0) return hipSuccess;
     const bool sh16 = in.shs && in.max_coeffs == 16 && ((uintptr_t)in.shs % 16 == 0);
     const bool cov = in.cov3D_precomp != nullptr;
+    const int j = (jac && in.shs && !in.colors_precomp) ? 1 : 0;
     const dim3 g((in.P + 255) / 256);
-    if (sh16 && cov) k_preprocess<true, true><<<g, 256, 0, st>>>(c, in, geom, radii);
-    else if (sh16) k_preprocess<true, false><<<g, 256, 0, st>>>(c, in, geom, radii);
-    else if (cov) k_preprocess<false, true><<<g, 256, 0, st>>>(c, in, geom, radii);
-    else k_preprocess<false, false><<<g, 256, 0, st>>>(c, in, geom, radii);
+    if (sh16 && cov) k_preprocess<true, true><<<g, 256, 0, st>>>(c, in, geom, radii, j);
+    else if (sh16) k_preprocess<true, false><<<g, 256, 0, st>>>(c, in, geom, radii, j);
+    else if (cov) k_preprocess<false, true><<<g, 256, 0, st>>>(c, in, geom, radii, j);
+    else k_preprocess<false, false><<<g, 256, 0, st>>>(c, in, geom, radii, j);
     return hipGetLastError();
 }
 
@@ -238,6 +339,7 @@ hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, 
 struct BwdRow {
     int rad;
     float4 g0, g1, g2;
+    float3 j0, j1, j2;   // the forward's SH colour Jacobian (jac: GeomLayout::shjac)
     float mx, my, mz;
     float4 q;
     float sc0, sc1, sc2;
@@ -247,13 +349,18 @@ struct BwdRow {
     // each, and every copy waits for its load)
     template <bool COV>
     __device__ __forceinline__ void load(const lsr_inputs& in, const int32_t* __restrict__ radii,
-                                         const float* __restrict__ gacc, int VP, int i)
+                                         const float* __restrict__ gacc, int VP, int i, const float3* __restrict__ jac)
     {
         const float4* g4 = reinterpret_cast<const float4*>(gacc + (size_t)i * VP);
         rad = radii[i];
         g0 = g4[0];
         g1 = g4[1];
         g2 = g4[2];
+        if (jac) {
+            j0 = jac[3 * (size_t)i];
+            j1 = jac[3 * (size_t)i + 1];
+            j2 = jac[3 * (size_t)i + 2];
+        }
         mx = in.means3D[3 * i]; my = in.means3D[3 * i + 1]; mz = in.means3D[3 * i + 2];
         q = make_float4(1.f, 0.f, 0.f, 0.f);
         sc0 = sc1 = sc2 = 0.f;
@@ -267,10 +374,12 @@ struct BwdRow {
     }
 };
 
+// jac: the forward stored the SH colour Jacobian (row.j0..j2); otherwise it is
+// evaluated here from the SH row (SH16: shrow holds it on entry)
 template <bool SH16>
 __device__ __forceinline__ void preprocess_bwd_one(const Cam& c, const lsr_inputs& in, const uint8_t* __restrict__ geom,
                                                    const BwdRow& row, const float* __restrict__ gacc, int VP,
-                                                   const lsr_bwd_out& out, int i, float* shrow)
+                                                   const lsr_bwd_out& out, int i, float* shrow, bool jac)
 {
     const int N = in.P;
     const GeomLayout L = geom_layout(N);
@@ -392,72 +501,26 @@ __device__ __forceinline__ void preprocess_bwd_one(const Cam& c, const lsr_input
         sh_dir(mx, my, mz, c.campos, dir, dor);
         const float x = dir[0], y = dir[1], z = dir[2];
         const int deg = c.sh_degree;
-        float sh[48];
-        if (SH16) {
+        // basis functions (dRGB/dsh_k), term order of the forward
+        float bk[16];
+        sh_basis(deg, x, y, z, bk);
+        float ddx[3], ddy[3], ddz[3];
+        if (jac) {
+            ddx[0] = row.j0.x; ddx[1] = row.j0.y; ddx[2] = row.j0.z;
+            ddy[0] = row.j1.x; ddy[1] = row.j1.y; ddy[2] = row.j1.z;
+            ddz[0] = row.j2.x; ddz[1] = row.j2.y; ddz[2] = row.j2.z;
+        } else if (SH16) {
+            float sh[48];
 #pragma unroll
             for (int k = 0; k < 48; k++) sh[k] = shrow[k];
+            sh_dir_jacobian(deg, sh, x, y, z, ddx, ddy, ddz);
         } else {
+            float sh[48];
             const float* src = in.shs + (size_t)i * M * 3;
 #pragma unroll
             for (int k = 0; k < 48; k++) sh[k] = (k < M * 3) ? src[k] : 0.f;
+            sh_dir_jacobian(deg, sh, x, y, z, ddx, ddy, ddz);
         }
-        // basis functions (dRGB/dsh_k), term order of the forward
-        float bk[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++) bk[k] = 0.f;
-        bk[0] = 0.28209479177387814f;
-        float ddx[3] = {0.f, 0.f, 0.f}, ddy[3] = {0.f, 0.f, 0.f}, ddz[3] = {0.f, 0.f, 0.f};
-#define S(k) sh[(k)*3 + ch]
-        if (deg > 0) {
-            const float c1 = 0.4886025119029199f;
-            bk[1] = -c1 * y;
-            bk[2] = c1 * z;
-            bk[3] = -c1 * x;
-#pragma unroll
-            for (int ch = 0; ch < 3; ch++) {
-                ddx[ch] = -c1 * S(3);
-                ddy[ch] = -c1 * S(1);
-                ddz[ch] = c1 * S(2);
-            }
-            if (deg > 1) {
-                const float xx = x * x, yy = y * y, zz = z * z;
-                const float xy = x * y, yz = y * z, xz = x * z;
-                bk[4] = LSR_C2_0 * xy;
-                bk[5] = LSR_C2_1 * yz;
-                bk[6] = LSR_C2_2 * (2.f * zz - xx - yy);
-                bk[7] = LSR_C2_3 * xz;
-                bk[8] = LSR_C2_4 * (xx - yy);
-#pragma unroll
-                for (int ch = 0; ch < 3; ch++) {
-                    ddx[ch] += LSR_C2_0 * y * S(4) + LSR_C2_2 * 2.f * -x * S(6) + LSR_C2_3 * z * S(7) + LSR_C2_4 * 2.f * x * S(8);
-                    ddy[ch] += LSR_C2_0 * x * S(4) + LSR_C2_1 * z * S(5) + LSR_C2_2 * 2.f * -y * S(6) + LSR_C2_4 * 2.f * -y * S(8);
-                    ddz[ch] += LSR_C2_1 * y * S(5) + LSR_C2_2 * 2.f * 2.f * z * S(6) + LSR_C2_3 * x * S(7);
-                }
-                if (deg > 2) {
-                    bk[9] = LSR_C3_0 * y * (3.f * xx - yy);
-                    bk[10] = LSR_C3_1 * xy * z;
-                    bk[11] = LSR_C3_2 * y * (4.f * zz - xx - yy);
-                    bk[12] = LSR_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
-                    bk[13] = LSR_C3_4 * x * (4.f * zz - xx - yy);
-                    bk[14] = LSR_C3_5 * z * (xx - yy);
-                    bk[15] = LSR_C3_6 * x * (xx - 3.f * yy);
-#pragma unroll
-                    for (int ch = 0; ch < 3; ch++) {
-                        ddx[ch] += LSR_C3_0 * S(9) * 3.f * 2.f * xy + LSR_C3_1 * S(10) * yz + LSR_C3_2 * S(11) * -2.f * xy +
-                                   LSR_C3_3 * S(12) * -3.f * 2.f * xz + LSR_C3_4 * S(13) * (-3.f * xx + 4.f * zz - yy) +
-                                   LSR_C3_5 * S(14) * 2.f * xz + LSR_C3_6 * S(15) * 3.f * (xx - yy);
-                        ddy[ch] += LSR_C3_0 * S(9) * 3.f * (xx - yy) + LSR_C3_1 * S(10) * xz +
-                                   LSR_C3_2 * S(11) * (-3.f * yy + 4.f * zz - xx) + LSR_C3_3 * S(12) * -3.f * 2.f * yz +
-                                   LSR_C3_4 * S(13) * -2.f * xy + LSR_C3_5 * S(14) * -2.f * yz +
-                                   LSR_C3_6 * S(15) * -3.f * 2.f * xy;
-                        ddz[ch] += LSR_C3_1 * S(10) * xy + LSR_C3_2 * S(11) * 4.f * 2.f * yz +
-                                   LSR_C3_3 * S(12) * 3.f * (2.f * zz - xx - yy) + LSR_C3_4 * S(13) * 4.f * 2.f * xz +
-                                   LSR_C3_5 * S(14) * (xx - yy);
-                    }
-                }
-            }
-        }
-#undef S
         if (want_sh) {
             if (SH16) {
 #pragma unroll
@@ -533,9 +596,11 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(Cam c, lsr_inputs in, co
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= in.P) return;
+    const bool jac = ((const uint32_t*)(geom + geom_layout(in.P).flags))[0] != 0u;
+    const float3* J = jac ? (const float3*)(geom + geom_layout(in.P).shjac) : nullptr;
     BwdRow row;
-    row.load<COV>(in, radii, gacc, VP, i);
-    preprocess_bwd_one<false>(c, in, geom, row, gacc, VP, out, i, nullptr);
+    row.load<COV>(in, radii, gacc, VP, i, J);
+    preprocess_bwd_one<false>(c, in, geom, row, gacc, VP, out, i, nullptr, jac);
 }
 
 template <bool COV>
@@ -547,13 +612,17 @@ __global__ void __launch_bounds__(64) k_preprocess_bwd_sh16(Cam c, lsr_inputs in
     const int b0 = blockIdx.x * 64, lane = threadIdx.x;
     const int cnt = min(64, in.P - b0);
     const bool sh = !in.colors_precomp;
+    // jac (uniform): the forward stored the SH colour Jacobian, so the SH rows
+    // are not read at all (the LDS tile only stages the SH gradient's stores)
+    const bool jac = ((const uint32_t*)(geom + geom_layout(in.P).flags))[0] != 0u;
+    const float3* J = jac ? (const float3*)(geom + geom_layout(in.P).shjac) : nullptr;
     BwdRow row;
-    row.load<COV>(in, radii, gacc, VP, b0 + min(lane, cnt - 1));
-    if (sh) {
+    row.load<COV>(in, radii, gacc, VP, b0 + min(lane, cnt - 1), J);
+    if (sh && !jac) {
         stage_sh_rows(shl, in.shs, b0, cnt, lane);
         __syncthreads();
     }
-    if (lane < cnt) preprocess_bwd_one<true>(c, in, geom, row, gacc, VP, out, b0 + lane, shl + lane * LSR_SH_ROW);
+    if (lane < cnt) preprocess_bwd_one<true>(c, in, geom, row, gacc, VP, out, b0 + lane, shl + lane * LSR_SH_ROW, jac);
     if (sh && out.dL_dsh) {
         __syncthreads();
         float4* dst = reinterpret_cast<float4*>(out.dL_dsh) + (size_t)b0 * 12;
@@ -583,42 +652,6 @@ hipError_t launch_preprocess_bwd(const Cam& c, const lsr_inputs& in, const uint8
     return hipGetLastError();
 }
 
-// dRGB/dsh_k of the forward's SH evaluation (sh_channel) at direction
-// (x, y, z): the basis value multiplying coefficient k, same expressions as
-// preprocess_bwd_one's.
-__device__ __forceinline__ void sh_basis(int deg, float x, float y, float z, float (&bk)[16])
-{
-#pragma unroll
-    for (int k = 0; k < 16; k++) bk[k] = 0.f;
-    bk[0] = 0.28209479177387814f;
-    if (deg > 0) {
-        const float c1 = 0.4886025119029199f;
-        bk[1] = -c1 * y;
-        bk[2] = c1 * z;
-        bk[3] = -c1 * x;
-        if (deg > 1) {
-            const float xx = x * x, yy = y * y, zz = z * z;
-            const float xy = x * y, yz = y * z, xz = x * z;
-            bk[4] = LSR_C2_0 * xy;
-            bk[5] = LSR_C2_1 * yz;
-            bk[6] = LSR_C2_2 * (2.f * zz - xx - yy);
-            bk[7] = LSR_C2_3 * xz;
-            bk[8] = LSR_C2_4 * (xx - yy);
-            if (deg > 2) {
-                bk[9] = LSR_C3_0 * y * (3.f * xx - yy);
-                bk[10] = LSR_C3_1 * xy * z;
-                bk[11] = LSR_C3_2 * y * (4.f * zz - xx - yy);
-                bk[12] = LSR_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
-                bk[13] = LSR_C3_4 * x * (4.f * zz - xx - yy);
-                bk[14] = LSR_C3_5 * z * (xx - yy);
-                bk[15] = LSR_C3_6 * x * (xx - 3.f * yy);
-            }
-        }
-    }
-}
-
-// The view-factored SH gradient: one thread per Gaussian sums R views'
-// basis (x) dRGB products in view order and writes the (M,3) row once.
 __global__ void __launch_bounds__(256) k_sh_grad_from_views(int64_t N, int M, int deg, const float* __restrict__ means3D,
                                                             int R, const float* __restrict__ campos,
                                                             const float* __restrict__ drgb, float* __restrict__ dL_dsh)

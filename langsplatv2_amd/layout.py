@@ -14,7 +14,8 @@ def _a(x: int) -> int:
 def geom_layout(N: int) -> dict:
     o, L = 0, {}
     for name, nb in (("splatA", N * 16), ("splatB", N * 16), ("rgb", N * 12), ("depth", N * 4), ("tiles", N * 4),
-                     ("offsets", N * 4), ("clamped", N * 4), ("scan_part", ((N + 4095) // 4096 + 1) * 8)):
+                     ("offsets", N * 4), ("clamped", N * 4), ("scan_part", ((N + 4095) // 4096 + 1) * 8),
+                     ("shjac", N * 36), ("flags", 256)):
         L[name] = o
         o += _a(nb)
     L["total"] = o

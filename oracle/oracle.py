@@ -129,13 +129,17 @@ class Problem:
         return s, i
 
 
-def forward(pb: Problem, nthreads: int = 1, tiles=None, cull: bool = True) -> dict:
+def forward(pb: Problem, nthreads: int = 1, tiles=None, cull: bool = True, timings: dict | None = None) -> dict:
     """Full oracle forward; returns geometry, binning and image outputs.
     `tiles`: optional subset of tile ids to render (others left zero).
     `cull`: the product's tile cull in the binning (lso_binning_ex); False
     gives the reference's instance lists (A.2) — the rendered outputs are the
-    same either way (tests/test_oracle.py::test_tile_cull_changes_no_output)."""
+    same either way (tests/test_oracle.py::test_tile_cull_changes_no_output).
+    `timings`: filled with the wall seconds of preprocess + binning and of the
+    render (bench.py's CPU baseline)."""
+    import time
     lib = load()
+    t0 = time.perf_counter()
     N = pb.N
     g = dict(depth=np.zeros(N, np.float32), radii=np.zeros(N, np.int32), xy=np.zeros((N, 2), np.float32),
              conic_opacity=np.zeros((N, 4), np.float32), rgb=np.zeros((N, 3), np.float32),
@@ -152,6 +156,7 @@ def forward(pb: Problem, nthreads: int = 1, tiles=None, cull: bool = True) -> di
     lib.lso_binning_ex(ctypes.byref(s), N, ctypes.byref(geom), _p(point_list), _p(ranges), int(bool(cull)))
     Dout = pb.quick_dim if pb.quick else pb.D
     H, W = pb.H, pb.W
+    t1 = time.perf_counter()
     color = np.zeros((3, H, W), np.float32)
     lang = np.zeros((Dout, H, W), np.float32)
     final_T = np.zeros((H, W), np.float32)
@@ -164,6 +169,8 @@ def forward(pb: Problem, nthreads: int = 1, tiles=None, cull: bool = True) -> di
         lib.lso_render_fwd_tiles(ctypes.byref(s), ctypes.byref(i), ctypes.byref(geom), _p(point_list), _p(ranges),
                                  _p(tl), len(tl), _p(color), _p(lang) if Dout else None, _p(final_T), _p(n_contrib),
                                  int(nthreads))
+    if timings is not None:
+        timings.update(preprocess_binning=t1 - t0, render=time.perf_counter() - t1)
     out = dict(g)
     out.update(num_rendered=M, point_list=point_list[:M], ranges=ranges, color=color, lang=lang, final_T=final_T,
                n_contrib=n_contrib)

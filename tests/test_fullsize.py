@@ -234,3 +234,4 @@ def test_d64_feature_step_shape_whole_frame(gpu, oracle_lib):
     assert float(np.abs(rb["dlang"]).max()) > 0.0
     _record("d64_lang_only_bwd", {"language_feature_precomp": grad_errors(g, rb["dlang"])})
     assert_grad_close("language_feature_precomp", g, rb["dlang"], rtol=GRAD_RTOL_FRAME)
+
