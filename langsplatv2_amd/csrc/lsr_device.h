@@ -84,12 +84,15 @@ __device__ __forceinline__ bool wave_any(bool b) { return __builtin_amdgcn_ballo
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // float -> int truncating + saturating; NaN -> 0 (matches oracle f2i).
+// Branch-free: the clamp keeps the conversion in range (one v_cvt_i32_f32),
+// the two selects give the saturated top and NaN.  (The branchy form made
+// the quick render's staging wait on each code's LDS read separately.)
 __device__ __forceinline__ int f2i(float v)
 {
-    if (v != v) return 0;
-    if (v >= 2147483520.0f) return 2147483647;
-    if (v <= -2147483648.0f) return (int)(-2147483647 - 1);
-    return (int)v;
+    const float c = fminf(fmaxf(v, -2147483648.0f), 2147483520.0f);   // NaN -> -2^31
+    int r = (int)c;
+    r = v >= 2147483520.0f ? 2147483647 : r;
+    return v != v ? 0 : r;
 }
 
 // Quick-path code index m of a Gaussian's sparse language row: fp32-encoded

@@ -440,6 +440,27 @@ __global__ void __launch_bounds__(256) k_codebook_chol(const float* __restrict__
 #define LSR_DEC2_NT 0        // non-temporal output stores
 #endif
 #define LSR_DEC2_MAXDB 32    // Df <= 512: fragments + norm factor fit in 144 KB of LDS
+#ifndef LSR_DEC2_STORE
+#define LSR_DEC2_STORE 1     // 1: 4 planes x 256 B per store (register transpose); 0: 16 planes x 64 B
+#endif
+
+// Exchange a register bit with lane bit log2(D) (D = 4 or 8) between X (bit 0)
+// and Y (bit 1): X's lanes with the lane bit set take Y's lanes D below, Y's
+// lanes with it clear take X's lanes D above (DPP row shifts within 16-lane
+// rows; bank masks select the 4-lane banks written).
+template <int D>
+__device__ __forceinline__ void dec_swap_lanebit(f32x4q& X, f32x4q& Y)
+{
+    static_assert(D == 4 || D == 8, "lane bit 2 or 3");
+    constexpr int SHR = 0x110 + D, SHL = 0x100 + D;
+    constexpr int HI = D == 4 ? 0xA : 0xC, LO = D == 4 ? 0x5 : 0x3;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int x = __float_as_int(X[r]), y = __float_as_int(Y[r]);
+        X[r] = __int_as_float(__builtin_amdgcn_update_dpp(x, y, SHR, 0xF, HI, false));
+        Y[r] = __int_as_float(__builtin_amdgcn_update_dpp(y, x, SHL, 0xF, LO, false));
+    }
+}
 
 template <bool NORM, bool VEC>
 __global__ void __launch_bounds__(64 * LSR_DEC2_WAVES, 1)
@@ -574,6 +595,43 @@ __global__ void __launch_bounds__(64 * LSR_DEC2_WAVES, 1)
                 for (int r = 0; r < 4; r++)
                     mul[pb][r] = sc / (sqrtf(fmaxf(row16_sum(sq[pb][r]) * ns2, 0.f)) + eps / osc[pb][r]);
         }
+#if LSR_DEC2_STORE == 1
+        if (VEC) {
+            // 4 planes x 256 B per store instruction (instead of 16 planes x 64 B):
+            // the four 16-pixel tiles' results are transposed in registers by two
+            // (register bit <-> lane bit) swaps — pb bit 0 <-> lane bit 2, pb bit 1
+            // <-> lane bit 3 (DPP row shifts by 4 and 8 under bank masks) — so
+            // register q holds dims 4 q + (li & 3) of pixel groups
+            // g = lg + 4 ((li >> 2) & 3), each dim's 64 pixels in one 256-B piece.
+            const int xo = bx + 4 * (lg + 4 * ((li >> 2) & 3));
+            float* const orow = out + (size_t)(l * Df + (li & 3)) * HW + (size_t)y * W + xo;
+            const bool st_ok = xo < W;   // W % 4 == 0: a pixel group is all in or all out
+#pragma unroll 1
+            for (int db = 0; db < NDB; db++) {
+                const uint4* f = sfr + (size_t)db * 256 + lane * 2;
+                const h8 c0h = __builtin_bit_cast(h8, f[0]), c0l = __builtin_bit_cast(h8, f[1]);
+                const h8 c1h = __builtin_bit_cast(h8, f[128]), c1l = __builtin_bit_cast(h8, f[129]);
+                f32x4q v[4];
+#pragma unroll
+                for (int pb = 0; pb < 4; pb++) {
+                    f32x4q acc = {0.f, 0.f, 0.f, 0.f};
+                    LSR_DEC_MFMA6(acc, pb);
+#pragma unroll
+                    for (int r = 0; r < 4; r++) v[pb][r] = acc[r] * mul[pb][r];
+                }
+                dec_swap_lanebit<4>(v[0], v[1]);   // pb bit 0 <-> lane bit 2
+                dec_swap_lanebit<4>(v[2], v[3]);
+                dec_swap_lanebit<8>(v[0], v[2]);   // pb bit 1 <-> lane bit 3
+                dec_swap_lanebit<8>(v[1], v[3]);
+                float* const od = orow + (size_t)db * 16 * HW;
+                if (st_ok) {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) *reinterpret_cast<f32x4q*>(od + (size_t)(4 * q) * HW) = v[q];
+                }
+            }
+            continue;
+        }
+#endif
         float* const orow = out + (size_t)(l * Df + li) * HW + (size_t)y * W;
 #pragma unroll 1
         for (int db = 0; db < NDB; db++) {

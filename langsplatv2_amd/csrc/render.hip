@@ -968,6 +968,7 @@ struct WaveRawQ {
     float rgb[3][64];                   // channel c of lane l (three 4-B DMAs)
     float4 W[3][64];                    // weight row part p (4 weights) of lane l
     uint4 Q[3 * QB / 4][64];            // index row bytes [16 p, 16 p + 16) of lane l
+    uint32_t nid[64];                   // the point-list ids of the chunk after next
 };
 
 template <int DT>
@@ -988,7 +989,12 @@ __device__ __forceinline__ int quick_code_raw(const WaveRawQ<DT == 2 ? 8 : 4>& r
 // record, rgb, weight row and index row land at slot l of each array (an LDS-
 // DMA writes wave-uniform M0 + lane x size).  One asm block walks M0 through
 // the arrays (raw's layout is fixed by the static_asserts below); the weight
-// and index row parts are the immediate offsets of one address each.  The
+// and index row parts are the immediate offsets of one address each; the same
+// asm block also copies the point-list ids two chunks ahead into raw.nid, so
+// no VGPR-destination load is ever in flight behind the DMAs (a compiler-
+// inserted wait for such a load is a vmcnt(N) that the compiler computes
+// without the asm's DMAs, and drained them: every chunk's first pair waited
+// for the prefetch just issued).  The
 // immediate offset applies to the LDS destination as well (M0 + offset + 16
 // lane), so M0 steps to each array's base minus that offset.  The colour
 // goes as three 4-B DMAs (one channel plane each): a dwordx3 LDS-DMA does not
@@ -998,10 +1004,11 @@ __device__ __forceinline__ int quick_code_raw(const WaveRawQ<DT == 2 ? 8 : 4>& r
 // s_waitcnt vmcnt before reading raw.
 #define LSR_GLDS(step, insn) "s_add_u32 m0, m0, " #step "\n\ts_nop 0\n\t" insn "\n\t"
 template <int QB>
-__device__ __forceinline__ void quick_dma12(WaveRawQ<QB>& raw, const RenderArgs& a, uint32_t g)
+__device__ __forceinline__ void quick_dma12(WaveRawQ<QB>& raw, const RenderArgs& a, uint32_t g, const uint32_t* pI)
 {
     static_assert(offsetof(WaveRawQ<QB>, B) == 1024 && offsetof(WaveRawQ<QB>, rgb) == 2048 &&
-                  offsetof(WaveRawQ<QB>, W) == 2816 && offsetof(WaveRawQ<QB>, Q) == 5888, "raw layout");
+                  offsetof(WaveRawQ<QB>, W) == 2816 && offsetof(WaveRawQ<QB>, Q) == 5888 &&
+                  offsetof(WaveRawQ<QB>, nid) == 5888 + 768 * QB, "raw layout");
     const uint32_t base = (uint32_t)(uintptr_t)&raw;   // the LDS byte address (low half of the flat address)
     const float4* pA = a.splatA + g;
     const float4* pB = a.splatB + g;
@@ -1022,9 +1029,11 @@ __device__ __forceinline__ void quick_dma12(WaveRawQ<QB>& raw, const RenderArgs&
                      LSR_GLDS(1056, "global_load_lds_dwordx4 %[pQ], off")
                      LSR_GLDS(1008, "global_load_lds_dwordx4 %[pQ], off offset:16")
                      LSR_GLDS(1008, "global_load_lds_dwordx4 %[pQ], off offset:32")
+                     LSR_GLDS(1056, "global_load_lds_dword %[pI], off")
                      "s_mov_b32 m0, %[keep]"
                      : [keep] "=&s"(keep)
-                     : [base] "s"(base), [pA] "v"(pA), [pB] "v"(pB), [pR] "v"(pR), [pW] "v"(pW), [pQ] "v"(pQ)
+                     : [base] "s"(base), [pA] "v"(pA), [pB] "v"(pB), [pR] "v"(pR), [pW] "v"(pW), [pQ] "v"(pQ),
+                       [pI] "v"(pI)
                      : "memory", "scc");
     } else {
         asm volatile("s_mov_b32 %[keep], m0\n\t"
@@ -1042,9 +1051,11 @@ __device__ __forceinline__ void quick_dma12(WaveRawQ<QB>& raw, const RenderArgs&
                      LSR_GLDS(1008, "global_load_lds_dwordx4 %[pQ], off offset:48")
                      LSR_GLDS(1008, "global_load_lds_dwordx4 %[pQ], off offset:64")
                      LSR_GLDS(1008, "global_load_lds_dwordx4 %[pQ], off offset:80")
+                     LSR_GLDS(1104, "global_load_lds_dword %[pI], off")
                      "s_mov_b32 m0, %[keep]"
                      : [keep] "=&s"(keep)
-                     : [base] "s"(base), [pA] "v"(pA), [pB] "v"(pB), [pR] "v"(pR), [pW] "v"(pW), [pQ] "v"(pQ)
+                     : [base] "s"(base), [pA] "v"(pA), [pB] "v"(pB), [pR] "v"(pR), [pW] "v"(pW), [pQ] "v"(pQ),
+                       [pI] "v"(pI)
                      : "memory", "scc");
     }
 }
@@ -1089,9 +1100,10 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
     float T = 1.0f, cr = 0.f, cg = 0.f, cbl = 0.f;
     uint32_t last = 0;
     bool done = !inside;
-    // ids two chunks ahead; positions past the list read gid 0 (a valid row, never staged)
-    uint32_t gid_n = (rs + 64 + lane < re) ? a.point_list[rs + 64 + lane] : 0u;
-    if (rs < re) quick_dma12<QB>(raw, a, (rs + lane < re) ? a.point_list[rs + lane] : 0u);
+    // the first chunk's rows, and (in raw.nid) the ids of the chunk after it; positions
+    // past the list read the list's last id, and gid 0 (a valid row, never staged) is used
+    if (rs < re) quick_dma12<QB>(raw, a, (rs + lane < re) ? a.point_list[rs + lane] : 0u,
+                                 a.point_list + min(rs + 64 + lane, re - 1));
     for (uint32_t base = rs; base < re; base += 64) {
         if (wave_ballot(!done) == 0) break;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this chunk's rows have landed in raw
@@ -1118,13 +1130,9 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
             }
             st.Q[r] = make_uint4(qv[0], qv[1], qv[2], 0u);
         }
+        const uint32_t gid_n = idx + 64 < re ? raw.nid[lane] : 0u;
         wave_lds_fence();   // raw read, stage written: raw may be refilled
-        if (base + 64 < re) quick_dma12<QB>(raw, a, gid_n);
-        {
-            const uint32_t q = min(idx + 128, re - 1);   // re > base: a valid position
-            const uint32_t v = a.point_list[q];
-            gid_n = idx + 128 < re ? v : 0u;
-        }
+        if (base + 64 < re) quick_dma12<QB>(raw, a, gid_n, a.point_list + min(idx + 128, re - 1));
         const int n = __popcll(m);
         // the blend of k_render_fwd_quick_v, unchanged
         for (int j0 = 0; j0 < n; j0 += 2) {

@@ -6,8 +6,12 @@
 //   C: as B but a wave covers 1024 px (4 instructions per plane)
 //   D: 8 planes x 128 B per instruction (lanes of a 16-B piece pair across two
 //      16-px MFMA tiles, DPP row_ror:8 merge), a wave covering 64 px x all planes
-//   P<n>/PD<n>: A / D from a persistent grid of one n-wave workgroup per CU
-//      looping over the 64-px tiles (the level-resident decode's occupancy)
+//   E: 4 planes x 256 B per instruction (two register-bit <-> lane-bit swaps of
+//      four 16-px MFMA tiles), a wave covering 64 px x all planes
+//   P<n>/PD<n>/PE<n>/PC<n>: A / D / E / 1 KB-contiguous from a persistent grid of
+//      one n-wave workgroup per CU looping over the 64-px tiles (the
+//      level-resident decode's occupancy); ...R: each tile also reads its 16 KB
+//      weight tile (64 planes x 256 B) first, as the decode does
 // Build: hipcc --offload-arch=gfx950 -O3 store_pattern.hip -o store_pattern
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -55,16 +59,51 @@ __global__ void kD(float* out, int W, int H, int planes)
             }
 }
 
-template <bool D128>
-__global__ void kP(float* out, int W, int H, int planes, int nw)
+__global__ void kE(float* out, int W, int H, int planes)
+{
+    const int lane = threadIdx.x, a = lane >> 4, b = lane & 15;
+    const int nbx = W / 64;
+    const int bx = (blockIdx.x % nbx) * 64, y = blockIdx.x / nbx;
+    const size_t HW = (size_t)W * H;
+    for (int p0 = 0; p0 < planes; p0 += 16)
+        for (int q = 0; q < 4; q++) {
+            float* o = out + (size_t)(p0 + 4 * q + a) * HW + (size_t)y * W + bx + 4 * b;
+            *reinterpret_cast<float4*>(o) = make_float4((float)p0, (float)q, 1.f, 2.f);
+        }
+}
+
+// MODE 0 = A, 1 = D, 2 = E, 3 = 1 KB contiguous (256 px of one plane) per instruction, 256-px tiles
+template <int MODE, bool RD>
+__global__ void kP(float* out, const float* in, int W, int H, int planes, int nw)
 {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, li = lane & 15, lg = lane >> 4;
-    const int nbx = W / 64, ntile = nbx * H;
+    const int TW = MODE == 3 ? 256 : 64;
+    const int nbx = W / TW, ntile = nbx * H;
     const size_t HW = (size_t)W * H;
+    float acc = 0.f;
     for (int t = blockIdx.x * nw + w; t < ntile; t += gridDim.x * nw) {
-        const int bx = (t % nbx) * 64, y = t / nbx;
+        const int bx = (t % nbx) * TW, y = t / nbx;
+        if (RD) {
+            // 64 planes x 64 px of weights (16 KB per 64 px), as the decode's tile load
+            for (int r = 0; r < TW / 64; r++)
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    const float4 v = *reinterpret_cast<const float4*>(in + (size_t)(4 * j + lg) * HW + (size_t)y * W + bx + 64 * r + 4 * li);
+                    acc += v.x + v.y + v.z + v.w;
+                }
+        }
         for (int p0 = 0; p0 < planes; p0 += 16) {
-            if (D128) {
+            if (MODE == 3) {
+                for (int p = 0; p < 16; p++) {
+                    float* o = out + (size_t)(p0 + p) * HW + (size_t)y * W + bx + 4 * lane;
+                    *reinterpret_cast<float4*>(o) = make_float4((float)p0, acc, 1.f, 2.f);
+                }
+            } else if (MODE == 2) {
+                for (int q = 0; q < 4; q++) {
+                    float* o = out + (size_t)(p0 + 4 * q + lg) * HW + (size_t)y * W + bx + 4 * li;
+                    *reinterpret_cast<float4*>(o) = make_float4((float)p0, acc, 1.f, 2.f);
+                }
+            } else if (MODE == 1) {
                 for (int pp = 0; pp < 2; pp++)
                     for (int h = 0; h < 2; h++) {
                         const int k = 4 * (li >> 3) + lg;
@@ -74,7 +113,7 @@ __global__ void kP(float* out, int W, int H, int planes, int nw)
             } else {
                 for (int pb = 0; pb < 4; pb++) {
                     float* o = out + (size_t)(p0 + li) * HW + (size_t)y * W + bx + 16 * pb + 4 * lg;
-                    *reinterpret_cast<float4*>(o) = make_float4((float)p0, (float)pb, 1.f, 2.f);
+                    *reinterpret_cast<float4*>(o) = make_float4((float)p0, acc, 1.f, 2.f);
                 }
             }
         }
@@ -86,7 +125,10 @@ int main()
     const int W = 1280, H = 800, planes = 1536;
     const size_t bytes = (size_t)W * H * planes * 4;
     float* out;
+    float* in;
     if (hipMalloc(&out, bytes) != hipSuccess) return 1;
+    if (hipMalloc(&in, (size_t)W * H * 192 * 4) != hipSuccess) return 1;
+    hipMemset(in, 0, (size_t)W * H * 192 * 4);
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
@@ -106,13 +148,21 @@ int main()
     run("B 1 KB / instr, 256 px per wave", [&] { kB<256><<<(W / 256) * H, 64>>>(out, W, H, planes); });
     run("C 1 KB / instr, 1280 px per wave", [&] { kB<1280><<<(W / 1280) * H, 64>>>(out, W, H, planes); });
     run("D 8 planes x 128 B / instr, 64 px per wave", [&] { kD<<<(W / 64) * H, 64>>>(out, W, H, planes); });
-    for (int nw : {8, 12, 16}) {
-        char n1[64], n2[64];
-        snprintf(n1, 64, "P%d  A persistent, %d waves per CU", nw, nw);
-        snprintf(n2, 64, "PD%d D persistent, %d waves per CU", nw, nw);
-        run(n1, [&] { kP<false><<<256, 64 * nw>>>(out, W, H, planes, nw); });
-        run(n2, [&] { kP<true><<<256, 64 * nw>>>(out, W, H, planes, nw); });
+    run("E 4 planes x 256 B / instr, 64 px per wave", [&] { kE<<<(W / 64) * H, 64>>>(out, W, H, planes); });
+    for (int nw : {8, 16}) {
+        char n[96];
+        const char* nm[4] = {"A", "D", "E", "C"};
+        for (int m = 0; m < 4; m++)
+            for (int rd = 0; rd < 2; rd++) {
+                snprintf(n, 96, "P%s%d%s %d waves per CU%s", nm[m], nw, rd ? "R" : "", nw, rd ? " + weight reads" : "");
+                auto L = [&](auto k) { run(n, [&] { k<<<256, 64 * nw>>>(out, in, W, H, planes, nw); }); };
+                if (m == 0) rd ? L(kP<0, true>) : L(kP<0, false>);
+                if (m == 1) rd ? L(kP<1, true>) : L(kP<1, false>);
+                if (m == 2) rd ? L(kP<2, true>) : L(kP<2, false>);
+                if (m == 3) rd ? L(kP<3, true>) : L(kP<3, false>);
+            }
     }
     hipFree(out);
+    hipFree(in);
     return 0;
 }
