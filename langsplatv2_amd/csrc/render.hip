@@ -1063,6 +1063,19 @@ __device__ __forceinline__ void quick_dma12(WaveRawQ<QB>& raw, const RenderArgs&
 
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"   // the v255 clobber is the point: it sizes the allocation
+#ifndef LSR_QUICK_BAND
+#define LSR_QUICK_BAND 1
+#endif
+// Epilogue of the 192-channel quick kernel: channel q = N - 64 is register vN.
+#define LSR_QEPI(N) "buffer_store_dword v" #N ", %[vo], %[rs], %[so] offen\n\ts_add_u32 %[so], %[so], %[hw4]\n\t"
+#define LSR_QEPI10(h) LSR_QEPI(h##0) LSR_QEPI(h##1) LSR_QEPI(h##2) LSR_QEPI(h##3) LSR_QEPI(h##4) \
+                      LSR_QEPI(h##5) LSR_QEPI(h##6) LSR_QEPI(h##7) LSR_QEPI(h##8) LSR_QEPI(h##9)
+#define LSR_QEPI_ALL                                                                                     \
+    LSR_QEPI(64) LSR_QEPI(65) LSR_QEPI(66) LSR_QEPI(67) LSR_QEPI(68) LSR_QEPI(69)                        \
+    LSR_QEPI10(7) LSR_QEPI10(8) LSR_QEPI10(9) LSR_QEPI10(10) LSR_QEPI10(11) LSR_QEPI10(12) LSR_QEPI10(13) \
+    LSR_QEPI10(14) LSR_QEPI10(15) LSR_QEPI10(16) LSR_QEPI10(17) LSR_QEPI10(18) LSR_QEPI10(19)             \
+    LSR_QEPI10(20) LSR_QEPI10(21) LSR_QEPI10(22) LSR_QEPI10(23) LSR_QEPI10(24)                           \
+    LSR_QEPI(250) LSR_QEPI(251) LSR_QEPI(252) LSR_QEPI(253) LSR_QEPI(254) LSR_QEPI(255)
 template <int DT>
 __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_render_fwd_quick_d(RenderArgs a)
 {
@@ -1072,7 +1085,16 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
     const Cam& c = a.cam;
     const WaveTile wt(a);
     const int lane = threadIdx.x;
-    const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
+    // one wave per 16x4 band of the tile (LSR_QUICK_BAND; else per 8x8 block): each of
+    // the 192 channel stores then writes 64-B row pieces instead of 32-B ones
+    constexpr int BW = LSR_QUICK_BAND ? 16 : 8, BH = 64 / BW;
+    PixMap pm(c, wt.tile, lane + (wt.sub << 6));
+    if constexpr (LSR_QUICK_BAND) {
+        pm.bx = (wt.tile % c.gx) * LSR_TILE;
+        pm.by = (wt.tile / c.gx) * LSR_TILE + wt.sub * BH;
+        pm.px = pm.bx + (lane & (BW - 1));
+        pm.py = pm.by + lane / BW;
+    }
     const bool inside = pm.px < c.W && pm.py < c.H;
     const float pfx = (float)pm.px, pfy = (float)pm.py;
     const uint32_t rs = a.tile_start[wt.tile], re = a.tile_start[wt.tile + 1];
@@ -1110,8 +1132,8 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
         const uint32_t idx = base + lane;
         const bool valid = idx < re;
         const float4 A = raw.A[lane], B = raw.B[lane];
-        const bool ok = valid && block_overlap(A.x, A.y, __float_as_uint(B.w), pm.bx, pm.by) &&
-                        block_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, pm.bx, pm.by);
+        const bool ok = valid && rect_overlap(A.x, A.y, __float_as_uint(B.w), pm.bx, pm.by, BW - 1, BH - 1) &&
+                        rect_overlap_exact(A.x, A.y, A.z, A.w, B.x, B.z, pm.bx, pm.by, (float)(BW - 1), (float)(BH - 1));
         const uint64_t m = wave_ballot(ok);
         if (ok) {
             const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -1199,20 +1221,35 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
         a.out_color[HW + pix] = fmaf(T, c.bg[1], cg);
         a.out_color[2 * HW + pix] = fmaf(T, c.bg[2], cbl);
         float* const o = a.out_lang + pix;
-        for (int q = 0; q < Dq; q++) {
-            float v;
-            uint32_t sv;
-            asm volatile(
-                "s_mov_b32 %[sv], m0\n\t"
-                "s_set_gpr_idx_on %[q], gpr_idx(SRC0)\n\t"
-                "s_nop 0\n\t"
-                "v_mov_b32 %[v], v64\n\t"
-                "s_set_gpr_idx_off\n\t"
-                "s_mov_b32 m0, %[sv]"
-                : [v] "=v"(v), [sv] "=&s"(sv)
-                : [q] "s"(q)
-                : "memory");
-            o[(size_t)q * HW] = v;
+        if (Dq == 192 && (uint64_t)HW * 192u * 4u < 0x80000000ull) {
+            // all 192 channels straight from v64..v255 by buffer stores, the channel
+            // plane's byte offset in an SGPR stepped by HW * 4: two instructions per
+            // channel instead of the index-mode read, the M0 save / restore and a
+            // 64-bit address per store
+            const __amdgpu_buffer_rsrc_t ro =
+                __builtin_amdgcn_make_buffer_rsrc(a.out_lang, 0, (int)(HW * 192u * 4u), 0x00020000);
+            uint32_t so;
+            asm volatile("s_mov_b32 %[so], 0\n\t"
+                         LSR_QEPI_ALL
+                         : [so] "=&s"(so)
+                         : [vo] "v"((uint32_t)pix * 4u), [rs] "s"(ro), [hw4] "s"((uint32_t)HW * 4u)
+                         : "memory", "scc");
+        } else {
+            for (int q = 0; q < Dq; q++) {
+                float v;
+                uint32_t sv;
+                asm volatile(
+                    "s_mov_b32 %[sv], m0\n\t"
+                    "s_set_gpr_idx_on %[q], gpr_idx(SRC0)\n\t"
+                    "s_nop 0\n\t"
+                    "v_mov_b32 %[v], v64\n\t"
+                    "s_set_gpr_idx_off\n\t"
+                    "s_mov_b32 m0, %[sv]"
+                    : [v] "=v"(v), [sv] "=&s"(sv)
+                    : [q] "s"(q)
+                    : "memory");
+                o[(size_t)q * HW] = v;
+            }
         }
     }
 }
