@@ -49,13 +49,13 @@ METRIC = "frames/s fwd+bwd @ 1M Gaussians 1080p 3+16ch; achieved HBM GB/s"
 HBM_PEAK_GBPS = 8000.0   # MI355X spec (MI355X_MICROARCH.md chip table)
 
 
-def settings(cam, dev, sh_degree, include_feature, quick=False, quick_dim=None):
+def settings(cam, dev, sh_degree, include_feature, quick=False, quick_dim=None, quick_layout=None):
     return GaussianRasterizationSettings(
         image_height=cam["H"], image_width=cam["W"], tanfovx=cam["tanfovx"], tanfovy=cam["tanfovy"],
         bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=cam["viewmatrix"].to(dev),
         projmatrix=cam["projmatrix"].to(dev), sh_degree=sh_degree, campos=cam["campos"].to(dev),
         prefiltered=False, debug=False, include_feature=include_feature, quick_render=quick,
-        language_feature_dim=quick_dim)
+        language_feature_dim=quick_dim, language_feature_layout=quick_layout)
 
 
 def algorithmic_bytes(g, rs, D, S):
@@ -287,29 +287,38 @@ def fwd_fps(g, dev, sh_degree, D, W=1280, H=800, iters=20):
 def quick_fps(N, dev, W=1280, H=800, iters=20):
     """The evaluation path behind the reference's "450+ FPS" (README.md:1, eval_lerf.py:210-220):
     quick render of 3 levels x top-4 codes into 192 channels, then the 3 x 64 x 512 codebook
-    decode + L2 normalise, at 1.0 Mpix."""
+    decode + L2 normalise, at 1.0 Mpix.  The headline fields time the map in the pixel-major
+    layout (language_feature_layout="hwc": the same values, a (192,H,W) view the reference's
+    .view(3, 64, H, W).view(3, 64, H*W) + einsum accept unchanged; tests/test_quick_layout.py);
+    `reference_layout` times the reference's contiguous (192,H,W) map."""
     from langsplatv2_amd import quick
     cam = make_camera(W, H)
     g = make_gaussians(N, cam, seed=0, sh_degree=3, quick_k=4)
     t = {k: v.to(dev) for k, v in g.items() if isinstance(v, torch.Tensor)}
-    r = GaussianRasterizer(settings(cam, dev, 3, False, quick=True))
     z = torch.zeros_like(t["means3D"])
     cb = torch.randn(3, 64, 512, device=dev)
 
-    def render():
-        with torch.no_grad():
-            return r(means3D=t["means3D"], means2D=z, opacities=t["opacities"], shs=t["shs"],
-                     language_feature_weights_quick=t["language_feature_weights_quick"],
-                     language_feature_indices=t["language_feature_indices"], scales=t["scales"],
-                     rotations=t["rotations"])[1]
+    def measure(layout):
+        r = GaussianRasterizer(settings(cam, dev, 3, False, quick=True, quick_layout=layout))
 
-    def both():
-        quick.decode_language_features(render(), cb)
-    s_render = timeit(render, iters)
-    s_total = timeit(both, iters)
-    return dict(workload=f"{N} Gaussians {W}x{H}, quick 3x top-4 -> 192 ch + 3x64x512 decode + L2 norm",
-                render_fps=round(1.0 / s_render, 1), render_decode_fps=round(1.0 / s_total, 1),
-                render_ms=round(s_render * 1e3, 4), decode_ms=round((s_total - s_render) * 1e3, 4))
+        def render():
+            with torch.no_grad():
+                return r(means3D=t["means3D"], means2D=z, opacities=t["opacities"], shs=t["shs"],
+                         language_feature_weights_quick=t["language_feature_weights_quick"],
+                         language_feature_indices=t["language_feature_indices"], scales=t["scales"],
+                         rotations=t["rotations"])[1]
+
+        def both():
+            quick.decode_language_features(render(), cb)
+        s_render = timeit(render, iters)
+        s_total = timeit(both, iters)
+        return dict(render_fps=round(1.0 / s_render, 1), render_decode_fps=round(1.0 / s_total, 1),
+                    render_ms=round(s_render * 1e3, 4), decode_ms=round((s_total - s_render) * 1e3, 4))
+    out = dict(workload=f"{N} Gaussians {W}x{H}, quick 3x top-4 -> 192 ch + 3x64x512 decode + L2 norm",
+               layout="hwc (pixel-major quick map, language_feature_layout='hwc')")
+    out.update(measure("hwc"))
+    out["reference_layout"] = measure(None)
+    return out
 
 
 def _free_port() -> int:

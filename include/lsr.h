@@ -42,7 +42,8 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 9   /* 9 (r05): LSR_OPT_LISTS_MAX_MB; LSR_BIN_ORDERED removed */
+#define LSR_ABI_VERSION 10  /* 10 (r05): lsr_settings.quick_layout, lsr_quick_decode_run weight_layout;
+                               9 (r05): LSR_OPT_LISTS_MAX_MB; LSR_BIN_ORDERED removed */
 
 enum {
     LSR_OK = 0,
@@ -73,7 +74,13 @@ typedef struct lsr_settings {
     int include_feature;      /* dense language channels on */
     int quick_render;         /* sparse (weights, indices) language channels on */
     int quick_dim;            /* Dq; 0 selects the reference default 192 */
+    int quick_layout;         /* LSR_LAYOUT_CHW (0, the reference's (Dq,H,W)) or LSR_LAYOUT_HWC:
+                                 out_lang is written pixel-major, (H,W,Dq) — every pixel's Dq
+                                 weights in one 768-B row at Dq = 192 (the quick_render kernel
+                                 with K = 12, Dq = 192 only; else LSR_EUNSUPPORTED) */
 } lsr_settings;
+
+enum { LSR_LAYOUT_CHW = 0, LSR_LAYOUT_HWC = 1 };
 
 enum { LSR_INDEX_F32 = 0, LSR_INDEX_I32 = 1, LSR_INDEX_I64 = 2 };
 
@@ -230,11 +237,13 @@ int lsr_quick_decode(const float* weight_map, const float* codebooks, int L, int
  * lsr_quick_decode_prepare writes the codebook-only part (fragments, norm
  * factor) into a caller-owned device buffer of lsr_quick_decode_plan_bytes
  * bytes (0 = unsupported shape); lsr_quick_decode_run decodes a frame with it.
- * The plan is valid until the codebooks change. */
+ * The plan is valid until the codebooks change.  weight_layout: LSR_LAYOUT_CHW
+ * for an (L*K, H, W) weight map, LSR_LAYOUT_HWC for a pixel-major (H, W, L*K)
+ * one (lsr_settings.quick_layout); the output is (L, Df, H, W) either way. */
 size_t lsr_quick_decode_plan_bytes(int L, int K, int Df, int normalize);
 int lsr_quick_decode_prepare(const float* codebooks, int L, int K, int Df, int normalize, void* plan, void* stream);
-int lsr_quick_decode_run(const float* weight_map, const void* plan, int L, int K, int Df, int H, int W, int normalize,
-                         float eps, float* out, void* stream);
+int lsr_quick_decode_run(const float* weight_map, int weight_layout, const void* plan, int L, int K, int Df, int H,
+                         int W, int normalize, float eps, float* out, void* stream);
 
 /* Fused top-k soft codes (replaces softmax_to_topk_soft_code,
  * utils/vq_utils.py:9-24; get_weights_and_indices, :26-40; the per-level

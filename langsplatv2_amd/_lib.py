@@ -21,6 +21,7 @@ LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_GRAD, LSR_BUF_DECODE, LSR_
 LSR_BUF_GUARD, LSR_BUF_SPARSE, LSR_BUF_GRAD_LANG, LSR_BUF_LISTS = 7, 8, 9, 10
 LSR_INDEX_F32, LSR_INDEX_I32, LSR_INDEX_I64 = 0, 1, 2
 LSR_GWS_GEOM, LSR_GWS_LANG = 1, 2
+LSR_LAYOUT_CHW, LSR_LAYOUT_HWC = 0, 1
 
 _vp = ctypes.c_void_p
 
@@ -42,6 +43,7 @@ class Settings(ctypes.Structure):
         ("include_feature", ctypes.c_int),
         ("quick_render", ctypes.c_int),
         ("quick_dim", ctypes.c_int),
+        ("quick_layout", ctypes.c_int),
     ]
 
 
@@ -159,8 +161,8 @@ def load(path: str | None = None):
     lib.lsr_quick_decode_plan_bytes.restype = ctypes.c_size_t
     lib.lsr_quick_decode_prepare.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]
     lib.lsr_quick_decode_prepare.restype = ctypes.c_int
-    lib.lsr_quick_decode_run.argtypes = [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                         ctypes.c_int, ctypes.c_int, ctypes.c_float, _vp, _vp]
+    lib.lsr_quick_decode_run.argtypes = [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float, _vp, _vp]
     lib.lsr_quick_decode_run.restype = ctypes.c_int
     lib.lsr_topk_code_forward.argtypes = [_vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp,
                                           _vp, ctypes.c_int, ctypes.c_int, _vp]

@@ -188,6 +188,8 @@ int validate(const lsr_settings* s, const lsr_inputs* in)
     if (!s || !in) return LSR_EINVAL;
     if (s->image_height <= 0 || s->image_width <= 0 || in->P < 0) return LSR_EINVAL;
     if (!s->bg || !s->viewmatrix || !s->projmatrix || !s->campos) return LSR_EINVAL;
+    if (s->quick_layout != LSR_LAYOUT_CHW && s->quick_layout != LSR_LAYOUT_HWC) return LSR_EINVAL;
+    if (s->quick_layout == LSR_LAYOUT_HWC && !s->quick_render) return LSR_EINVAL;
     if (in->P > 0) {
         if (!in->means3D || !in->opacities) return LSR_EINVAL;
         if ((in->shs == nullptr) == (in->colors_precomp == nullptr)) return LSR_EINVAL;
@@ -203,6 +205,13 @@ int validate(const lsr_settings* s, const lsr_inputs* in)
             return LSR_EINVAL;
         if (in->quick_index_dtype < LSR_INDEX_F32 || in->quick_index_dtype > LSR_INDEX_I64) return LSR_EINVAL;
         if ((size_t)quick_dim(s) * 256 + 64 * (32 + 12 + 8 * (size_t)in->quick_k) > 65536) return LSR_EUNSUPPORTED;
+        if (s->quick_layout == LSR_LAYOUT_HWC) {
+            // the pixel-major map is written by the 12-code, 192-channel LDS-DMA kernel only
+            if (in->quick_k != 12 || quick_dim(s) != 192) return LSR_EUNSUPPORTED;
+            if (in->P > 0 && (((uintptr_t)in->language_feature_weights_quick % 16) != 0 ||
+                              ((uintptr_t)in->language_feature_indices % 16) != 0))
+                return LSR_EUNSUPPORTED;
+        }
     } else if (s->include_feature) {
         if (in->P > 0 && (!in->language_feature_precomp || in->lang_dim <= 0)) return LSR_EINVAL;
         if (lang_set_for(in->lang_dim) < 0) return LSR_EUNSUPPORTED;
@@ -250,6 +259,7 @@ RenderArgs make_render_args(const lsr_settings* s, const lsr_inputs* in, const C
     a.qidx_dtype = in->quick_index_dtype;
     a.K = s->quick_render ? in->quick_k : 0;
     a.Dq = s->quick_render ? quick_dim(s) : 0;
+    a.quick_hwc = s->quick_render && s->quick_layout == LSR_LAYOUT_HWC;
     a.point_list = (const uint32_t*)(bin + BL.point_list);
     a.tile_start = (const uint32_t*)(img + IL.tile_start);
     a.final_T = (float*)(img + IL.final_T);
@@ -315,15 +325,18 @@ int lsr_quick_decode_prepare(const float* codebooks, int L, int K, int Df, int n
     return LSR_OK;
 }
 
-int lsr_quick_decode_run(const float* weight_map, const void* plan, int L, int K, int Df, int H, int W, int normalize,
-                         float eps, float* out, void* stream)
+int lsr_quick_decode_run(const float* weight_map, int weight_layout, const void* plan, int L, int K, int Df, int H,
+                         int W, int normalize, float eps, float* out, void* stream)
 {
     if (L < 0 || H < 0 || W < 0 || Df <= 0 || (Df % 16) != 0) return LSR_EINVAL;
+    if (weight_layout != LSR_LAYOUT_CHW && weight_layout != LSR_LAYOUT_HWC) return LSR_EINVAL;
     if (K != 64) return LSR_EUNSUPPORTED;
     if (L == 0 || H == 0 || W == 0) return LSR_OK;
     if (!weight_map || !plan || !out) return LSR_EINVAL;
+    // the pixel-major map is read in 32-B pieces by the level-resident kernel (Df <= 512)
+    if (weight_layout == LSR_LAYOUT_HWC && (Df > 512 || ((uintptr_t)weight_map % 16) != 0)) return LSR_EUNSUPPORTED;
     if (lsr::launch_quick_decode_run(weight_map, nullptr, L, K, Df, H, W, normalize, eps, plan, out,
-                                     (hipStream_t)stream) != hipSuccess)
+                                     (hipStream_t)stream, weight_layout == LSR_LAYOUT_HWC) != hipSuccess)
         return LSR_EHIP;
     return LSR_OK;
 }

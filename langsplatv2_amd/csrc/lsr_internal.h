@@ -72,6 +72,7 @@ struct RenderArgs {
     const float* qw;             // quick weights (P,K) or NULL
     const void* qi;              // quick indices (P,K)
     int qidx_dtype, K, Dq;
+    int quick_hwc;   // out_lang pixel-major (H, W, Dq) (lsr_settings.quick_layout)
     const uint32_t* point_list;
     const uint32_t* tile_start;  // T+1
     float* final_T;
@@ -130,7 +131,8 @@ hipError_t launch_knn_dist2(const float* points, int64_t N, float* out, uint8_t*
 size_t quick_decode_workspace_bytes(int L, int K, int Df, int normalize);
 hipError_t launch_quick_decode_prepare(const float* cb, int L, int K, int Df, int normalize, void* ws, hipStream_t st);
 hipError_t launch_quick_decode_run(const float* wmap, const float* cb, int L, int K, int Df, int H, int W,
-                                   int normalize, float eps, const void* ws, float* out, hipStream_t st);
+                                   int normalize, float eps, const void* ws, float* out, hipStream_t st,
+                                   bool hwc = false);
 hipError_t launch_quick_decode(const float* wmap, const float* cb, int L, int K, int Df, int H, int W, int normalize,
                                float eps, void* ws, float* out, hipStream_t st);
 

@@ -462,11 +462,14 @@ __device__ __forceinline__ void dec_swap_lanebit(f32x4q& X, f32x4q& Y)
     }
 }
 
-template <bool NORM, bool VEC>
+// HWC: the weight map is pixel-major (H, W, lk) (LSR_LAYOUT_HWC): a lane's 8 codes
+// of one pixel are 32 contiguous bytes, two 16-B loads instead of eight 4-B ones
+// from eight channel planes.
+template <bool NORM, bool VEC, bool HWC = false>
 __global__ void __launch_bounds__(64 * LSR_DEC2_WAVES, 1)
     k_quick_decode_l(const float* __restrict__ wmap, int Df, int W, int H, const uint4* __restrict__ frag,
                      const float* __restrict__ scales, const uint4* __restrict__ nfrag,
-                     const float* __restrict__ nscales, float* __restrict__ out, float eps, int nwg)
+                     const float* __restrict__ nscales, float* __restrict__ out, float eps, int nwg, int lk)
 {
     extern __shared__ uint4 sfr[];   // [db][s][lane][hi, lo] codebook, then 4 blocks of the norm factor
     const int l = (int)blockIdx.x / nwg, wi = (int)blockIdx.x % nwg;
@@ -498,13 +501,29 @@ __global__ void __launch_bounds__(64 * LSR_DEC2_WAVES, 1)
             const int xa = bx + 16 * pb + li;
             const size_t pa = (size_t)y * W + min(xa, W - 1);
             const bool in = ok && xa < W;
+            if constexpr (HWC) {
+                const float4* wp = reinterpret_cast<const float4*>(wmap + pa * lk + l * 64 + 8 * lg);
 #pragma unroll
-            for (int s2 = 0; s2 < 2; s2++)
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    const float v = wmap[(size_t)(l * 64 + 32 * s2 + 8 * lg + j) * HW + pa];
-                    raw[pb][s2][j] = in ? v : 0.f;
+                for (int s2 = 0; s2 < 2; s2++) {
+                    const float4 v0 = wp[8 * s2], v1 = wp[8 * s2 + 1];
+                    raw[pb][s2][0] = in ? v0.x : 0.f;
+                    raw[pb][s2][1] = in ? v0.y : 0.f;
+                    raw[pb][s2][2] = in ? v0.z : 0.f;
+                    raw[pb][s2][3] = in ? v0.w : 0.f;
+                    raw[pb][s2][4] = in ? v1.x : 0.f;
+                    raw[pb][s2][5] = in ? v1.y : 0.f;
+                    raw[pb][s2][6] = in ? v1.z : 0.f;
+                    raw[pb][s2][7] = in ? v1.w : 0.f;
                 }
+            } else {
+#pragma unroll
+                for (int s2 = 0; s2 < 2; s2++)
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        const float v = wmap[(size_t)(l * 64 + 32 * s2 + 8 * lg + j) * HW + pa];
+                        raw[pb][s2][j] = in ? v : 0.f;
+                    }
+            }
         }
     };
     int t = wi * LSR_DEC2_WAVES + w;
@@ -712,7 +731,7 @@ hipError_t launch_quick_decode_prepare(const float* cb, int L, int K, int Df, in
 }
 
 hipError_t launch_quick_decode_run(const float* wmap, const float* cb, int L, int K, int Df, int H, int W,
-                                   int normalize, float eps, const void* ws, float* out, hipStream_t st)
+                                   int normalize, float eps, const void* ws, float* out, hipStream_t st, bool hwc)
 {
     if (L == 0 || H == 0 || W == 0) return hipSuccess;
 #ifdef LSR_DECODE_F32
@@ -741,9 +760,17 @@ hipError_t launch_quick_decode_run(const float* wmap, const float* cb, int L, in
         auto run = [&](auto kern) {
             (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
             kern<<<(unsigned)(nwg * L), 64 * LSR_DEC2_WAVES, lds, st>>>(wmap, Df, W, H, frag, scales, nfrag, nscales,
-                                                                      out, eps, nwg);
+                                                                      out, eps, nwg, L * K);
         };
-        if (normalize) {
+        if (hwc) {
+            if (normalize) {
+                if (vec) run(k_quick_decode_l<true, true, true>);
+                else run(k_quick_decode_l<true, false, true>);
+            } else {
+                if (vec) run(k_quick_decode_l<false, true, true>);
+                else run(k_quick_decode_l<false, false, true>);
+            }
+        } else if (normalize) {
             if (vec) run(k_quick_decode_l<true, true>);
             else run(k_quick_decode_l<true, false>);
         } else {
@@ -753,6 +780,7 @@ hipError_t launch_quick_decode_run(const float* wmap, const float* cb, int L, in
         return hipGetLastError();
     }
 #endif
+    if (hwc) return hipErrorInvalidValue;   // the pixel-major map: level-resident kernel only
     const unsigned nb = (unsigned)(((W + 63) / 64) * H);
     if (normalize) {
         if (vec)

@@ -1066,6 +1066,22 @@ __device__ __forceinline__ void quick_dma12(WaveRawQ<QB>& raw, const RenderArgs&
 #ifndef LSR_QUICK_BAND
 #define LSR_QUICK_BAND 1
 #endif
+// Pixel-major epilogue (LSR_LAYOUT_HWC): the pixel's 192 weights, v64..v255, as 48
+// 16-B stores into its 768-B row (immediate offsets from one address).
+#define LSR_QHWC(a, b, off) "global_store_dwordx4 %[p], v[" #a ":" #b "], off offset:" #off "\n\t"
+#define LSR_QHWC_ALL \
+    LSR_QHWC(64, 67, 0) LSR_QHWC(68, 71, 16) LSR_QHWC(72, 75, 32) LSR_QHWC(76, 79, 48) \
+    LSR_QHWC(80, 83, 64) LSR_QHWC(84, 87, 80) LSR_QHWC(88, 91, 96) LSR_QHWC(92, 95, 112) \
+    LSR_QHWC(96, 99, 128) LSR_QHWC(100, 103, 144) LSR_QHWC(104, 107, 160) LSR_QHWC(108, 111, 176) \
+    LSR_QHWC(112, 115, 192) LSR_QHWC(116, 119, 208) LSR_QHWC(120, 123, 224) LSR_QHWC(124, 127, 240) \
+    LSR_QHWC(128, 131, 256) LSR_QHWC(132, 135, 272) LSR_QHWC(136, 139, 288) LSR_QHWC(140, 143, 304) \
+    LSR_QHWC(144, 147, 320) LSR_QHWC(148, 151, 336) LSR_QHWC(152, 155, 352) LSR_QHWC(156, 159, 368) \
+    LSR_QHWC(160, 163, 384) LSR_QHWC(164, 167, 400) LSR_QHWC(168, 171, 416) LSR_QHWC(172, 175, 432) \
+    LSR_QHWC(176, 179, 448) LSR_QHWC(180, 183, 464) LSR_QHWC(184, 187, 480) LSR_QHWC(188, 191, 496) \
+    LSR_QHWC(192, 195, 512) LSR_QHWC(196, 199, 528) LSR_QHWC(200, 203, 544) LSR_QHWC(204, 207, 560) \
+    LSR_QHWC(208, 211, 576) LSR_QHWC(212, 215, 592) LSR_QHWC(216, 219, 608) LSR_QHWC(220, 223, 624) \
+    LSR_QHWC(224, 227, 640) LSR_QHWC(228, 231, 656) LSR_QHWC(232, 235, 672) LSR_QHWC(236, 239, 688) \
+    LSR_QHWC(240, 243, 704) LSR_QHWC(244, 247, 720) LSR_QHWC(248, 251, 736) LSR_QHWC(252, 255, 752)
 // Epilogue of the 192-channel quick kernel: channel q = N - 64 is register vN.
 #define LSR_QEPI(N) "buffer_store_dword v" #N ", %[vo], %[rs], %[so] offen\n\ts_add_u32 %[so], %[so], %[hw4]\n\t"
 #define LSR_QEPI10(h) LSR_QEPI(h##0) LSR_QEPI(h##1) LSR_QEPI(h##2) LSR_QEPI(h##3) LSR_QEPI(h##4) \
@@ -1221,7 +1237,10 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
         a.out_color[HW + pix] = fmaf(T, c.bg[1], cg);
         a.out_color[2 * HW + pix] = fmaf(T, c.bg[2], cbl);
         float* const o = a.out_lang + pix;
-        if (Dq == 192 && (uint64_t)HW * 192u * 4u < 0x80000000ull) {
+        if (a.quick_hwc) {   // Dq == 192 (lsr_api validate)
+            float* const row = a.out_lang + pix * 192;
+            asm volatile(LSR_QHWC_ALL : : [p] "v"(row) : "memory");
+        } else if (Dq == 192 && (uint64_t)HW * 192u * 4u < 0x80000000ull) {
             // all 192 channels straight from v64..v255 by buffer stores, the channel
             // plane's byte offset in an SGPR stepped by HW * 4: two instructions per
             // channel instead of the index-mode read, the M0 save / restore and a
@@ -1281,6 +1300,7 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
     const int T = a.cam.gx * a.cam.gy;
     if (T == 0) return hipSuccess;
     if (a.qw) {
+        if (a.quick_hwc && !(quick_dma_ok(a) && a.Dq == 192)) return hipErrorInvalidValue;
         if (quick_dma_ok(a)) {
             switch (a.qidx_dtype) {
                 case LSR_INDEX_F32: k_render_fwd_quick_d<0><<<T * 4, 64, 0, st>>>(a); break;

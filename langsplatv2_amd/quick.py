@@ -29,7 +29,9 @@ from .rasterizer import _stream
 def decode_language_features(weight_map: torch.Tensor, codebooks: torch.Tensor, normalize: bool = True,
                              eps: float = 1e-10) -> torch.Tensor:
     """weight_map (L*K, H, W) fp32 CUDA, codebooks (L, K, Df) fp32 CUDA ->
-    features (L, Df, H, W); L2-normalised over Df per pixel when `normalize`."""
+    features (L, Df, H, W); L2-normalised over Df per pixel when `normalize`.
+    A pixel-major weight map (strides (1, L*K*W, L*K): the rasterizer's
+    language_feature_layout="hwc" output) is read as it is (LSR_LAYOUT_HWC)."""
     if weight_map.dim() != 3 or codebooks.dim() != 3:
         raise ValueError("decode_language_features: weight_map must be (L*K, H, W) and codebooks (L, K, Df)")
     L, K, Df = codebooks.shape
@@ -40,12 +42,15 @@ def decode_language_features(weight_map: torch.Tensor, codebooks: torch.Tensor, 
         raise RuntimeError("decode_language_features: tensors must be on the ROCm device (there is no CPU path)")
     if K != 64 or Df % 16 != 0:
         raise ValueError("decode_language_features: K must be 64 and Df a multiple of 16")
-    wm = weight_map.contiguous().float()
+    hwc = (weight_map.dtype == torch.float32 and weight_map.stride() == (1, D * W, D) and Df <= 512
+           and weight_map.data_ptr() % 16 == 0 and H * W > 1)
+    wm = weight_map if hwc else weight_map.contiguous().float()
     cb = codebooks.contiguous().float()
     out = torch.empty((L, Df, H, W), dtype=torch.float32, device=weight_map.device)
     lib = _lib.load()
     plan = decode_plan(cb, normalize)
-    rc = lib.lsr_quick_decode_run(wm.data_ptr(), plan.data_ptr(), L, K, Df, H, W, int(bool(normalize)), float(eps),
+    rc = lib.lsr_quick_decode_run(wm.data_ptr(), _lib.LSR_LAYOUT_HWC if hwc else _lib.LSR_LAYOUT_CHW,
+                                  plan.data_ptr(), L, K, Df, H, W, int(bool(normalize)), float(eps),
                                   out.data_ptr(), _stream(weight_map.device))
     _lib.check(rc, "lsr_quick_decode_run")
     return out

@@ -4,7 +4,14 @@ Surface (what gaussian_renderer/__init__.py:15,37-54,108-119 uses):
   GaussianRasterizationSettings  NamedTuple, the 14 fields of
                                  gaussian_renderer/__init__.py:37-52, plus an
                                  optional trailing `language_feature_dim`
-                                 (quick-path output channels, default 192).
+                                 (quick-path output channels, default 192) and
+                                 `language_feature_layout` ("chw", the default
+                                 and the reference's layout, or "hwc": the
+                                 quick map stored pixel-major, returned as a
+                                 (Dq,H,W) view with strides (1, Dq*W, Dq);
+                                 values identical, and the reference's
+                                 consumers' .view(3, 64, H, W).view(3, 64, H*W)
+                                 + einsum run on it unchanged).
   GaussianRasterizer(raster_settings)  nn.Module;
       forward(means3D, means2D, opacities, shs=None, colors_precomp=None,
               language_feature_precomp=None,
@@ -143,6 +150,19 @@ class GaussianRasterizationSettings(NamedTuple):
     include_feature: bool = False
     quick_render: bool = False
     language_feature_dim: Optional[int] = None
+    language_feature_layout: Optional[str] = None
+
+
+def _quick_layout(rs) -> int:
+    """LSR_LAYOUT_* of the quick map ("chw" / None: the reference's (Dq,H,W); "hwc": pixel-major)."""
+    lay = rs.language_feature_layout if len(rs) > 15 else None
+    if lay is None or lay == "chw":
+        return _lib.LSR_LAYOUT_CHW
+    if lay == "hwc":
+        if not rs.quick_render:
+            raise ValueError('language_feature_layout="hwc" applies to the quick_render map only')
+        return _lib.LSR_LAYOUT_HWC
+    raise ValueError(f'language_feature_layout must be "chw" or "hwc", got {lay!r}')
 
 
 def _present(t: Optional[torch.Tensor]) -> bool:
@@ -188,7 +208,7 @@ def _settings_struct(rs: GaussianRasterizationSettings, dev) -> tuple:
     s = _lib.Settings(int(rs.image_height), int(rs.image_width), float(rs.tanfovx), float(rs.tanfovy),
                       bg.data_ptr(), float(rs.scale_modifier), view.data_ptr(), proj.data_ptr(),
                       int(rs.sh_degree), campos.data_ptr(), int(bool(rs.prefiltered)), int(bool(rs.debug)),
-                      int(bool(rs.include_feature)), int(bool(rs.quick_render)), int(qdim))
+                      int(bool(rs.include_feature)), int(bool(rs.quick_render)), int(qdim), _quick_layout(rs))
     return s, (bg, view, proj, campos)
 
 
@@ -253,7 +273,10 @@ def _run_forward(means3D, sh, colors_precomp, language_feature_precomp, language
                       means3D_c.data_ptr(), _ptr(sh_c), _ptr(col_c), opac_c.data_ptr(), _ptr(sc_c), _ptr(rot_c),
                       _ptr(cov_c), _ptr(lang_c), _ptr(qw_c), _ptr(qi_c))
     color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
-    lang_out = torch.empty((Dout, H, W), dtype=torch.float32, device=dev)
+    if quick and _quick_layout(rs) == _lib.LSR_LAYOUT_HWC:
+        lang_out = torch.empty((H, W, Dout), dtype=torch.float32, device=dev).permute(2, 0, 1)
+    else:
+        lang_out = torch.empty((Dout, H, W), dtype=torch.float32, device=dev)
     radii = torch.empty((N,), dtype=torch.int32, device=dev)
     out = _lib.FwdOut(color.data_ptr(), lang_out.data_ptr() if Dout else None, radii.data_ptr())
     out.grad_ws_request = int(grad_request)

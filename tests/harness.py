@@ -102,7 +102,7 @@ def cov3d_torch(s, q):
     return torch.stack([S[:, 0, 0], S[:, 0, 1], S[:, 0, 2], S[:, 1, 1], S[:, 1, 2], S[:, 2, 2]], 1)
 
 
-def settings_for(case, device):
+def settings_for(case, device, layout=None):
     from diff_gaussian_rasterization import GaussianRasterizationSettings
     cam, g = case["cam"], case["g"]
     quick = case["quick"]
@@ -112,7 +112,7 @@ def settings_for(case, device):
         viewmatrix=cam["viewmatrix"].to(device), projmatrix=cam["projmatrix"].to(device),
         sh_degree=g.get("sh_degree", 0), campos=cam["campos"].to(device), prefiltered=False, debug=False,
         include_feature=("language_feature_precomp" in g) and not quick, quick_render=quick,
-        language_feature_dim=g.get("quick_dim") if quick else None)
+        language_feature_dim=g.get("quick_dim") if quick else None, language_feature_layout=layout)
 
 
 def gpu_inputs(case, device, requires_grad=True):
@@ -127,10 +127,11 @@ def gpu_inputs(case, device, requires_grad=True):
     return t
 
 
-def run_gpu_forward(case, device):
-    """Forward through the library with workspace buffers decoded."""
+def run_gpu_forward(case, device, lang_layout=None):
+    """Forward through the library with workspace buffers decoded (lang_layout:
+    the quick map's language_feature_layout, None = the reference's (Dq,H,W))."""
     from langsplatv2_amd import layout, rasterizer
-    rs = settings_for(case, device)
+    rs = settings_for(case, device, lang_layout)
     t = gpu_inputs(case, device, requires_grad=False)
     e = torch.empty(0, device=device)
     color, lang, radii, M, bufs, _, _, _ = rasterizer._run_forward(

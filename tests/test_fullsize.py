@@ -184,16 +184,19 @@ def test_cfg5_binning_and_image_properties(gpu):
 
 # --- the paths the bench and tools time at full size ---
 
-def test_quick_1mpix_whole_frame(gpu, oracle_lib):
+@pytest.mark.parametrize("lang_layout", ["chw", "hwc"])
+def test_quick_1mpix_whole_frame(gpu, oracle_lib, lang_layout):
     """bench.py quick_1mpix's render: 1M Gaussians, 1280x800, 3 levels x top-4
     codes -> 192 channels (k_render_fwd_quick_d, the LDS-DMA quick kernel,
     reference eval_lerf.py:210-220).  The whole binning and the whole frame's
-    colour, 192-channel weight map, final_T and n_contrib."""
+    colour, 192-channel weight map, final_T and n_contrib; the map in the
+    reference's (Dq,H,W) layout and pixel-major (language_feature_layout="hwc",
+    the layout bench.py's quick line renders)."""
     case = make_case(N=1_000_000, W=1280, H=800, sh_degree=3, quick_k=4, seed=0)
     ref = oracle_lib.forward(oracle_problem(case), nthreads=_threads())
-    got = run_gpu_forward(case, gpu)
+    got = run_gpu_forward(case, gpu, lang_layout)
     assert got["lang"].shape == (192, 800, 1280)
-    _compare_forward(got, ref, True, case, "quick_1mpix")
+    _compare_forward(got, ref, True, case, "quick_1mpix_" + lang_layout)
     assert float(np.abs(ref["lang"]).max()) > 0.1
 
 

@@ -21,7 +21,8 @@ W, H, N = 1280, 800, 1_000_000
 cam = make_camera(W, H)
 g = make_gaussians(N, cam, seed=0, sh_degree=3, quick_k=4)
 t = {k: v.to(dev) for k, v in g.items() if isinstance(v, torch.Tensor)}
-r = GaussianRasterizer(bench.settings(cam, dev, 3, False, quick=True))
+# LSR_AB_LAYOUT=hwc: the pixel-major quick map (language_feature_layout)
+r = GaussianRasterizer(bench.settings(cam, dev, 3, False, quick=True, quick_layout=os.environ.get("LSR_AB_LAYOUT")))
 z = torch.zeros_like(t["means3D"])
 cb = torch.randn(3, 64, 512, device=dev)
 

@@ -89,7 +89,8 @@ assert lib.lsr_quick_decode(None, None, 3, 64, 500, 4, 4, 1, 1e-10, None, ALLOC,
 assert lib.lsr_quick_decode(None, None, 3, 32, 512, 4, 4, 1, 1e-10, None, ALLOC, None, None) == EUNSUP
 assert lib.lsr_quick_decode_plan_bytes(3, 32, 512, 1) == 0 and lib.lsr_quick_decode_plan_bytes(3, 64, 512, 1) > 0
 assert lib.lsr_quick_decode_prepare(None, -1, 64, 512, 1, None, None) == EINVAL
-assert lib.lsr_quick_decode_run(None, None, 3, 64, 17, 4, 4, 1, 1e-10, None, None) == EINVAL
+assert lib.lsr_quick_decode_run(None, 0, None, 3, 64, 17, 4, 4, 1, 1e-10, None, None) == EINVAL
+assert lib.lsr_quick_decode_run(None, 2, None, 3, 64, 16, 4, 4, 1, 1e-10, None, None) == EINVAL
 assert lib.lsr_knn_dist2(None, -5, None, ALLOC, None, None) == EINVAL
 assert lib.lsr_adam_step(None, None, None, None, -1, 0.1, 0.9, 0.999, 1e-8, 0.0, 1, None) == EINVAL
 calls += 9

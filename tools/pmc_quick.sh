@@ -15,5 +15,5 @@ run S1 "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VMEM SQ_
 run S2 "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_WR"
 cd $ROOT
 python tools/pmc_traffic.py $OUT/F $OUT/W $OUT/quick_traffic.json > $OUT/traffic.txt && cat $OUT/traffic.txt
-python tools/pmc_kernel.py $OUT/S1 k_render_fwd_quick_v $OUT/S2 k_render_fwd_quick_v $OUT/S1 k_quick_decode_l $OUT/S2 k_quick_decode_l > $OUT/sq.txt 2>&1; cat $OUT/sq.txt
+python tools/pmc_kernel.py $OUT/S1 k_render_fwd_quick_d $OUT/S2 k_render_fwd_quick_d $OUT/S1 k_quick_decode_l $OUT/S2 k_quick_decode_l > $OUT/sq.txt 2>&1; cat $OUT/sq.txt
 echo "pmc quick $TAG done"
