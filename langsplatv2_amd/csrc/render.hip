@@ -1179,6 +1179,10 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
             const int j1 = two ? j0 + 1 : j0;
             const float4 A0 = st.A[j0], B0 = st.B[j0];
             const float4 A1 = st.A[j1], B1 = st.B[j1];
+            // the colours read with the geometry, and the blend below as selects
+            // (the same fmaf on the same operands where a pixel takes the
+            // candidate): no LDS round trip or exec-mask branch per candidate
+            const float4 C0 = st.C[j0], C1 = st.C[j1];
             const float p0 = splat_power(A0.z, A0.w, B0.x, A0.x - pfx, A0.y - pfy);
             const float p1 = splat_power(A1.z, A1.w, B1.x, A1.x - pfx, A1.y - pfy);
             bool ok0 = !done && !(p0 > 0.0f || p0 < B0.z);
@@ -1197,14 +1201,11 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
                 ok0 = ok0 && !term;
                 ok1 = ok1 && !term;
                 aT0 = ok0 ? al0 * T : 0.f;
-                if (ok0) {
-                    const float4 C0 = st.C[j0];
-                    cr = fmaf(C0.x, aT0, cr);
-                    cg = fmaf(C0.y, aT0, cg);
-                    cbl = fmaf(C0.z, aT0, cbl);
-                    T = test_T;
-                    last = (uint32_t)__float_as_int(B0.w);
-                }
+                cr = ok0 ? fmaf(C0.x, aT0, cr) : cr;
+                cg = ok0 ? fmaf(C0.y, aT0, cg) : cg;
+                cbl = ok0 ? fmaf(C0.z, aT0, cbl) : cbl;
+                T = ok0 ? test_T : T;
+                last = ok0 ? (uint32_t)__float_as_int(B0.w) : last;
             }
             {
                 const float test_T = T * (1.0f - al1);
@@ -1212,14 +1213,11 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
                 done = done || term;
                 ok1 = ok1 && !term;
                 aT1 = ok1 ? al1 * T : 0.f;
-                if (ok1) {
-                    const float4 C1 = st.C[j1];
-                    cr = fmaf(C1.x, aT1, cr);
-                    cg = fmaf(C1.y, aT1, cg);
-                    cbl = fmaf(C1.z, aT1, cbl);
-                    T = test_T;
-                    last = (uint32_t)__float_as_int(B1.w);
-                }
+                cr = ok1 ? fmaf(C1.x, aT1, cr) : cr;
+                cg = ok1 ? fmaf(C1.y, aT1, cg) : cg;
+                cbl = ok1 ? fmaf(C1.z, aT1, cbl) : cbl;
+                T = ok1 ? test_T : T;
+                last = ok1 ? (uint32_t)__float_as_int(B1.w) : last;
             }
             if (wave_any(ok0)) LSR_QV_UPDATE(aT0, st.Q[j0], st.Wt[j0][0], st.Wt[j0][1], st.Wt[j0][2]);
             if (wave_any(ok1)) LSR_QV_UPDATE(aT1, st.Q[j1], st.Wt[j1][0], st.Wt[j1][1], st.Wt[j1][2]);
