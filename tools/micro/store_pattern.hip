@@ -103,6 +103,15 @@ __global__ void kP(float* out, const float* in, int W, int H, int planes, int nw
                     float* o = out + (size_t)(p0 + 4 * q + lg) * HW + (size_t)y * W + bx + 4 * li;
                     *reinterpret_cast<float4*>(o) = make_float4((float)p0, acc, 1.f, 2.f);
                 }
+            } else if (MODE >= 4) {   // E with a cache-policy modifier: 4 sc1, 5 nt, 6 sc0 sc1
+                for (int q = 0; q < 4; q++) {
+                    float* o = out + (size_t)(p0 + 4 * q + lg) * HW + (size_t)y * W + bx + 4 * li;
+                    typedef float f4v __attribute__((ext_vector_type(4)));
+                    const f4v v = {(float)p0, acc, 1.f, 2.f};
+                    if (MODE == 4) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(o), "v"(v) : "memory");
+                    if (MODE == 5) asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(o), "v"(v) : "memory");
+                    if (MODE == 6) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(o), "v"(v) : "memory");
+                }
             } else if (MODE == 1) {
                 for (int pp = 0; pp < 2; pp++)
                     for (int h = 0; h < 2; h++) {
@@ -149,6 +158,17 @@ int main()
     run("C 1 KB / instr, 1280 px per wave", [&] { kB<1280><<<(W / 1280) * H, 64>>>(out, W, H, planes); });
     run("D 8 planes x 128 B / instr, 64 px per wave", [&] { kD<<<(W / 64) * H, 64>>>(out, W, H, planes); });
     run("E 4 planes x 256 B / instr, 64 px per wave", [&] { kE<<<(W / 64) * H, 64>>>(out, W, H, planes); });
+    {
+        const char* nm[3] = {"E sc1", "E nt", "E sc0 sc1"};
+        for (int m = 0; m < 3; m++) {
+            char n[96];
+            snprintf(n, 96, "P%s 8 waves per CU", nm[m]);
+            auto L = [&](auto k) { run(n, [&] { k<<<256, 64 * 8>>>(out, in, W, H, planes, 8); }); };
+            if (m == 0) L(kP<4, false>);
+            if (m == 1) L(kP<5, false>);
+            if (m == 2) L(kP<6, false>);
+        }
+    }
     for (int nw : {8, 16}) {
         char n[96];
         const char* nm[4] = {"A", "D", "E", "C"};
