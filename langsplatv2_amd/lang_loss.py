@@ -102,3 +102,58 @@ def language_cos_loss(weight_map: torch.Tensor, codebooks: torch.Tensor, seg: to
     codebooks (layers, 64, Df) or (64, Df), seg (H, W) int, features (S, Df).
     Differentiable w.r.t. weight_map and codebooks."""
     return _LanguageCosLoss.apply(weight_map, codebooks, seg, features)
+
+
+def language_feature_loss(weight_map: torch.Tensor, codebooks: torch.Tensor, seg: torch.Tensor,
+                          features: torch.Tensor, layer_idx: int = 0, normalize: bool = False, cos: bool = True,
+                          l1: bool = False) -> torch.Tensor:
+    """The feature-phase loss of train.py:151-167 under each of its flags:
+
+        f = gaussians.compute_layer_feature_map(weight_map, layer_idx)     scene/gaussian_model.py:533-543
+            # sum over levels i <= layer_idx of codebooks[i].T @ W[i K:(i+1) K], earlier levels detached
+        if --normalize: f = f / (f.norm(dim=0, keepdim=True) + 1e-10)
+        loss = [--cos_loss] cos_loss(f * mask, gt * mask) + [--l1_loss] l1_loss(f * mask, gt * mask)
+
+    weight_map (L*K, H, W) (the rasterizer's dense language map), codebooks
+    (L, K, Df), seg (H, W) int segment ids (-1 = masked), features (S, Df).
+
+    The configuration train.sh trains with (layer 0, cosine loss; vq_layer_num
+    1) runs the fused kernel (`language_cos_loss`); so does --normalize with the
+    cosine loss alone, because the cosine of a per-pixel rescaled feature is
+    the cosine of the feature (the only difference is the 1e-10 added to the
+    norm: relative 1e-10 / |f_p|, far below fp32 resolution for any pixel with
+    |f_p| > 1e-3; tests/test_lang_loss_variants.py).  The other flags (--l1_loss,
+    the elementwise L1 over Df x H x W, and layer_idx > 0) are the reference's
+    own tensor formulation on the device (torch ops over the Df-wide map)."""
+    if codebooks.dim() != 3:
+        raise ValueError("language_feature_loss: codebooks must be (layers, K, Df)")
+    L, K, Df = codebooks.shape
+    D, H, W = weight_map.shape
+    if D < (layer_idx + 1) * K or not (0 <= layer_idx < L):
+        raise ValueError(f"language_feature_loss: layer_idx {layer_idx} needs levels 0..{layer_idx} of the "
+                         f"{L} codebooks and {(layer_idx + 1) * K} weight-map channels (got {D})")
+    if not (cos or l1):
+        raise ValueError("language_feature_loss: at least one of cos / l1 (train.py:161-167 sums them)")
+    if layer_idx == 0 and cos and not l1:
+        return language_cos_loss(weight_map[:K], codebooks, seg, features)
+    for t, n in ((weight_map, "weight_map"), (codebooks, "codebooks"), (seg, "seg"), (features, "features")):
+        if not t.is_cuda:
+            raise RuntimeError(f"language_feature_loss: {n} must be a ROCm device tensor (there is no CPU path)")
+    wm = weight_map.reshape(D, -1)
+    f = None
+    for i in range(layer_idx + 1):   # compute_layer_feature_map
+        fi = (codebooks[i].T @ wm[i * K:(i + 1) * K]).view(Df, H, W)
+        f = fi if f is None else fi + f.detach()
+    if normalize:
+        f = f / (f.norm(dim=0, keepdim=True) + 1e-10)
+    S = features.shape[0]
+    sg = seg.long()
+    mask = (sg != -1).unsqueeze(0)                                   # scene/cameras.py:80
+    gt = features[sg].permute(2, 0, 1)                               # features[-1] where masked, as the reference
+    fm, gm = f * mask, gt * mask
+    loss = torch.zeros((), dtype=f.dtype, device=f.device)
+    if cos:
+        loss = loss + (1 - torch.nn.functional.cosine_similarity(fm, gm, dim=0).mean())   # utils/loss_utils.py:24-25
+    if l1:
+        loss = loss + (fm - gm).abs().mean()                                          # utils/loss_utils.py:18-19
+    return loss

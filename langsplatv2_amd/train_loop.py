@@ -244,6 +244,8 @@ class LanguageState:
                     "scales": scales.detach(), "rotations": rotations.detach()}
         self.logits = logits.detach().clone().contiguous().requires_grad_(True)
         self.codebooks = codebooks.detach().clone().contiguous().requires_grad_(True)
+        # one codebook level (vq_layer_num 1, train.sh and the paper): L levels of K codes
+        # would render L*K dense language channels, past the rasterizer's 64
         if self.codebooks.dim() != 3 or self.codebooks.shape[0] != 1:
             raise ValueError("LanguageState: codebooks must be (1, K, Df): vq_layer_num 1 (the paper's setting)")
         self.topk = topk
@@ -285,11 +287,20 @@ def render_language(cam: dict, ls: LanguageState, bg: torch.Tensor) -> dict:
             "radii": radii}
 
 
-def language_view_loss(pkg: dict, ls: LanguageState, seg: torch.Tensor, features: torch.Tensor) -> torch.Tensor:
-    """train.py:151-166 with --cos_loss: 1 - cos(CB^T W * mask, gt * mask), the
-    ground truth gathered from the view's (S, Df) table by its segment map."""
-    from .lang_loss import language_cos_loss
-    return language_cos_loss(pkg["language_feature_weight_map"], ls.codebooks, seg, features)
+def language_view_loss(pkg: dict, ls: LanguageState, seg: torch.Tensor, features: torch.Tensor,
+                       normalize: bool = False, cos: bool = True, l1: bool = False,
+                       iteration: int = 0) -> torch.Tensor:
+    """train.py:151-167: the decoded feature map of level layer_idx =
+    min(int(iteration / 10000 * layer_num), layer_num - 1) (always 0 with the
+    single codebook level this phase trains, see LanguageState) against the
+    view's ground truth gathered from its (S, Df) table by its segment map,
+    under the --normalize / --cos_loss / --l1_loss flags (default: train.sh's
+    --cos_loss alone, the fused kernel)."""
+    from .lang_loss import language_feature_loss
+    layer_num = ls.codebooks.shape[0]
+    layer_idx = min(int(iteration / 10000 * layer_num), layer_num - 1)
+    return language_feature_loss(pkg["language_feature_weight_map"], ls.codebooks, seg, features,
+                                 layer_idx=layer_idx, normalize=normalize, cos=cos, l1=l1)
 
 
 class LanguageTrainer:
@@ -297,9 +308,11 @@ class LanguageTrainer:
     view, the exchange sums the R ranks' (logits, codebooks) gradients in one
     bucket, every rank steps its replica (= --accum_iter R on one GPU)."""
 
-    def __init__(self, ls: LanguageState, bg: torch.Tensor, group=None, fused_adam: bool = True):
+    def __init__(self, ls: LanguageState, bg: torch.Tensor, group=None, fused_adam: bool = True,
+                 normalize: bool = False, cos_loss: bool = True, l1_loss: bool = False):
         self.ls = ls
         self.bg = bg
+        self.loss_flags = dict(normalize=normalize, cos=cos_loss, l1=l1_loss)   # train.py --normalize / --cos_loss / --l1_loss
         self.opt = ls.optimizer(fused=fused_adam)
         self.exchange = dp.ViewShardedExchange(ls.params(), with_stats=False, group=group,
                                                names=list(LANG_PARAM_NAMES))
@@ -308,7 +321,7 @@ class LanguageTrainer:
 
     def step(self, cam: dict, seg: torch.Tensor, features: torch.Tensor) -> float:
         pkg = render_language(cam, self.ls, self.bg)
-        loss = language_view_loss(pkg, self.ls, seg, features)
+        loss = language_view_loss(pkg, self.ls, seg, features, iteration=self.iteration, **self.loss_flags)
         loss.backward()
         params = self.ls.params()
         grads, _, _ = self.exchange.exchange([p.grad for p in params])
@@ -322,14 +335,14 @@ class LanguageTrainer:
 
 
 def accumulate_language_views(ls: LanguageState, opt, cams: list, segs: list, feats: list, bg: torch.Tensor,
-                              grads_out: list | None = None):
+                              grads_out: list | None = None, **loss_flags):
     """Single-GPU reference of one feature-phase DP step: len(cams) iterations
     with accum_iter = len(cams) (train.py:261-263), one optimizer step
     (`grads_out` receives copies of the accumulated gradients it steps with)."""
     losses = []
     for cam, seg, feat in zip(cams, segs, feats):
         pkg = render_language(cam, ls, bg)
-        loss = language_view_loss(pkg, ls, seg, feat)
+        loss = language_view_loss(pkg, ls, seg, feat, **loss_flags)
         loss.backward()
         losses.append(float(loss.detach()))
     if grads_out is not None:
