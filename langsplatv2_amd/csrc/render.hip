@@ -1063,9 +1063,6 @@ __device__ __forceinline__ void quick_dma12(WaveRawQ<QB>& raw, const RenderArgs&
 
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"   // the v255 clobber is the point: it sizes the allocation
-#ifndef LSR_QUICK_BAND
-#define LSR_QUICK_BAND 1
-#endif
 // Pixel-major epilogue (LSR_LAYOUT_HWC): the pixel's 192 weights, v64..v255, as 48
 // 16-B stores into its 768-B row (immediate offsets from one address).
 #define LSR_QHWC(a, b, off) "global_store_dwordx4 %[p], v[" #a ":" #b "], off offset:" #off "\n\t"
@@ -1092,7 +1089,11 @@ __device__ __forceinline__ void quick_dma12(WaveRawQ<QB>& raw, const RenderArgs&
     LSR_QEPI10(14) LSR_QEPI10(15) LSR_QEPI10(16) LSR_QEPI10(17) LSR_QEPI10(18) LSR_QEPI10(19)             \
     LSR_QEPI10(20) LSR_QEPI10(21) LSR_QEPI10(22) LSR_QEPI10(23) LSR_QEPI10(24)                           \
     LSR_QEPI(250) LSR_QEPI(251) LSR_QEPI(252) LSR_QEPI(253) LSR_QEPI(254) LSR_QEPI(255)
-template <int DT>
+// BAND: one wave per 16x4 band of the tile (the channel-major map: each of the
+// 192 channel stores then writes 64-B row pieces instead of 32-B ones, render
+// -2.5 %); else one wave per 8x8 block (the pixel-major map, whose stores are
+// per-pixel rows: the tighter block cull wins, -5.6 %)
+template <int DT, bool BAND>
 __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_render_fwd_quick_d(RenderArgs a)
 {
     constexpr int QB = DT == 2 ? 8 : 4;
@@ -1101,11 +1102,9 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
     const Cam& c = a.cam;
     const WaveTile wt(a);
     const int lane = threadIdx.x;
-    // one wave per 16x4 band of the tile (LSR_QUICK_BAND; else per 8x8 block): each of
-    // the 192 channel stores then writes 64-B row pieces instead of 32-B ones
-    constexpr int BW = LSR_QUICK_BAND ? 16 : 8, BH = 64 / BW;
+    constexpr int BW = BAND ? 16 : 8, BH = 64 / BW;
     PixMap pm(c, wt.tile, lane + (wt.sub << 6));
-    if constexpr (LSR_QUICK_BAND) {
+    if constexpr (BAND) {
         pm.bx = (wt.tile % c.gx) * LSR_TILE;
         pm.by = (wt.tile / c.gx) * LSR_TILE + wt.sub * BH;
         pm.px = pm.bx + (lane & (BW - 1));
@@ -1300,10 +1299,18 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
     if (a.qw) {
         if (a.quick_hwc && !(quick_dma_ok(a) && a.Dq == 192)) return hipErrorInvalidValue;
         if (quick_dma_ok(a)) {
-            switch (a.qidx_dtype) {
-                case LSR_INDEX_F32: k_render_fwd_quick_d<0><<<T * 4, 64, 0, st>>>(a); break;
-                case LSR_INDEX_I32: k_render_fwd_quick_d<1><<<T * 4, 64, 0, st>>>(a); break;
-                default: k_render_fwd_quick_d<2><<<T * 4, 64, 0, st>>>(a); break;
+            if (a.quick_hwc) {
+                switch (a.qidx_dtype) {
+                    case LSR_INDEX_F32: k_render_fwd_quick_d<0, false><<<T * 4, 64, 0, st>>>(a); break;
+                    case LSR_INDEX_I32: k_render_fwd_quick_d<1, false><<<T * 4, 64, 0, st>>>(a); break;
+                    default: k_render_fwd_quick_d<2, false><<<T * 4, 64, 0, st>>>(a); break;
+                }
+            } else {
+                switch (a.qidx_dtype) {
+                    case LSR_INDEX_F32: k_render_fwd_quick_d<0, true><<<T * 4, 64, 0, st>>>(a); break;
+                    case LSR_INDEX_I32: k_render_fwd_quick_d<1, true><<<T * 4, 64, 0, st>>>(a); break;
+                    default: k_render_fwd_quick_d<2, true><<<T * 4, 64, 0, st>>>(a); break;
+                }
             }
             return hipGetLastError();
         }

@@ -77,7 +77,7 @@ def test_loss_variants_match_reference(gpu, L, layer_idx, normalize, cos, l1):
     got = language_feature_loss(wg, cg, seg.to(gpu), feat.to(gpu), layer_idx=layer_idx, normalize=normalize,
                                 cos=cos, l1=l1)
     got.backward()
-    assert abs(float(got) - float(ref)) <= LOSS_ATOL, (float(got), float(ref))
+    assert abs(float(got.detach()) - float(ref)) <= LOSS_ATOL, (float(got.detach()), float(ref))
     for name, a, b in (("weight_map", wg.grad, w64.grad), ("codebooks", cg.grad, c64.grad)):
         a = a.double().cpu().numpy()
         b = b.numpy()
@@ -92,7 +92,11 @@ def test_loss_variants_match_reference(gpu, L, layer_idx, normalize, cos, l1):
 @pytest.mark.gpu
 def test_trainer_step_with_l1_and_normalize(gpu):
     """LanguageTrainer (one rank) with --normalize --cos_loss --l1_loss takes the
-    same step as the single-GPU accumulate_language_views with those flags."""
+    step accumulate_language_views takes with those flags: the same loss, and
+    gradients equal up to the rasterizer backward's float-atomic summation
+    order (the parameters after Adam are not compared: with eps 1e-15 it turns
+    the rounding noise on zero-signal logits into +-lr steps, see
+    test_0_train_dp_lang.py)."""
     from langsplatv2_amd.train_loop import LanguageTrainer, accumulate_language_views
     from test_0_train_dp_lang import _scene
     flags = dict(normalize=True, cos=True, l1=True)
@@ -100,8 +104,11 @@ def test_trainer_step_with_l1_and_normalize(gpu):
     _, _, _, ls_b = _scene(gpu)
     tr = LanguageTrainer(ls_a, torch.zeros(3, device=gpu), normalize=True, cos_loss=True, l1_loss=True)
     la = tr.step(cams[0], segs[0], feats[0])
+    ga = [g.detach().clone() for g in tr.last_grads]
+    gb = []
     lb = accumulate_language_views(ls_b, ls_b.optimizer(), [cams[0]], [segs[0]], [feats[0]],
-                                   torch.zeros(3, device=gpu), **flags)
+                                   torch.zeros(3, device=gpu), grads_out=gb, **flags)
     assert np.isfinite(la) and la == lb[0]
-    for pa, pb in zip(ls_a.params(), ls_b.params()):
-        assert torch.equal(pa, pb)
+    for a, b in zip(ga, gb):
+        assert float(b.abs().max()) > 0.0
+        assert float((a - b).abs().max()) <= 1e-5 * float(b.abs().max()) + 1e-12
