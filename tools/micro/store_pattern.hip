@@ -103,6 +103,16 @@ __global__ void kP(float* out, const float* in, int W, int H, int planes, int nw
                     float* o = out + (size_t)(p0 + 4 * q + lg) * HW + (size_t)y * W + bx + 4 * li;
                     *reinterpret_cast<float4*>(o) = make_float4((float)p0, acc, 1.f, 2.f);
                 }
+            } else if (MODE == 7 || MODE == 8) {
+                // channel-last output ((H, W, planes): a pixel's planes contiguous), the 16
+                // planes p0.. of the tile's 64 pixels: 7 = 4 px x 64 B per instruction
+                // (lane: px 4 q + lg... 16 planes = 64 B per pixel), 8 = per instruction
+                // 1 KB = 16 pixels x 64 B
+                for (int q = 0; q < 4; q++) {
+                    const int px = MODE == 7 ? (16 * q + li) : (16 * q + li);
+                    float* o = out + ((size_t)y * W + bx + px) * planes + p0 + 4 * lg;
+                    *reinterpret_cast<float4*>(o) = make_float4((float)p0, acc, 1.f, 2.f);
+                }
             } else if (MODE >= 4) {   // E with a cache-policy modifier: 4 sc1, 5 nt, 6 sc0 sc1
                 for (int q = 0; q < 4; q++) {
                     float* o = out + (size_t)(p0 + 4 * q + lg) * HW + (size_t)y * W + bx + 4 * li;
@@ -158,6 +168,14 @@ int main()
     run("C 1 KB / instr, 1280 px per wave", [&] { kB<1280><<<(W / 1280) * H, 64>>>(out, W, H, planes); });
     run("D 8 planes x 128 B / instr, 64 px per wave", [&] { kD<<<(W / 64) * H, 64>>>(out, W, H, planes); });
     run("E 4 planes x 256 B / instr, 64 px per wave", [&] { kE<<<(W / 64) * H, 64>>>(out, W, H, planes); });
+    {
+        // channel-last: each wave's 64 pixels x 1536 planes is one 384-KB contiguous block
+        char n[96];
+        snprintf(n, 96, "PL8 channel-last, 16 px x 64 B per instruction, 8 waves per CU");
+        run(n, [&] { kP<7, false><<<256, 64 * 8>>>(out, in, W, H, planes, 8); });
+        snprintf(n, 96, "PL8R channel-last + weight reads, 8 waves per CU");
+        run(n, [&] { kP<7, true><<<256, 64 * 8>>>(out, in, W, H, planes, 8); });
+    }
     {
         const char* nm[3] = {"E sc1", "E nt", "E sc0 sc1"};
         for (int m = 0; m < 3; m++) {
