@@ -26,7 +26,13 @@ dev = torch.device("cuda:0")
 cam = make_camera(cfg["W"], cfg["H"])
 g0 = make_gaussians(cfg["N"], cam, seed=0, sh_degree=3, lang_dim=D)
 keys = ("means3D", "shs", "opacities", "scales", "rotations", "language_feature_precomp")
-if os.environ.get("LSR_SPATIAL"):
+if os.environ.get("LSR_SPATIAL") == "y":
+    # layout probe: the Gaussians sorted by their projected screen row (y / z)
+    # only, so a wave's lanes share rows but spread over the columns
+    m = g0["means3D"].double()
+    perm = torch.argsort(m[:, 1] / m[:, 2].clamp_min(1e-6))
+    g0 = {k: (v[perm] if isinstance(v, torch.Tensor) and v.shape[:1] == perm.shape else v) for k, v in g0.items()}
+elif os.environ.get("LSR_SPATIAL"):
     # layout probe: the same Gaussians in a spatial order (3-D Morton code of the
     # means, 10 bits per axis) instead of the generator's random order
     m = g0["means3D"].double()
