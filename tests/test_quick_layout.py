@@ -100,3 +100,24 @@ def test_hwc_unsupported_shapes_raise(gpu):
     case = make_case(**dict(QUICK, quick_k=2))   # 3 levels x top-2 = 6 codes
     with pytest.raises(RuntimeError):
         _render_quick(case, gpu, "hwc")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("idx_dtype", [torch.int32, torch.int64])
+def test_hwc_integer_indices(gpu, idx_dtype):
+    """The pixel-major map with int32 / int64 code indices (u5: the integer
+    index forms of language_feature_indices) equals the fp32-index map."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    case = make_case(**dict(QUICK, W=61, H=47))
+    t = {k: v.to(gpu) for k, v in case["g"].items() if isinstance(v, torch.Tensor)}
+    r = GaussianRasterizer(raster_settings=settings_for(case, gpu, "hwc"))
+    kw = {k: t[k] for k in ("shs", "colors_precomp", "scales", "rotations") if k in t}
+    outs = []
+    for qi in (t["language_feature_indices"], t["language_feature_indices"].round().to(idx_dtype)):
+        with torch.no_grad():
+            _, lang, _ = r(means3D=t["means3D"], means2D=torch.zeros_like(t["means3D"]), opacities=t["opacities"],
+                           language_feature_weights_quick=t["language_feature_weights_quick"],
+                           language_feature_indices=qi.contiguous(), **kw)
+        outs.append(lang)
+    assert outs[1].stride() == (1, 192 * 61, 192)
+    assert torch.equal(outs[0], outs[1])

@@ -44,7 +44,7 @@ for S in $STEPS; do
     LSR_STEPS=2 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/${TAG}_pmcF -o run --output-format csv -- python3 $ROOT/tools/pmc_step.py > $OUT/${TAG}_pmcF.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
     LSR_STEPS=2 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/${TAG}_pmcW -o run --output-format csv -- python3 $ROOT/tools/pmc_step.py > $OUT/${TAG}_pmcW.log 2>&1 || { echo "pmc write failed"; exit 1; }
     cd $ROOT
-    UNITS=$(python tools/bwd_work.py --units-only 2>/dev/null || echo 3490000)
+    UNITS=$(python tools/lst_units.py 2>/dev/null || echo 3490000)
     python tools/pmc_issue.py $OUT/${TAG}_sq1 $OUT/${TAG}_sq2 $OUT/${TAG}_pmc_issue.json --units k_render_bwd_mf=$UNITS > $OUT/${TAG}_pmc_issue.txt
     python tools/pmc_traffic.py $OUT/${TAG}_pmcF $OUT/${TAG}_pmcW $OUT/${TAG}_pmc_traffic.json > $OUT/${TAG}_pmc_traffic.txt
     cat $OUT/${TAG}_pmc_issue.txt $OUT/${TAG}_pmc_traffic.txt
