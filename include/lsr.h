@@ -42,7 +42,8 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 10  /* 10 (r05): lsr_settings.quick_layout, lsr_quick_decode_run weight_layout;
+#define LSR_ABI_VERSION 11  /* 11 (r05): LSR_INDEX_PACKED, lsr_quick_pack_codes;
+                               10 (r05): lsr_settings.quick_layout, lsr_quick_decode_run weight_layout;
                                9 (r05): LSR_OPT_LISTS_MAX_MB; LSR_BIN_ORDERED removed */
 
 enum {
@@ -82,7 +83,15 @@ typedef struct lsr_settings {
 
 enum { LSR_LAYOUT_CHW = 0, LSR_LAYOUT_HWC = 1 };
 
-enum { LSR_INDEX_F32 = 0, LSR_INDEX_I32 = 1, LSR_INDEX_I64 = 2 };
+/* Code-index dtypes of language_feature_indices.  LSR_INDEX_PACKED: an (N, 4)
+ * uint32 array written by lsr_quick_pack_codes (K = 12 codes per Gaussian as
+ * bytes code + 1, 0 = no code, 16-B rows): what the quick render stages per
+ * candidate, so a caller rendering many views of one model converts the
+ * reference's fp32 indices once instead of every frame.  Forward and backward
+ * of quick_render with K = 12, Dq <= 192 and 16-B aligned weights / indices
+ * only (else LSR_EUNSUPPORTED); bytes above Dq are dropped as out-of-range
+ * codes are. */
+enum { LSR_INDEX_F32 = 0, LSR_INDEX_I32 = 1, LSR_INDEX_I64 = 2, LSR_INDEX_PACKED = 3 };
 
 /* GaussianRasterizer.forward kwargs (gaussian_renderer/__init__.py:108-119). */
 typedef struct lsr_inputs {
@@ -240,6 +249,13 @@ int lsr_quick_decode(const float* weight_map, const float* codebooks, int L, int
  * The plan is valid until the codebooks change.  weight_layout: LSR_LAYOUT_CHW
  * for an (L*K, H, W) weight map, LSR_LAYOUT_HWC for a pixel-major (H, W, L*K)
  * one (lsr_settings.quick_layout); the output is (L, Df, H, W) either way. */
+/* The packed code rows (LSR_INDEX_PACKED) of K = 12 code indices per Gaussian:
+ * indices (N, 12) of LSR_INDEX_F32 / I32 / I64 index_dtype (fp32 values round
+ * half up, u5), packed (N, 4) uint32, 16-B aligned: byte m of row i holds
+ * code m + 1 when 0 <= code < quick_dim (0 selects 192), else 0. */
+int lsr_quick_pack_codes(const void* indices, int index_dtype, int64_t N, int K, int quick_dim, uint32_t* packed,
+                         void* stream);
+
 size_t lsr_quick_decode_plan_bytes(int L, int K, int Df, int normalize);
 int lsr_quick_decode_prepare(const float* codebooks, int L, int K, int Df, int normalize, void* plan, void* stream);
 int lsr_quick_decode_run(const float* weight_map, int weight_layout, const void* plan, int L, int K, int Df, int H,

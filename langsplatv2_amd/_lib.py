@@ -19,7 +19,7 @@ LSR_ENONFINITE = 6
 LSR_ELISTS = 7
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_GRAD, LSR_BUF_DECODE, LSR_BUF_KNN, LSR_BUF_LOSS = 0, 1, 2, 3, 4, 5, 6
 LSR_BUF_GUARD, LSR_BUF_SPARSE, LSR_BUF_GRAD_LANG, LSR_BUF_LISTS = 7, 8, 9, 10
-LSR_INDEX_F32, LSR_INDEX_I32, LSR_INDEX_I64 = 0, 1, 2
+LSR_INDEX_F32, LSR_INDEX_I32, LSR_INDEX_I64, LSR_INDEX_PACKED = 0, 1, 2, 3
 LSR_GWS_GEOM, LSR_GWS_LANG = 1, 2
 LSR_LAYOUT_CHW, LSR_LAYOUT_HWC = 0, 1
 
@@ -126,7 +126,7 @@ class BwdOut(ctypes.Structure):
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
 
 EXPORTS = ("lsr_forward", "lsr_backward", "lsr_mark_visible", "lsr_quick_decode", "lsr_quick_decode_plan_bytes",
-           "lsr_quick_decode_prepare", "lsr_quick_decode_run", "lsr_topk_code_forward",
+           "lsr_quick_decode_prepare", "lsr_quick_decode_run", "lsr_quick_pack_codes", "lsr_topk_code_forward",
            "lsr_topk_code_backward", "lsr_topk_code_backward_sparse", "lsr_knn_dist2", "lsr_lang_loss_forward", "lsr_lang_loss_backward", "lsr_adam_step", "lsr_sh_grad_from_views", "lsr_strerror",
            "lsr_abi_version", "lsr_max_lang_dim", "lsr_profile_enable", "lsr_profile_stages", "lsr_profile_reset",
            "lsr_profile_query", "lsr_set_option", "lsr_get_option")
@@ -164,6 +164,9 @@ def load(path: str | None = None):
     lib.lsr_quick_decode_run.argtypes = [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float, _vp, _vp]
     lib.lsr_quick_decode_run.restype = ctypes.c_int
+    if hasattr(lib, "lsr_quick_pack_codes"):   # (older A/B builds lack it)
+        lib.lsr_quick_pack_codes.argtypes = [_vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, _vp, _vp]
+        lib.lsr_quick_pack_codes.restype = ctypes.c_int
     lib.lsr_topk_code_forward.argtypes = [_vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp,
                                           _vp, ctypes.c_int, ctypes.c_int, _vp]
     lib.lsr_topk_code_forward.restype = ctypes.c_int

@@ -109,4 +109,29 @@ hipError_t launch_sparse_gather(const float* g, const void* qi, int dtype, int N
     return hipGetLastError();
 }
 
+// Packed code rows (LSR_INDEX_PACKED): the 12 codes of Gaussian i as bytes
+// code + 1 (0 = out of range), one 16-B row each; the quick render stages
+// them as they are instead of converting 12 indices per candidate and frame.
+__global__ void __launch_bounds__(256) k_quick_pack_codes(const void* __restrict__ qi, int dtype, int64_t N, int Dq,
+                                                          uint4* __restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    uint32_t w[3] = {0u, 0u, 0u};
+#pragma unroll
+    for (int m = 0; m < 12; m++) {
+        const int q = quick_index(qi, dtype, (size_t)i * 12 + m);
+        const uint32_t b = (q >= 0 && q < Dq) ? (uint32_t)(q + 1) : 0u;
+        w[m >> 2] |= b << (8 * (m & 3));
+    }
+    out[i] = make_uint4(w[0], w[1], w[2], 0u);
+}
+
+hipError_t launch_quick_pack_codes(const void* qi, int dtype, int64_t N, int Dq, void* packed, hipStream_t st)
+{
+    if (N == 0) return hipSuccess;
+    k_quick_pack_codes<<<(unsigned)((N + 255) / 256), 256, 0, st>>>(qi, dtype, N, Dq, (uint4*)packed);
+    return hipGetLastError();
+}
+
 }  // namespace lsr

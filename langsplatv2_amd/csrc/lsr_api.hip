@@ -203,7 +203,14 @@ int validate(const lsr_settings* s, const lsr_inputs* in)
     if (s->quick_render) {
         if (in->P > 0 && (!in->language_feature_weights_quick || !in->language_feature_indices || in->quick_k <= 0))
             return LSR_EINVAL;
-        if (in->quick_index_dtype < LSR_INDEX_F32 || in->quick_index_dtype > LSR_INDEX_I64) return LSR_EINVAL;
+        if (in->quick_index_dtype < LSR_INDEX_F32 || in->quick_index_dtype > LSR_INDEX_PACKED) return LSR_EINVAL;
+        if (in->quick_index_dtype == LSR_INDEX_PACKED) {
+            // packed rows: the 12-code LDS-DMA kernel's staging format
+            if (in->quick_k != 12 || quick_dim(s) > 192) return LSR_EUNSUPPORTED;
+            if (in->P > 0 && (((uintptr_t)in->language_feature_weights_quick % 16) != 0 ||
+                              ((uintptr_t)in->language_feature_indices % 16) != 0))
+                return LSR_EUNSUPPORTED;
+        }
         if ((size_t)quick_dim(s) * 256 + 64 * (32 + 12 + 8 * (size_t)in->quick_k) > 65536) return LSR_EUNSUPPORTED;
         if (s->quick_layout == LSR_LAYOUT_HWC) {
             // the pixel-major map is written by the 12-code, 192-channel LDS-DMA kernel only
@@ -304,6 +311,19 @@ int lsr_quick_decode(const float* weight_map, const float* codebooks, int L, int
         if (!ws) return LSR_ENOMEM;
     }
     if (lsr::launch_quick_decode(weight_map, codebooks, L, K, Df, H, W, normalize, eps, ws, out, st) != hipSuccess)
+        return LSR_EHIP;
+    return LSR_OK;
+}
+
+int lsr_quick_pack_codes(const void* indices, int index_dtype, int64_t N, int K, int quick_dim, uint32_t* packed,
+                         void* stream)
+{
+    if (N < 0 || quick_dim < 0 || index_dtype < LSR_INDEX_F32 || index_dtype > LSR_INDEX_I64) return LSR_EINVAL;
+    if (K != 12 || quick_dim > 255) return LSR_EUNSUPPORTED;
+    if (N == 0) return LSR_OK;
+    if (!indices || !packed || ((uintptr_t)packed % 16) != 0) return LSR_EINVAL;
+    if (lsr::launch_quick_pack_codes(indices, index_dtype, N, quick_dim > 0 ? quick_dim : 192, packed,
+                                     (hipStream_t)stream) != hipSuccess)
         return LSR_EHIP;
     return LSR_OK;
 }

@@ -95,12 +95,26 @@ __device__ __forceinline__ int f2i(float v)
     return v != v ? 0 : r;
 }
 
+// An fp32-encoded code index (u5): round half up, floor(v + 0.5); NaN and
+// values outside [0, 2^31) -> -1 (dropped as every out-of-range code is).
+__device__ __forceinline__ int quick_code_f32(float v)
+{
+    const float r = floorf(v + 0.5f);
+    return (r >= 0.0f && r < 2147483648.0f) ? (int)r : -1;
+}
+
 // Quick-path code index m of a Gaussian's sparse language row: fp32-encoded
-// integers round half up (u5), int32 as is, int64 outside [0, 2^31) -> -1.
+// integers as quick_code_f32, int32 as is, int64 outside [0, 2^31) -> -1;
+// packed rows (LSR_INDEX_PACKED, K = 12): byte m of the row's 16 B, code + 1.
 __device__ __forceinline__ int quick_index(const void* qi, int dtype, size_t off)
 {
-    if (dtype == 0) return f2i(((const float*)qi)[off] + 0.5f);
+    if (dtype == 0) return quick_code_f32(((const float*)qi)[off]);
     if (dtype == 1) return ((const int32_t*)qi)[off];
+    if (dtype == 3) {
+        const size_t i = off / 12, m = off - i * 12;
+        const uint32_t w = ((const uint32_t*)qi)[4 * i + (m >> 2)];
+        return (int)((w >> (8 * (m & 3))) & 0xffu) - 1;
+    }
     const int64_t v = ((const int64_t*)qi)[off];
     return (v < 0 || v > 0x7fffffff) ? -1 : (int)v;
 }

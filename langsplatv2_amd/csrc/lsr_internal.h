@@ -154,6 +154,7 @@ hipError_t launch_sparse_expand(const float* qw, const void* qi, int dtype, int 
                                 hipStream_t st);
 hipError_t launch_sparse_gather(const float* g, const void* qi, int dtype, int N, int K, int Dq, float* dw,
                                 hipStream_t st);
+hipError_t launch_quick_pack_codes(const void* qi, int dtype, int64_t N, int Dq, void* packed, hipStream_t st);
 
 // adam.hip
 struct AdamArgs {

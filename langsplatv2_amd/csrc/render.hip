@@ -674,13 +674,7 @@ __global__ void __launch_bounds__(64) k_render_fwd_quick(RenderArgs a)
             sRGB[3 * t + 2] = a.rgb[3 * gid + 2];
             for (int k = 0; k < K; k++) {
                 sW[t * K + k] = a.qw[(size_t)gid * K + k];
-                int q;
-                if (a.qidx_dtype == LSR_INDEX_F32)
-                    q = f2i(((const float*)a.qi)[(size_t)gid * K + k] + 0.5f);
-                else if (a.qidx_dtype == LSR_INDEX_I32)
-                    q = ((const int32_t*)a.qi)[(size_t)gid * K + k];
-                else
-                    q = (int)((const int64_t*)a.qi)[(size_t)gid * K + k];
+                const int q = quick_index(a.qi, a.qidx_dtype, (size_t)gid * K + k);
                 sI[t * K + k] = (q >= 0 && q < Dq) ? q : -1;
             }
         }
@@ -761,29 +755,35 @@ struct WaveStageV {
 // lands in the junk register v63.  M0 (the index) is saved and restored.
 // (s_set_gpr_idx_idx reads only bits [7:0], so byte k of a code word is
 // selected by a shift.)
-#define LSR_QV_STEP0(word, wv)                                                          \
+// The index needs one wait state before the VALU that uses it: the shift
+// forming the NEXT code's index (into the other of two SGPRs) fills it, so only
+// the word's last code takes an s_nop (3 per candidate instead of 12).
+#define LSR_QV_WORD(word, w0, w1, w2, w3)                                               \
     "s_set_gpr_idx_idx %[" #word "]\n\t"                                                \
+    "s_lshr_b32 %[ia], %[" #word "], 8\n\t"                                             \
+    "v_fma_f32 v63, %[" #w0 "], %[aT], v63\n\t"                                         \
+    "s_set_gpr_idx_idx %[ia]\n\t"                                                       \
+    "s_lshr_b32 %[ib], %[" #word "], 16\n\t"                                            \
+    "v_fma_f32 v63, %[" #w1 "], %[aT], v63\n\t"                                         \
+    "s_set_gpr_idx_idx %[ib]\n\t"                                                       \
+    "s_lshr_b32 %[ia], %[" #word "], 24\n\t"                                            \
+    "v_fma_f32 v63, %[" #w2 "], %[aT], v63\n\t"                                         \
+    "s_set_gpr_idx_idx %[ia]\n\t"                                                       \
     "s_nop 0\n\t"                                                                       \
-    "v_fma_f32 v63, %[" #wv "], %[aT], v63\n\t"
-#define LSR_QV_STEP(word, sh, wv)                                                       \
-    "s_lshr_b32 %[ix], %[" #word "], " #sh "\n\t"                                         \
-    "s_set_gpr_idx_idx %[ix]\n\t"                                                       \
-    "s_nop 0\n\t"                                                                       \
-    "v_fma_f32 v63, %[" #wv "], %[aT], v63\n\t"
+    "v_fma_f32 v63, %[" #w3 "], %[aT], v63\n\t"
 // one candidate's K <= 12 pairs (codes in three words q0..q2, weights w0..w11)
 #define LSR_QV_UPDATE(aT_, Q_, W0_, W1_, W2_)                                                                   \
     do {                                                                                                        \
         const uint32_t qw0 = __builtin_amdgcn_readfirstlane((Q_).x), qw1 = __builtin_amdgcn_readfirstlane((Q_).y), \
                        qw2 = __builtin_amdgcn_readfirstlane((Q_).z);                                            \
-        uint32_t ix, sv;                                                                                        \
+        uint32_t ia, ib, sv;                                                                                    \
         asm volatile("s_mov_b32 %[sv], m0\n\t"                                                                  \
                      "s_set_gpr_idx_on 0, gpr_idx(SRC2,DST)\n\t"                                                \
-                     LSR_QV_STEP0(q0, w0) LSR_QV_STEP(q0, 8, w1) LSR_QV_STEP(q0, 16, w2) LSR_QV_STEP(q0, 24, w3)  \
-                     LSR_QV_STEP0(q1, w4) LSR_QV_STEP(q1, 8, w5) LSR_QV_STEP(q1, 16, w6) LSR_QV_STEP(q1, 24, w7)  \
-                     LSR_QV_STEP0(q2, w8) LSR_QV_STEP(q2, 8, w9) LSR_QV_STEP(q2, 16, w10) LSR_QV_STEP(q2, 24, w11) \
+                     LSR_QV_WORD(q0, w0, w1, w2, w3) LSR_QV_WORD(q1, w4, w5, w6, w7)                            \
+                     LSR_QV_WORD(q2, w8, w9, w10, w11)                                                          \
                      "s_set_gpr_idx_off\n\t"                                                                    \
                      "s_mov_b32 m0, %[sv]"                                                                      \
-                     : [ix] "=&s"(ix), [sv] "=&s"(sv)                                                           \
+                     : [ia] "=&s"(ia), [ib] "=&s"(ib), [sv] "=&s"(sv)                                           \
                      : [q0] "s"(qw0), [q1] "s"(qw1), [q2] "s"(qw2), [aT] "v"(aT_), [w0] "v"((W0_).x),           \
                        [w1] "v"((W0_).y), [w2] "v"((W0_).z), [w3] "v"((W0_).w), [w4] "v"((W1_).x),              \
                        [w5] "v"((W1_).y), [w6] "v"((W1_).z), [w7] "v"((W1_).w), [w8] "v"((W2_).x),              \
@@ -961,18 +961,21 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
 // into a per-wave LDS buffer by global_load_lds (no VGPR destination, ids
 // loaded two chunks ahead) while the current chunk blends; staging then reads
 // LDS.  Blend, accumulation and outputs are k_render_fwd_quick_v's, bit for bit.
-template <int QB>
+// NQ = 16-B parts of an index row: 3 (fp32 / int32), 6 (int64), 1 (packed)
+template <int NQ>
 struct WaveRawQ {
     float4 A[64];
     float4 B[64];
     float rgb[3][64];                   // channel c of lane l (three 4-B DMAs)
     float4 W[3][64];                    // weight row part p (4 weights) of lane l
-    uint4 Q[3 * QB / 4][64];            // index row bytes [16 p, 16 p + 16) of lane l
+    uint4 Q[NQ][64];                    // index row bytes [16 p, 16 p + 16) of lane l
     uint32_t nid[64];                   // the point-list ids of the chunk after next
 };
+template <int DT>
+constexpr int quick_nq() { return DT == 2 ? 6 : DT == 3 ? 1 : 3; }
 
 template <int DT>
-__device__ __forceinline__ int quick_code_raw(const WaveRawQ<DT == 2 ? 8 : 4>& raw, int lane, int k)
+__device__ __forceinline__ int quick_code_raw(const WaveRawQ<quick_nq<DT>()>& raw, int lane, int k)
 {
     if constexpr (DT == 2) {
         const uint4 q = raw.Q[k >> 1][lane];
@@ -981,7 +984,7 @@ __device__ __forceinline__ int quick_code_raw(const WaveRawQ<DT == 2 ? 8 : 4>& r
     } else {
         const uint4 q = raw.Q[k >> 2][lane];
         const uint32_t v = (k & 3) == 0 ? q.x : (k & 3) == 1 ? q.y : (k & 3) == 2 ? q.z : q.w;
-        return DT == 0 ? f2i(__uint_as_float(v) + 0.5f) : (int)v;
+        return DT == 0 ? quick_code_f32(__uint_as_float(v)) : (int)v;
     }
 }
 
@@ -1003,20 +1006,37 @@ __device__ __forceinline__ int quick_code_raw(const WaveRawQ<DT == 2 ? 8 : 4>& r
 // this kernel, and per-call M0 constants spilled SGPRs.)  The caller waits with
 // s_waitcnt vmcnt before reading raw.
 #define LSR_GLDS(step, insn) "s_add_u32 m0, m0, " #step "\n\ts_nop 0\n\t" insn "\n\t"
-template <int QB>
-__device__ __forceinline__ void quick_dma12(WaveRawQ<QB>& raw, const RenderArgs& a, uint32_t g, const uint32_t* pI)
+template <int NQ>
+__device__ __forceinline__ void quick_dma12(WaveRawQ<NQ>& raw, const RenderArgs& a, uint32_t g, const uint32_t* pI)
 {
-    static_assert(offsetof(WaveRawQ<QB>, B) == 1024 && offsetof(WaveRawQ<QB>, rgb) == 2048 &&
-                  offsetof(WaveRawQ<QB>, W) == 2816 && offsetof(WaveRawQ<QB>, Q) == 5888 &&
-                  offsetof(WaveRawQ<QB>, nid) == 5888 + 768 * QB, "raw layout");
+    static_assert(offsetof(WaveRawQ<NQ>, B) == 1024 && offsetof(WaveRawQ<NQ>, rgb) == 2048 &&
+                  offsetof(WaveRawQ<NQ>, W) == 2816 && offsetof(WaveRawQ<NQ>, Q) == 5888 &&
+                  offsetof(WaveRawQ<NQ>, nid) == 5888 + 1024 * NQ, "raw layout");
     const uint32_t base = (uint32_t)(uintptr_t)&raw;   // the LDS byte address (low half of the flat address)
     const float4* pA = a.splatA + g;
     const float4* pB = a.splatB + g;
     const float* pR = a.rgb + 3 * (size_t)g;
     const float* pW = a.qw + 12 * (size_t)g;
-    const char* pQ = reinterpret_cast<const char*>(a.qi) + (size_t)g * (12 * QB);
+    const char* pQ = reinterpret_cast<const char*>(a.qi) + (size_t)g * (16 * NQ);
     uint32_t keep;
-    if constexpr (QB == 4) {
+    if constexpr (NQ == 1) {
+        asm volatile("s_mov_b32 %[keep], m0\n\t"
+                     "s_mov_b32 m0, %[base]\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[pA], off\n\t"
+                     LSR_GLDS(1024, "global_load_lds_dwordx4 %[pB], off")
+                     LSR_GLDS(1024, "global_load_lds_dword %[pR], off")
+                     LSR_GLDS(252, "global_load_lds_dword %[pR], off offset:4")
+                     LSR_GLDS(252, "global_load_lds_dword %[pR], off offset:8")
+                     LSR_GLDS(264, "global_load_lds_dwordx4 %[pW], off")
+                     LSR_GLDS(1008, "global_load_lds_dwordx4 %[pW], off offset:16")
+                     LSR_GLDS(1008, "global_load_lds_dwordx4 %[pW], off offset:32")
+                     LSR_GLDS(1056, "global_load_lds_dwordx4 %[pQ], off")
+                     LSR_GLDS(1024, "global_load_lds_dword %[pI], off")
+                     "s_mov_b32 m0, %[keep]"
+                     : [keep] "=&s"(keep)
+                     : [base] "s"(base), [pA] "v"(pA), [pB] "v"(pB), [pR] "v"(pR), [pW] "v"(pW), [pQ] "v"(pQ),
+                       [pI] "v"(pI)
+                     : "memory", "scc");
+    } else if constexpr (NQ == 3) {
         asm volatile("s_mov_b32 %[keep], m0\n\t"
                      "s_mov_b32 m0, %[base]\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[pA], off\n\t"
                      LSR_GLDS(1024, "global_load_lds_dwordx4 %[pB], off")
@@ -1096,9 +1116,9 @@ __device__ __forceinline__ void quick_dma12(WaveRawQ<QB>& raw, const RenderArgs&
 template <int DT, bool BAND>
 __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_render_fwd_quick_d(RenderArgs a)
 {
-    constexpr int QB = DT == 2 ? 8 : 4;
+    constexpr int NQ = quick_nq<DT>();
     __shared__ WaveStageV st;
-    __shared__ WaveRawQ<QB> raw;
+    __shared__ WaveRawQ<NQ> raw;
     const Cam& c = a.cam;
     const WaveTile wt(a);
     const int lane = threadIdx.x;
@@ -1139,7 +1159,7 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
     bool done = !inside;
     // the first chunk's rows, and (in raw.nid) the ids of the chunk after it; positions
     // past the list read the list's last id, and gid 0 (a valid row, never staged) is used
-    if (rs < re) quick_dma12<QB>(raw, a, (rs + lane < re) ? a.point_list[rs + lane] : 0u,
+    if (rs < re) quick_dma12<NQ>(raw, a, (rs + lane < re) ? a.point_list[rs + lane] : 0u,
                                  a.point_list + min(rs + 64 + lane, re - 1));
     for (uint32_t base = rs; base < re; base += 64) {
         if (wave_ballot(!done) == 0) break;
@@ -1159,17 +1179,30 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
             st.Wt[r][1] = raw.W[1][lane];
             st.Wt[r][2] = raw.W[2][lane];
             uint32_t qv[3] = {0u, 0u, 0u};   // register index q + 1 per code; 0 = the junk register
+            if constexpr (DT == 3) {
+                // packed rows are register indices already; a byte above Dq (not
+                // written by lsr_quick_pack_codes for this Dq) is dropped, so no
+                // index can leave v64 .. v(63 + Dq)
+                const uint4 p = raw.Q[0][lane];
+                const uint32_t pw[3] = {p.x, p.y, p.z};
 #pragma unroll
-            for (int k = 0; k < 12; k++) {   // K = 12 (quick_dma_ok)
-                const int q = quick_code_raw<DT>(raw, lane, k);
-                const uint32_t qb = (q >= 0 && q < Dq) ? (uint32_t)(q + 1) : 0u;
-                qv[k >> 2] |= qb << (8 * (k & 3));
+                for (int k = 0; k < 12; k++) {
+                    const uint32_t b = (pw[k >> 2] >> (8 * (k & 3))) & 0xffu;
+                    qv[k >> 2] |= (b <= (uint32_t)Dq ? b : 0u) << (8 * (k & 3));
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 12; k++) {   // K = 12 (quick_dma_ok)
+                    const int q = quick_code_raw<DT>(raw, lane, k);
+                    const uint32_t qb = (q >= 0 && q < Dq) ? (uint32_t)(q + 1) : 0u;
+                    qv[k >> 2] |= qb << (8 * (k & 3));
+                }
             }
             st.Q[r] = make_uint4(qv[0], qv[1], qv[2], 0u);
         }
         const uint32_t gid_n = idx + 64 < re ? raw.nid[lane] : 0u;
         wave_lds_fence();   // raw read, stage written: raw may be refilled
-        if (base + 64 < re) quick_dma12<QB>(raw, a, gid_n, a.point_list + min(idx + 128, re - 1));
+        if (base + 64 < re) quick_dma12<NQ>(raw, a, gid_n, a.point_list + min(idx + 128, re - 1));
         const int n = __popcll(m);
         // the blend of k_render_fwd_quick_v, unchanged
         for (int j0 = 0; j0 < n; j0 += 2) {
@@ -1274,9 +1307,8 @@ __global__ void __launch_bounds__(64, 2) __attribute__((amdgpu_num_vgpr(63))) k_
 // the LDS-DMA quick kernel applies: 12 codes per Gaussian (3 levels x top-4), 16-B aligned rows
 static bool quick_dma_ok(const RenderArgs& a)
 {
-    const int qb = a.qidx_dtype == LSR_INDEX_I64 ? 8 : 4;
     return a.K == 12 && a.Dq <= 192 && ((uintptr_t)a.qw % 16) == 0 && ((uintptr_t)a.qi % 16) == 0 &&
-           ((uintptr_t)a.rgb % 4) == 0 && qb > 0;
+           ((uintptr_t)a.rgb % 4) == 0;
 }
 
 #pragma clang diagnostic pop
@@ -1298,17 +1330,20 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st)
     if (T == 0) return hipSuccess;
     if (a.qw) {
         if (a.quick_hwc && !(quick_dma_ok(a) && a.Dq == 192)) return hipErrorInvalidValue;
+        if (a.qidx_dtype == LSR_INDEX_PACKED && !quick_dma_ok(a)) return hipErrorInvalidValue;
         if (quick_dma_ok(a)) {
             if (a.quick_hwc) {
                 switch (a.qidx_dtype) {
                     case LSR_INDEX_F32: k_render_fwd_quick_d<0, false><<<T * 4, 64, 0, st>>>(a); break;
                     case LSR_INDEX_I32: k_render_fwd_quick_d<1, false><<<T * 4, 64, 0, st>>>(a); break;
+                    case LSR_INDEX_PACKED: k_render_fwd_quick_d<3, false><<<T * 4, 64, 0, st>>>(a); break;
                     default: k_render_fwd_quick_d<2, false><<<T * 4, 64, 0, st>>>(a); break;
                 }
             } else {
                 switch (a.qidx_dtype) {
                     case LSR_INDEX_F32: k_render_fwd_quick_d<0, true><<<T * 4, 64, 0, st>>>(a); break;
                     case LSR_INDEX_I32: k_render_fwd_quick_d<1, true><<<T * 4, 64, 0, st>>>(a); break;
+                    case LSR_INDEX_PACKED: k_render_fwd_quick_d<3, true><<<T * 4, 64, 0, st>>>(a); break;
                     default: k_render_fwd_quick_d<2, true><<<T * 4, 64, 0, st>>>(a); break;
                 }
             }

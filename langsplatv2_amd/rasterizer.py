@@ -222,6 +222,47 @@ def _index_dtype(t: torch.Tensor) -> int:
     raise RuntimeError(f"language_feature_indices dtype {t.dtype} unsupported (float32/int32/int64)")
 
 
+# The quick render stages each candidate's 12 code indices; converting the
+# reference's fp32 indices (u5: round half up, range check) is per candidate and
+# frame work, so the forward hands the library packed rows (LSR_INDEX_PACKED,
+# lsr_quick_pack_codes) converted once per indices tensor and kept while that
+# tensor is unchanged (same object, same version counter; the entry holds the
+# tensor, so its storage cannot be reused under the key).  False: the forward
+# passes the indices as they are (A/B, tests).
+QUICK_PACKED_CODES = True
+_PACKED = {}
+_PACKED_MAX = 2
+
+
+def _packed_codes(qi: torch.Tensor, Dq: int) -> torch.Tensor:
+    try:
+        ver = qi._version
+    except RuntimeError:   # an inference tensor tracks no version: convert every call
+        ver = None
+    key = (qi.data_ptr(), qi.device, tuple(qi.shape), qi.dtype, int(Dq))
+    hit = _PACKED.get(key)
+    if ver is not None and hit is not None and hit[0] is qi and hit[1] == ver:
+        return hit[2]
+    packed = torch.empty((qi.shape[0], 4), dtype=torch.int32, device=qi.device)
+    _lib.check(_lib.load().lsr_quick_pack_codes(qi.data_ptr(), _index_dtype(qi), int(qi.shape[0]), int(qi.shape[1]),
+                                                int(Dq), packed.data_ptr(), _stream(qi.device)),
+               "lsr_quick_pack_codes")
+    if ver is not None:
+        _PACKED.pop(key, None)
+        while len(_PACKED) >= _PACKED_MAX:
+            _PACKED.pop(next(iter(_PACKED)))
+        _PACKED[key] = (qi, ver, packed)
+    return packed
+
+
+def _use_packed(qw: torch.Tensor, qi: torch.Tensor, Dq: int) -> bool:
+    """The packed rows apply: 12 codes per Gaussian, Dq <= 192, 16-B aligned rows
+    (the LDS-DMA quick kernel, csrc/render.hip k_render_fwd_quick_d)."""
+    return (QUICK_PACKED_CODES and qi.dim() == 2 and qi.shape[0] > 0 and qi.shape[1] == 12 and qw.shape[1] == 12
+            and Dq <= 192 and qi.dtype in (torch.float32, torch.int32, torch.int64)
+            and qw.data_ptr() % 16 == 0 and qi.data_ptr() % 16 == 0)
+
+
 def _stream(dev) -> int:
     return torch.cuda.current_stream(dev).cuda_stream
 
@@ -269,9 +310,12 @@ def _run_forward(means3D, sh, colors_precomp, language_feature_precomp, language
     H, W = int(rs.image_height), int(rs.image_width)
 
     s, keep = _settings_struct(rs, dev)
-    ins = _lib.Inputs(N, M, D, K, _index_dtype(qi_c) if qi_c is not None else 0,
+    qi_fwd, qi_dt = qi_c, (_index_dtype(qi_c) if qi_c is not None else 0)
+    if quick and _use_packed(qw_c, qi_c, Dq):
+        qi_fwd, qi_dt = _packed_codes(qi_c, Dq), _lib.LSR_INDEX_PACKED
+    ins = _lib.Inputs(N, M, D, K, qi_dt,
                       means3D_c.data_ptr(), _ptr(sh_c), _ptr(col_c), opac_c.data_ptr(), _ptr(sc_c), _ptr(rot_c),
-                      _ptr(cov_c), _ptr(lang_c), _ptr(qw_c), _ptr(qi_c))
+                      _ptr(cov_c), _ptr(lang_c), _ptr(qw_c), _ptr(qi_fwd))
     color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
     if quick and _quick_layout(rs) == _lib.LSR_LAYOUT_HWC:
         lang_out = torch.empty((H, W, Dout), dtype=torch.float32, device=dev).permute(2, 0, 1)

@@ -525,7 +525,12 @@ void lso_binning_ex(const lso_settings* s, int N, const lso_geom* g, uint32_t* p
 }
 
 /* ---------------------------------------------------------- render fwd -- */
-static inline int quick_index(float v) { return (int)(v + 0.5f); }
+/* u5: round half up, floor(v + 0.5); NaN and values outside [0, 2^31) -> -1 */
+static inline int quick_index(float v)
+{
+    const float r = floorf(v + 0.5f);
+    return (r >= 0.f && r < 2147483648.f) ? (int)r : -1;
+}
 
 static void render_tile_fwd(const lso_settings* s, const lso_inputs* in, const lso_geom* g,
                             const uint32_t* point_list, const uint32_t* ranges, int tile,

@@ -246,7 +246,9 @@ def quick_codes(qi: np.ndarray) -> np.ndarray:
     """Integer codes of quick indices: fp32-encoded integers round half up (u5)."""
     qi = np.asarray(qi)
     if qi.dtype.kind == "f":
-        return np.floor(qi.astype(np.float32) + np.float32(0.5)).astype(np.int64)
+        r = np.floor(qi.astype(np.float32) + np.float32(0.5))
+        ok = (r >= 0) & (r < 2.0 ** 31)   # NaN and out-of-range values -> -1 (dropped)
+        return np.where(ok, np.where(ok, r, 0).astype(np.int64), -1)
     return qi.astype(np.int64)
 
 

@@ -1,7 +1,9 @@
 """A/B of the quick decode (lsr_quick_decode_run) and the quick render between
 liblsr variants in ONE process, interleaved rounds, at bench.py's quick_1mpix
 workload (1M Gaussians, 1280x800, 3 levels x top-4 -> 192 channels, 3 x 64 x 512
-codebooks).  Usage: python tools/ab_quick.py name=path.so ..."""
+codebooks).  Usage: python tools/ab_quick.py name=path.so ...; a name ending in
+":nopack" runs that library with rasterizer.QUICK_PACKED_CODES off (the
+indices passed as they are instead of the cached packed rows)."""
 import os
 import statistics
 import sys
@@ -10,7 +12,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from diff_gaussian_rasterization import GaussianRasterizer  # noqa: E402
-from langsplatv2_amd import _lib, quick  # noqa: E402
+from langsplatv2_amd import _lib, quick, rasterizer  # noqa: E402
 from langsplatv2_amd.scenes import make_camera, make_gaussians  # noqa: E402
 import bench  # noqa: E402
 
@@ -49,6 +51,8 @@ res = {name: {"render": [], "decode": [], "both": []} for name, _ in variants}
 for rnd in range(6):
     for name, _ in variants:
         _lib._lib = libs[name]
+        rasterizer.QUICK_PACKED_CODES = not name.endswith(":nopack")
+        rasterizer._PACKED.clear()
         quick._PLANS.clear()
         wm = render()
         quick.decode_language_features(wm, cb)   # plan + warm
