@@ -290,7 +290,9 @@ def quick_fps(N, dev, W=1280, H=800, iters=20):
     decode + L2 normalise, at 1.0 Mpix.  The headline fields time the map in the pixel-major
     layout (language_feature_layout="hwc": the same values, a (192,H,W) view the reference's
     .view(3, 64, H, W).view(3, 64, H*W) + einsum accept unchanged; tests/test_quick_layout.py);
-    `reference_layout` times the reference's contiguous (192,H,W) map."""
+    `reference_layout` times the reference's contiguous (192,H,W) map.  render_decode_fps is
+    one view at a time (render, then decode); render_decode_stream_fps is the throughput over a
+    stream of views with each decode overlapping the next render (quick.QuickFeatureStream)."""
     from langsplatv2_amd import quick
     cam = make_camera(W, H)
     g = make_gaussians(N, cam, seed=0, sh_degree=3, quick_k=4)
@@ -312,8 +314,15 @@ def quick_fps(N, dev, W=1280, H=800, iters=20):
             quick.decode_language_features(render(), cb)
         s_render = timeit(render, iters)
         s_total = timeit(both, iters)
+        fs = quick.QuickFeatureStream(cb)
+
+        def streamed():
+            fs.push(render)
+        s_stream = timeit(streamed, iters)
+        fs.flush()
         return dict(render_fps=round(1.0 / s_render, 1), render_decode_fps=round(1.0 / s_total, 1),
-                    render_ms=round(s_render * 1e3, 4), decode_ms=round((s_total - s_render) * 1e3, 4))
+                    render_ms=round(s_render * 1e3, 4), decode_ms=round((s_total - s_render) * 1e3, 4),
+                    render_decode_stream_fps=round(1.0 / s_stream, 1))
     out = dict(workload=f"{N} Gaussians {W}x{H}, quick 3x top-4 -> 192 ch + 3x64x512 decode + L2 norm",
                layout="hwc (pixel-major quick map, language_feature_layout='hwc')")
     out.update(measure("hwc"))

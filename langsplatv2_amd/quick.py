@@ -27,11 +27,12 @@ from .rasterizer import _stream
 
 
 def decode_language_features(weight_map: torch.Tensor, codebooks: torch.Tensor, normalize: bool = True,
-                             eps: float = 1e-10) -> torch.Tensor:
+                             eps: float = 1e-10, out: torch.Tensor | None = None) -> torch.Tensor:
     """weight_map (L*K, H, W) fp32 CUDA, codebooks (L, K, Df) fp32 CUDA ->
     features (L, Df, H, W); L2-normalised over Df per pixel when `normalize`.
     A pixel-major weight map (strides (1, L*K*W, L*K): the rasterizer's
-    language_feature_layout="hwc" output) is read as it is (LSR_LAYOUT_HWC)."""
+    language_feature_layout="hwc" output) is read as it is (LSR_LAYOUT_HWC).
+    `out`: an optional contiguous fp32 (L, Df, H, W) tensor to write into."""
     if weight_map.dim() != 3 or codebooks.dim() != 3:
         raise ValueError("decode_language_features: weight_map must be (L*K, H, W) and codebooks (L, K, Df)")
     L, K, Df = codebooks.shape
@@ -46,7 +47,11 @@ def decode_language_features(weight_map: torch.Tensor, codebooks: torch.Tensor, 
            and weight_map.data_ptr() % 16 == 0 and H * W > 1)
     wm = weight_map if hwc else weight_map.contiguous().float()
     cb = codebooks.contiguous().float()
-    out = torch.empty((L, Df, H, W), dtype=torch.float32, device=weight_map.device)
+    if out is None:
+        out = torch.empty((L, Df, H, W), dtype=torch.float32, device=weight_map.device)
+    elif (tuple(out.shape) != (L, Df, H, W) or out.dtype != torch.float32 or not out.is_contiguous()
+          or out.device != weight_map.device):
+        raise ValueError(f"decode_language_features: out must be a contiguous float32 ({L}, {Df}, {H}, {W}) tensor")
     lib = _lib.load()
     plan = decode_plan(cb, normalize)
     rc = lib.lsr_quick_decode_run(wm.data_ptr(), _lib.LSR_LAYOUT_HWC if hwc else _lib.LSR_LAYOUT_CHW,
@@ -84,6 +89,70 @@ def decode_plan(codebooks: torch.Tensor, normalize: bool = True) -> torch.Tensor
     while len(_PLANS) > _PLAN_CACHE_SIZE:
         _PLANS.popitem(last=False)
     return plan
+
+
+class QuickFeatureStream:
+    """Render + decode over a stream of views, frame i's decode overlapping
+    frame i+1's render.  The reference evaluates view after view, each as
+    render -> einsum -> normalise (eval_lerf.py:210-220, :320-350;
+    backend_renderer.py:16-36).  The quick render is latency-bound (2 waves per
+    SIMD, its HBM traffic ~1 GB per 1-Mpix frame) and the decode HBM-bound
+    (7.08 GB per frame), so running them back to back leaves each one's
+    resources idle while the other runs.  Here the decode goes to a second HIP
+    stream and the caller's stream goes on to the next render; the features
+    of frame i come back from the push of frame i + 1 (or from `flush`), made
+    safe to use on the caller's stream.
+
+        fs = QuickFeatureStream(codebooks)
+        for view in views:
+            prev = fs.push(lambda: render(view, ...)["language_feature_weight_map"])
+            if prev is not None:
+                use(prev)                   # (L, Df, H, W), the previous view's
+        use(fs.flush())
+
+    Each frame's values equal decode_language_features(weight map) exactly (the
+    same kernels; only the issue order differs)."""
+
+    def __init__(self, codebooks: torch.Tensor, normalize: bool = True, eps: float = 1e-10):
+        self.codebooks, self.normalize, self.eps = codebooks, bool(normalize), float(eps)
+        self._decode_stream = torch.cuda.Stream(codebooks.device)
+        self._pending = None
+
+    def push(self, render_fn) -> torch.Tensor | None:
+        """Render one view on the caller's current stream (render_fn returns its
+        (L*K, H, W) weight map) and queue its decode; returns the previous
+        view's features, or None for the first view."""
+        with torch.no_grad():
+            wm = render_fn()
+        cur = torch.cuda.current_stream(wm.device)
+        rendered = torch.cuda.Event()
+        rendered.record(cur)
+        prev = self._take(cur)   # the caller's stream waits for the previous decode only now
+        # the output is allocated on the caller's stream (where it is used and freed) and
+        # kept from reuse until the decode stream has written it
+        L, _, Df = self.codebooks.shape
+        out = torch.empty((L, Df) + tuple(wm.shape[1:]), dtype=torch.float32, device=wm.device)
+        with torch.cuda.stream(self._decode_stream):
+            self._decode_stream.wait_event(rendered)
+            decode_language_features(wm, self.codebooks, self.normalize, self.eps, out=out)
+            decoded = torch.cuda.Event()
+            decoded.record(self._decode_stream)
+        wm.record_stream(self._decode_stream)    # the map stays allocated until its decode ran
+        out.record_stream(self._decode_stream)
+        self._pending = (out, decoded)
+        return prev
+
+    def flush(self) -> torch.Tensor | None:
+        """The last pushed view's features (None if there is none pending)."""
+        return self._take(torch.cuda.current_stream(self.codebooks.device))
+
+    def _take(self, cur):
+        if self._pending is None:
+            return None
+        out, decoded = self._pending
+        self._pending = None
+        cur.wait_event(decoded)
+        return out
 
 
 def compute_final_feature_map(weight_map: torch.Tensor, codebooks: torch.Tensor) -> torch.Tensor:

@@ -64,13 +64,37 @@ def pipelined(F):
     return (time.perf_counter() - t0) / F
 
 
+fs = quick.QuickFeatureStream(cb)
+
+
+def qfs(F):
+    """quick.QuickFeatureStream from the caller's (default) stream."""
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(F):
+        fs.push(render)
+    fs.flush()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / F
+
+
+s_c = torch.cuda.Stream()
+
+
+def qfs_side(F):
+    """The same with the caller on a side stream."""
+    with torch.cuda.stream(s_c):
+        return qfs(F)
+
+
+modes = {"seq": sequential, "pipe": pipelined, "qfs": qfs, "qfs_side": qfs_side}
 for _ in range(3):
-    sequential(3)
-    pipelined(3)
-res = {"seq": [], "pipe": []}
+    for f in modes.values():
+        f(3)
+res = {k: [] for k in modes}
 for rnd in range(5):
-    res["seq"].append(sequential(20))
-    res["pipe"].append(pipelined(20))
+    for k, f in modes.items():
+        res[k].append(f(20))
 import statistics  # noqa: E402
 ncu = os.environ.get("LSR_DEC_NCU", "all")
 print(f"dec_cus={ncu} " + " ".join(f"{k}_ms={1e3 * statistics.median(v):.4f} fps={1 / statistics.median(v):.1f}"
