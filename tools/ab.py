@@ -77,13 +77,37 @@ def run(name, steps):
     return {k: ms / n for k, (ms, n) in q.items() if n}
 
 
+def step_ms(name, steps):
+    """Whole steps back to back, no stage events (what bench.py times)."""
+    _lib._lib = libs[name]
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        for p in g.values():
+            p.grad = None
+        with torch.set_grad_enabled(not FWD_ONLY):
+            c, l, _ = r(means3D=g["means3D"], means2D=g["means2D"], opacities=g["opacities"], shs=g["shs"],
+                        language_feature_precomp=g["language_feature_precomp"], scales=g["scales"],
+                        rotations=g["rotations"])
+        if not FWD_ONLY:
+            torch.autograd.backward([c, l], [dc, dl])
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / steps
+
+
 res = {name: [] for name, _ in variants}
+whole = {name: [] for name, _ in variants}
 for name, _ in variants:
     run(name, 3)
+    step_ms(name, 3)
 for rnd in range(5):
     for name, _ in variants:
         res[name].append(run(name, 5))
+        whole[name].append(step_ms(name, 10))
 for name, _ in variants:
     stages = res[name][0].keys()
     med = {k: statistics.median(x[k] for x in res[name]) for k in stages}
-    print(name, " ".join(f"{k}={v:.4f}" for k, v in med.items()), f"SUM={sum(med.values()):.4f}")
+    print(name, " ".join(f"{k}={v:.4f}" for k, v in med.items()), f"SUM={sum(med.values()):.4f}",
+          f"STEP={statistics.median(whole[name]):.4f}")
