@@ -340,6 +340,12 @@ int lsr_abi_version(void);
  * for an unknown option/value. */
 #define LSR_OPT_BIN_MODE 1
 #define LSR_OPT_LISTS_MAX_MB 2
+/* LSR_OPT_SPLIT_PREPROCESS (default 1): a forward with SH colours of at least
+ * 2^21 Gaussians evaluates the SH colour on a library-owned second stream
+ * of the current device, concurrent with the tile binning (the geometry the
+ * binning needs stays on the caller's stream, and the render waits for both);
+ * 0: one fused preprocess kernel on the caller's stream.  Results identical. */
+#define LSR_OPT_SPLIT_PREPROCESS 3
 #define LSR_BIN_AUTO 0
 #define LSR_BIN_SORTED_TILES 1
 #define LSR_BIN_ORDERED 2

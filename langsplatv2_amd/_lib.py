@@ -249,6 +249,20 @@ def set_lists_max_mb(mb: int) -> int:
     return int(prev.value)
 
 
+LSR_OPT_SPLIT_PREPROCESS = 3
+
+
+def set_split_preprocess(on: bool) -> bool:
+    """SH colour pass of the forward's preprocess on a second stream,
+    concurrent with the binning (lsr_set_option LSR_OPT_SPLIT_PREPROCESS,
+    default on; results identical).  Returns the previous setting."""
+    lib = load()
+    prev = ctypes.c_int64(0)
+    check(lib.lsr_get_option(LSR_OPT_SPLIT_PREPROCESS, ctypes.byref(prev)), "lsr_get_option")
+    check(lib.lsr_set_option(LSR_OPT_SPLIT_PREPROCESS, 1 if on else 0), "lsr_set_option")
+    return bool(prev.value)
+
+
 def profile_enable(on: bool = True):
     load().lsr_profile_enable(1 if on else 0)
 

@@ -504,6 +504,10 @@ static std::atomic<int64_t> g_bin_mode{LSR_BIN_AUTO};
 // the backward re-stages its candidates from the tile lists (same results,
 // measured 2.8 % slower at cfg3).  cfg3: 0.6 GB; cfg5 (M = 60 M): 7.7 GB -> off.
 static std::atomic<int64_t> g_lists_max_mb{2048};
+// LSR_OPT_SPLIT_PREPROCESS: the SH colour pass on a second stream, concurrent
+// with the binning (preprocess.hip k_preprocess_colour).
+static std::atomic<int64_t> g_split_pre{1};
+static constexpr int kSplitPreMinP = 1 << 21;
 
 int lsr_set_option(int option, int64_t value)
 {
@@ -516,6 +520,10 @@ int lsr_set_option(int option, int64_t value)
             if (value < 0) return LSR_EINVAL;
             g_lists_max_mb.store(value, std::memory_order_relaxed);
             return LSR_OK;
+        case LSR_OPT_SPLIT_PREPROCESS:
+            if (value != 0 && value != 1) return LSR_EINVAL;
+            g_split_pre.store(value, std::memory_order_relaxed);
+            return LSR_OK;
         default:
             return LSR_EINVAL;
     }
@@ -527,6 +535,7 @@ int lsr_get_option(int option, int64_t* value)
     switch (option) {
         case LSR_OPT_BIN_MODE: *value = g_bin_mode.load(std::memory_order_relaxed); return LSR_OK;
         case LSR_OPT_LISTS_MAX_MB: *value = g_lists_max_mb.load(std::memory_order_relaxed); return LSR_OK;
+        case LSR_OPT_SPLIT_PREPROCESS: *value = g_split_pre.load(std::memory_order_relaxed); return LSR_OK;
         default: return LSR_EINVAL;
     }
 }
@@ -581,6 +590,48 @@ int lsr_profile_query(const char** names, double* ms, int64_t* calls, int max_st
     }
     return n;
 }
+
+// ------------------------------------------- split preprocess: colour stream
+// One non-blocking stream and two events per host thread and device (created
+// on first use, never destroyed: like a BLAS handle).  The SH colour pass runs
+// there behind the geometry pass while the caller's stream bins.
+struct ColourStream {
+    hipStream_t stream = nullptr;
+    hipEvent_t geom_done = nullptr, colour_done = nullptr;
+};
+
+static ColourStream* colour_stream()
+{
+    thread_local ColourStream tab[16];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+    ColourStream& cs = tab[dev];
+    if (!cs.stream) {
+        if (hipStreamCreateWithFlags(&cs.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&cs.geom_done, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&cs.colour_done, hipEventDisableTiming) != hipSuccess) {
+            cs.stream = nullptr;
+            return nullptr;
+        }
+    }
+    return &cs;
+}
+
+// Makes the caller's stream wait for the colour pass exactly once: before the
+// render, or on any early return (the pass writes into the caller's geometry
+// buffer, which must not be released while it runs).
+struct ColourJoin {
+    ColourStream* cs;
+    hipStream_t st;
+    bool done = false;
+    hipError_t wait()
+    {
+        if (!cs || done) return hipSuccess;
+        done = true;
+        return hipStreamWaitEvent(st, cs->colour_done, 0);
+    }
+    ~ColourJoin() { (void)wait(); }
+};
 
 // ------------------------------------------------- host-visible scan total
 // One coherent pinned word per host thread: k_publish_total stores
@@ -726,13 +777,25 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     uint32_t* cls_cnt = (uint32_t*)(img + IL.cls_cnt);
     uint32_t* cls_list = (uint32_t*)(img + IL.cls_list);
 
-    // 1. preprocess
+    // 1. preprocess (the SH colour pass on the second stream when split)
+    ColourStream* colour = nullptr;
+    // from 2M Gaussians up (cfg5 5M: whole forward 2.974 -> 2.812 ms; cfg3 1M: 1.1188 ->
+    // 1.1176 ms, the colour pass only slowing the short count; cfg2 100K: slower,
+    // its forward is bound by host launches; profiles/r05s3_ab_split_cfg*.txt)
+    if (g_split_pre.load(std::memory_order_relaxed) && !s->debug && P >= kSplitPreMinP && in->shs &&
+        !in->colors_precomp) {
+        colour = colour_stream();
+        if (!colour) return LSR_EHIP;
+    }
+    ColourJoin join{colour, st};   // every return after the launch leaves `st` behind the colour pass
     {
         // a pending geometry gradient: the preprocess also stores the SH colour
         // Jacobian the preprocess backward needs (48 B instead of the 192-B SH row)
         const bool jac = (out->grad_ws_request & LSR_GWS_GEOM) != 0 && !s->quick_render;
         StageScope sc(ST_PRE, st);
-        LSR_HIP(launch_preprocess(c, *in, geom, out->radii, jac, st));
+        if (colour) LSR_HIP(launch_preprocess(c, *in, geom, out->radii, jac, st, colour->stream, colour->geom_done,
+                                              colour->colour_done));
+        else LSR_HIP(launch_preprocess(c, *in, geom, out->radii, jac, st));
     }
     LSR_DEBUG_SYNC(s, st, "preprocess");
     HostSlot& hs = host_slot();
@@ -865,6 +928,7 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
             }
         }
     }
+    LSR_HIP(join.wait());   // the SH colours of a split preprocess
     { StageScope sc(ST_RENDER, st); LSR_HIP(launch_render_fwd(ra, st)); }
     LSR_DEBUG_SYNC(s, st, "render");
     LSR_GUARD(guard, "out_color", out->out_color, 3 * NPIX);

@@ -19,7 +19,11 @@ struct Cam {
 };
 
 // preprocess.hip
-hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, int32_t* radii, bool jac, hipStream_t st);
+// colour_st != nullptr (with two events): the SH colour pass runs there behind
+// geom_done and records colour_done (lsr_api.hip waits for it before the render)
+hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, int32_t* radii, bool jac,
+                             hipStream_t st, hipStream_t colour_st = nullptr, hipEvent_t geom_done = nullptr,
+                             hipEvent_t colour_done = nullptr);
 hipError_t launch_sh_grad_from_views(int64_t N, int M, int deg, const float* means3D, int R, const float* campos,
                                      const float* drgb, float* dL_dsh, hipStream_t st);
 hipError_t launch_preprocess_bwd(const Cam& c, const lsr_inputs& in, const uint8_t* geom, const int32_t* radii,

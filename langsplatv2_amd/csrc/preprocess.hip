@@ -134,10 +134,55 @@ __device__ __forceinline__ void sh_dir_jacobian(int deg, const SHV& sh, float x,
 #undef S
 }
 
-template <bool SH16, bool COV>
+// The SH colour of a visible Gaussian (A.1: SH -> RGB, +0.5, clamp >= 0, and the
+// clamp mask), and with `jac` the colour Jacobian d(RGB)/d(dir) the preprocess
+// backward reads instead of the SH row.  sh: the 48 SH values when SH16.
+template <bool SH16>
+__device__ __forceinline__ void sh_colour_one(const Cam& c, const lsr_inputs& in, const GeomLayout& L,
+                                              uint8_t* __restrict__ geom, int i, float mx, float my, float mz,
+                                              const float* sh, bool jac)
+{
+    float* rgbo = (float*)(geom + L.rgb);
+    uint32_t* clampm = (uint32_t*)(geom + L.clamped);
+    float dir[3], dor[3];
+    sh_dir(mx, my, mz, c.campos, dir, dor);
+    float out[3];
+    if constexpr (SH16) {
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) out[ch] = sh_channel(c.sh_degree, sh, ch, dir[0], dir[1], dir[2]);
+    } else {
+        const float* shg = in.shs + (size_t)i * in.max_coeffs * 3;
+        for (int ch = 0; ch < 3; ch++) out[ch] = sh_channel(c.sh_degree, shg, ch, dir[0], dir[1], dir[2]);
+    }
+    if (jac) {
+        // the backward's dRGB/d(dir), from the SH row already in registers: the
+        // preprocess backward then reads 36 B instead of the 192-B SH row
+        float ddx[3], ddy[3], ddz[3];
+        if constexpr (SH16) sh_dir_jacobian(c.sh_degree, sh, dir[0], dir[1], dir[2], ddx, ddy, ddz);
+        else sh_dir_jacobian(c.sh_degree, in.shs + (size_t)i * in.max_coeffs * 3, dir[0], dir[1], dir[2], ddx, ddy,
+                             ddz);
+        float3* J = (float3*)(geom + L.shjac) + (size_t)3 * i;
+        J[0] = make_float3(ddx[0], ddx[1], ddx[2]);
+        J[1] = make_float3(ddy[0], ddy[1], ddy[2]);
+        J[2] = make_float3(ddz[0], ddz[1], ddz[2]);
+    }
+    uint32_t m = 0;
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+        m |= (out[ch] < 0.f ? 1u : 0u) << ch;
+        rgbo[3 * i + ch] = fmaxf(out[ch], 0.f);
+    }
+    clampm[i] = m;
+}
+
+// PART 0: the whole of A.1 for Gaussian i; PART 1: the geometry only (no SH
+// colour, rgb or clamp mask: k_preprocess_colour writes those, on a second
+// stream, while the binning runs).
+template <bool SH16, bool COV, int PART = 0>
 __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& in, uint8_t* __restrict__ geom,
                                                int32_t* __restrict__ radii, int i, const float* shrow, bool jac)
 {
+    constexpr bool SHL = SH16 && PART == 0;   // this pass evaluates the SH colour from registers
     const int N = in.P;
     const GeomLayout L = geom_layout(N);
     float4* splatA = (float4*)(geom + L.splatA);
@@ -152,11 +197,11 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
     auto invisible = [&]() {
         radii[i] = 0;
         tiles[i] = 0;
-        clampm[i] = 0;
+        if (PART == 0 || in.colors_precomp) clampm[i] = 0;
         depth[i] = 0.f;
         splatA[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         splatB[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (!in.colors_precomp) {
+        if (PART == 0 && !in.colors_precomp) {
             rgbo[3 * i + 0] = 0.f;
             rgbo[3 * i + 1] = 0.f;
             rgbo[3 * i + 2] = 0.f;
@@ -172,7 +217,7 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
     float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
     float s0 = 0.f, s1 = 0.f, s2 = 0.f;
     float o = 0.f;
-    float sh[SH16 ? 48 : 1];
+    float sh[SHL ? 48 : 1];
     if (LSR_PRE_SH_EARLY) {
         if constexpr (COV) {
 #pragma unroll
@@ -182,7 +227,7 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
             s0 = in.scales[3 * i]; s1 = in.scales[3 * i + 1]; s2 = in.scales[3 * i + 2];
         }
         o = in.opacities[i];
-        if constexpr (SH16) {
+        if constexpr (SHL) {
             const float4* src = reinterpret_cast<const float4*>(in.shs) + (size_t)i * 12;
 #pragma unroll
             for (int k = 0; k < 12; k++) {
@@ -192,7 +237,7 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
         }
         // keep the loads here: the compiler otherwise sinks them past the
         // visibility tests into the blocks that use them (empty asm: no code)
-        if constexpr (SH16) {
+        if constexpr (SHL) {
 #pragma unroll
             for (int k = 0; k < 48; k++) asm volatile("" : "+v"(sh[k]));
         }
@@ -246,11 +291,8 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
         return;
     }
 
-    if (!in.colors_precomp) {
-        float dir[3], dor[3];
-        sh_dir(mx, my, mz, c.campos, dir, dor);
-        float out[3];
-        if constexpr (SH16) {
+    if (PART == 0 && !in.colors_precomp) {
+        if constexpr (SHL) {
             // direct float4 loads (staging every row through LDS measured slower)
             if (!LSR_PRE_SH_EARLY) {
                 const float4* src = reinterpret_cast<const float4*>(in.shs) + (size_t)i * 12;
@@ -260,32 +302,9 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
                     sh[4 * k] = v.x; sh[4 * k + 1] = v.y; sh[4 * k + 2] = v.z; sh[4 * k + 3] = v.w;
                 }
             }
-#pragma unroll
-            for (int ch = 0; ch < 3; ch++) out[ch] = sh_channel(c.sh_degree, sh, ch, dir[0], dir[1], dir[2]);
-        } else {
-            const float* shg = in.shs + (size_t)i * in.max_coeffs * 3;
-            for (int ch = 0; ch < 3; ch++) out[ch] = sh_channel(c.sh_degree, shg, ch, dir[0], dir[1], dir[2]);
         }
-        if (jac) {
-            // the backward's dRGB/d(dir), from the SH row already in registers: the
-            // preprocess backward then reads 48 B instead of the 192-B SH row
-            float ddx[3], ddy[3], ddz[3];
-            if constexpr (SH16) sh_dir_jacobian(c.sh_degree, sh, dir[0], dir[1], dir[2], ddx, ddy, ddz);
-            else sh_dir_jacobian(c.sh_degree, in.shs + (size_t)i * in.max_coeffs * 3, dir[0], dir[1], dir[2], ddx, ddy,
-                                 ddz);
-            float3* J = (float3*)(geom + L.shjac) + (size_t)3 * i;
-            J[0] = make_float3(ddx[0], ddx[1], ddx[2]);
-            J[1] = make_float3(ddy[0], ddy[1], ddy[2]);
-            J[2] = make_float3(ddz[0], ddz[1], ddz[2]);
-        }
-        uint32_t m = 0;
-#pragma unroll
-        for (int ch = 0; ch < 3; ch++) {
-            m |= (out[ch] < 0.f ? 1u : 0u) << ch;
-            rgbo[3 * i + ch] = fmaxf(out[ch], 0.f);
-        }
-        clampm[i] = m;
-    } else {
+        sh_colour_one<SHL>(c, in, L, geom, i, mx, my, mz, sh, jac);
+    } else if (in.colors_precomp) {
         clampm[i] = 0;
     }
     if (!LSR_PRE_SH_EARLY) o = in.opacities[i];
@@ -298,26 +317,74 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
     tiles[i] = (uint32_t)area;
 }
 
-template <bool SH16, bool COV>
+template <bool SH16, bool COV, int PART = 0>
 __global__ void __launch_bounds__(256) k_preprocess(Cam c, lsr_inputs in, uint8_t* __restrict__ geom,
                                                     int32_t* __restrict__ radii, int jac)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) ((uint32_t*)(geom + geom_layout(in.P).flags))[0] = jac ? 1u : 0u;
+    if (PART == 0 && i == 0) ((uint32_t*)(geom + geom_layout(in.P).flags))[0] = jac ? 1u : 0u;
     if (i >= in.P) return;
-    preprocess_one<SH16, COV>(c, in, geom, radii, i, nullptr, jac != 0);
+    preprocess_one<SH16, COV, PART>(c, in, geom, radii, i, nullptr, jac != 0);
+}
+
+// The SH colour pass of a split preprocess (PART 1 above did the geometry):
+// every input loaded up front; invisible Gaussians get rgb 0 and mask 0 as in
+// the fused pass.  Same expressions, so rgb / mask / Jacobian are bit-identical.
+template <bool SH16>
+__global__ void __launch_bounds__(256) k_preprocess_colour(Cam c, lsr_inputs in, uint8_t* __restrict__ geom,
+                                                           const int32_t* __restrict__ radii, int jac)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const GeomLayout L = geom_layout(in.P);
+    if (i == 0) ((uint32_t*)(geom + L.flags))[0] = jac ? 1u : 0u;
+    if (i >= in.P) return;
+    const int r = radii[i];
+    const float mx = in.means3D[3 * i], my = in.means3D[3 * i + 1], mz = in.means3D[3 * i + 2];
+    float sh[SH16 ? 48 : 1];
+    if constexpr (SH16) {
+        const float4* src = reinterpret_cast<const float4*>(in.shs) + (size_t)i * 12;
+#pragma unroll
+        for (int k = 0; k < 12; k++) {
+            const float4 v = src[k];
+            sh[4 * k] = v.x; sh[4 * k + 1] = v.y; sh[4 * k + 2] = v.z; sh[4 * k + 3] = v.w;
+        }
+    }
+    if (r <= 0) {
+        float* rgbo = (float*)(geom + L.rgb);
+        rgbo[3 * i] = 0.f;
+        rgbo[3 * i + 1] = 0.f;
+        rgbo[3 * i + 2] = 0.f;
+        ((uint32_t*)(geom + L.clamped))[i] = 0;
+        return;
+    }
+    sh_colour_one<SH16>(c, in, L, geom, i, mx, my, mz, sh, jac != 0);
 }
 
 // jac: a geometry gradient is pending -- store the SH colour Jacobian for the
 // preprocess backward (SH inputs only)
 hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, int32_t* radii, bool jac,
-                             hipStream_t st)
+                             hipStream_t st, hipStream_t colour_st, hipEvent_t geom_done, hipEvent_t colour_done)
 {
     if (in.P == 0) return hipSuccess;
     const bool sh16 = in.shs && in.max_coeffs == 16 && ((uintptr_t)in.shs % 16 == 0);
     const bool cov = in.cov3D_precomp != nullptr;
     const int j = (jac && in.shs && !in.colors_precomp) ? 1 : 0;
     const dim3 g((in.P + 255) / 256);
+    if (colour_st && in.shs && !in.colors_precomp) {
+        // split: the geometry on `st` (what the binning needs), the SH colour on
+        // colour_st behind geom_done; the caller makes `st` wait for colour_done
+        // before the render
+        if (cov) k_preprocess<false, true, 1><<<g, 256, 0, st>>>(c, in, geom, radii, j);
+        else k_preprocess<false, false, 1><<<g, 256, 0, st>>>(c, in, geom, radii, j);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        if ((e = hipEventRecord(geom_done, st)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(colour_st, geom_done, 0)) != hipSuccess) return e;
+        if (sh16) k_preprocess_colour<true><<<g, 256, 0, colour_st>>>(c, in, geom, radii, j);
+        else k_preprocess_colour<false><<<g, 256, 0, colour_st>>>(c, in, geom, radii, j);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        return hipEventRecord(colour_done, colour_st);
+    }
     if (sh16 && cov) k_preprocess<true, true><<<g, 256, 0, st>>>(c, in, geom, radii, j);
     else if (sh16) k_preprocess<true, false><<<g, 256, 0, st>>>(c, in, geom, radii, j);
     else if (cov) k_preprocess<false, true><<<g, 256, 0, st>>>(c, in, geom, radii, j);

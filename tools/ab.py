@@ -17,6 +17,8 @@ from langsplatv2_amd.scenes import CONFIGS, make_camera, make_gaussians  # noqa:
 import bench  # noqa: E402
 
 variants = [a.split("=", 1) for a in sys.argv[1:]]
+split0 = {name: path.endswith("#split0") for name, path in variants}
+variants = [(name, path[:-len("#split0")] if split0[name] else path) for name, path in variants]
 modes = {name: _lib.BIN_MODES[path.split("#", 1)[1]] if "#" in path else None for name, path in variants}
 libs = {name: _lib.load(path.split("#", 1)[0]) for name, path in variants}
 cfg = CONFIGS[int(os.environ.get("LSR_CFG", "3"))]
@@ -54,9 +56,18 @@ dc = torch.randn(3, cfg["H"], cfg["W"], device=dev)
 dl = torch.randn(D, cfg["H"], cfg["W"], device=dev)
 
 
+def set_split(name):
+    # "name=path#split0": the fused preprocess (LSR_OPT_SPLIT_PREPROCESS 0)
+    lib = libs[name]
+    if hasattr(lib, "lsr_set_option"):
+        lib.lsr_set_option.argtypes = [ctypes.c_int, ctypes.c_int64]
+        lib.lsr_set_option(3, 0 if split0[name] else 1)
+
+
 def run(name, steps):
     lib = libs[name]
     _lib._lib = lib
+    set_split(name)
     if modes[name] is not None:
         lib.lsr_set_option.argtypes = [ctypes.c_int, ctypes.c_int64]
         assert lib.lsr_set_option(_lib.LSR_OPT_BIN_MODE, modes[name]) == 0
@@ -80,6 +91,7 @@ def run(name, steps):
 def step_ms(name, steps):
     """Whole steps back to back, no stage events (what bench.py times)."""
     _lib._lib = libs[name]
+    set_split(name)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
