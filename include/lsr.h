@@ -341,7 +341,7 @@ int lsr_abi_version(void);
 #define LSR_OPT_BIN_MODE 1
 #define LSR_OPT_LISTS_MAX_MB 2
 /* LSR_OPT_SPLIT_PREPROCESS (default 1): a forward with SH colours of at least
- * 2^21 Gaussians evaluates the SH colour on a library-owned second stream
+ * 2^19 Gaussians evaluates the SH colour on a library-owned second stream
  * of the current device, concurrent with the tile binning (the geometry the
  * binning needs stays on the caller's stream, and the render waits for both);
  * 0: one fused preprocess kernel on the caller's stream.  Results identical. */

@@ -507,7 +507,13 @@ static std::atomic<int64_t> g_lists_max_mb{2048};
 // LSR_OPT_SPLIT_PREPROCESS: the SH colour pass on a second stream, concurrent
 // with the binning (preprocess.hip k_preprocess_colour).
 static std::atomic<int64_t> g_split_pre{1};
-static constexpr int kSplitPreMinP = 1 << 21;
+#ifndef LSR_SPLIT_MIN_P
+#define LSR_SPLIT_MIN_P (1 << 19)
+#endif
+#ifndef LSR_SPLIT_AFTER_COUNT
+#define LSR_SPLIT_AFTER_COUNT 0   // 1: the colour pass starts behind the tile count instead of the geometry
+#endif
+static constexpr int kSplitPreMinP = LSR_SPLIT_MIN_P;
 
 int lsr_set_option(int option, int64_t value)
 {
@@ -779,9 +785,11 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
 
     // 1. preprocess (the SH colour pass on the second stream when split)
     ColourStream* colour = nullptr;
-    // from 2M Gaussians up (cfg5 5M: whole forward 2.974 -> 2.812 ms; cfg3 1M: 1.1188 ->
-    // 1.1176 ms, the colour pass only slowing the short count; cfg2 100K: slower,
-    // its forward is bound by host launches; profiles/r05s3_ab_split_cfg*.txt)
+    // from 512K Gaussians up (cfg5 5M: whole forward 2.974 -> 2.812 and 2.995 -> 2.835 ms;
+    // cfg3 1M fwd+bwd: 1.1188 -> 1.1176 and 1.1259 -> 1.1156 ms, the colour pass slowing
+    // the short count; cfg2 100K: slower, its forward is bound by host launches; the
+    // colour pass started behind the count instead: cfg5 2.946, cfg3 1.1159 ms;
+    // profiles/r05s3_ab_split_cfg*.txt, r05s3_ab_split_start_cfg*.txt)
     if (g_split_pre.load(std::memory_order_relaxed) && !s->debug && P >= kSplitPreMinP && in->shs &&
         !in->colors_precomp) {
         colour = colour_stream();
@@ -793,9 +801,10 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
         // Jacobian the preprocess backward needs (48 B instead of the 192-B SH row)
         const bool jac = (out->grad_ws_request & LSR_GWS_GEOM) != 0 && !s->quick_render;
         StageScope sc(ST_PRE, st);
-        if (colour) LSR_HIP(launch_preprocess(c, *in, geom, out->radii, jac, st, colour->stream, colour->geom_done,
-                                              colour->colour_done));
-        else LSR_HIP(launch_preprocess(c, *in, geom, out->radii, jac, st));
+        LSR_HIP(launch_preprocess(c, *in, geom, out->radii, jac, st, colour != nullptr));
+        if (colour && !LSR_SPLIT_AFTER_COUNT)
+            LSR_HIP(launch_preprocess_colour(c, *in, geom, out->radii, jac, st, colour->stream, colour->geom_done,
+                                             colour->colour_done));
     }
     LSR_DEBUG_SYNC(s, st, "preprocess");
     HostSlot& hs = host_slot();
@@ -819,6 +828,11 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
         LSR_HIP(launch_scan_u32((const uint32_t*)(geom + GL.tiles), (uint32_t*)(geom + GL.offsets), gpart,
                                 (size_t)P, false, st));
         LSR_HIP(launch_publish_total(gpart + gnb, nullptr, hs.dev, seq, nullptr, st));
+    }
+    if (colour && LSR_SPLIT_AFTER_COUNT) {
+        const bool jac = (out->grad_ws_request & LSR_GWS_GEOM) != 0 && !s->quick_render;
+        LSR_HIP(launch_preprocess_colour(c, *in, geom, out->radii, jac, st, colour->stream, colour->geom_done,
+                                         colour->colour_done));
     }
     // speculative binning workspace sized from the previous call's M, taken
     // while the GPU is still counting, so the host usually has nothing but

@@ -19,11 +19,12 @@ struct Cam {
 };
 
 // preprocess.hip
-// colour_st != nullptr (with two events): the SH colour pass runs there behind
-// geom_done and records colour_done (lsr_api.hip waits for it before the render)
+// geom_only (SH inputs): the geometry pass only; the SH colour pass is
+// launch_preprocess_colour, on a second stream (lsr_api.hip, split preprocess)
 hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, int32_t* radii, bool jac,
-                             hipStream_t st, hipStream_t colour_st = nullptr, hipEvent_t geom_done = nullptr,
-                             hipEvent_t colour_done = nullptr);
+                             hipStream_t st, bool geom_only = false);
+hipError_t launch_preprocess_colour(const Cam& c, const lsr_inputs& in, uint8_t* geom, const int32_t* radii, bool jac,
+                                    hipStream_t st, hipStream_t colour_st, hipEvent_t ready, hipEvent_t done);
 hipError_t launch_sh_grad_from_views(int64_t N, int M, int deg, const float* means3D, int R, const float* campos,
                                      const float* drgb, float* dL_dsh, hipStream_t st);
 hipError_t launch_preprocess_bwd(const Cam& c, const lsr_inputs& in, const uint8_t* geom, const int32_t* radii,

@@ -362,28 +362,38 @@ __global__ void __launch_bounds__(256) k_preprocess_colour(Cam c, lsr_inputs in,
 
 // jac: a geometry gradient is pending -- store the SH colour Jacobian for the
 // preprocess backward (SH inputs only)
+// The SH colour pass of a split preprocess on colour_st, behind everything
+// enqueued on `st` so far (`ready` recorded there); records `done` on colour_st.
+hipError_t launch_preprocess_colour(const Cam& c, const lsr_inputs& in, uint8_t* geom, const int32_t* radii, bool jac,
+                                    hipStream_t st, hipStream_t colour_st, hipEvent_t ready, hipEvent_t done)
+{
+    if (in.P == 0) return hipSuccess;
+    const bool sh16 = in.shs && in.max_coeffs == 16 && ((uintptr_t)in.shs % 16 == 0);
+    const int j = (jac && in.shs && !in.colors_precomp) ? 1 : 0;
+    const dim3 g((in.P + 255) / 256);
+    hipError_t e;
+    if ((e = hipEventRecord(ready, st)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(colour_st, ready, 0)) != hipSuccess) return e;
+    if (sh16) k_preprocess_colour<true><<<g, 256, 0, colour_st>>>(c, in, geom, radii, j);
+    else k_preprocess_colour<false><<<g, 256, 0, colour_st>>>(c, in, geom, radii, j);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return hipEventRecord(done, colour_st);
+}
+
 hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, int32_t* radii, bool jac,
-                             hipStream_t st, hipStream_t colour_st, hipEvent_t geom_done, hipEvent_t colour_done)
+                             hipStream_t st, bool geom_only)
 {
     if (in.P == 0) return hipSuccess;
     const bool sh16 = in.shs && in.max_coeffs == 16 && ((uintptr_t)in.shs % 16 == 0);
     const bool cov = in.cov3D_precomp != nullptr;
     const int j = (jac && in.shs && !in.colors_precomp) ? 1 : 0;
     const dim3 g((in.P + 255) / 256);
-    if (colour_st && in.shs && !in.colors_precomp) {
-        // split: the geometry on `st` (what the binning needs), the SH colour on
-        // colour_st behind geom_done; the caller makes `st` wait for colour_done
-        // before the render
+    if (geom_only && in.shs && !in.colors_precomp) {
+        // split: the geometry only (what the binning needs); the caller launches
+        // the SH colour pass (launch_preprocess_colour) on its second stream
         if (cov) k_preprocess<false, true, 1><<<g, 256, 0, st>>>(c, in, geom, radii, j);
         else k_preprocess<false, false, 1><<<g, 256, 0, st>>>(c, in, geom, radii, j);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        if ((e = hipEventRecord(geom_done, st)) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(colour_st, geom_done, 0)) != hipSuccess) return e;
-        if (sh16) k_preprocess_colour<true><<<g, 256, 0, colour_st>>>(c, in, geom, radii, j);
-        else k_preprocess_colour<false><<<g, 256, 0, colour_st>>>(c, in, geom, radii, j);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        return hipEventRecord(colour_done, colour_st);
+        return hipGetLastError();
     }
     if (sh16 && cov) k_preprocess<true, true><<<g, 256, 0, st>>>(c, in, geom, radii, j);
     else if (sh16) k_preprocess<true, false><<<g, 256, 0, st>>>(c, in, geom, radii, j);

@@ -32,7 +32,7 @@ def _both(fn):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kw", [dict(sh_degree=3, lang_dim=16), dict(sh_degree=1), dict(sh_degree=3, quick_k=4)])
 def test_split_equals_fused_forward(gpu, kw):
-    case = make_case(N=(1 << 21) + 5000, W=512, H=384, seed=5, **kw)   # P >= 2^21: the split applies
+    case = make_case(N=(1 << 19) + 5000, W=512, H=384, seed=5, **kw)   # P >= 2^19: the split applies
     a, b = _both(lambda: run_gpu_forward(case, gpu))
     for k in ("color", "lang", "radii", "rgb", "clamped", "depth", "xy", "conic_opacity", "n_contrib", "final_T",
               "point_list"):
@@ -41,7 +41,7 @@ def test_split_equals_fused_forward(gpu, kw):
 
 @pytest.mark.gpu
 def test_split_equals_fused_backward(gpu):
-    case = make_case(N=(1 << 21) + 5000, W=512, H=384, seed=6, sh_degree=3, lang_dim=16)
+    case = make_case(N=(1 << 19) + 5000, W=512, H=384, seed=6, sh_degree=3, lang_dim=16)
     rng = np.random.default_rng(2)
     dc = rng.standard_normal((3, 384, 512)).astype(np.float32)
     dl = rng.standard_normal((16, 384, 512)).astype(np.float32)
@@ -49,5 +49,6 @@ def test_split_equals_fused_backward(gpu):
     np.testing.assert_array_equal(b["color"], a["color"])
     for k in a:
         if k.startswith("grad_"):
-            np.testing.assert_allclose(b[k], a[k], rtol=1e-5, atol=1e-6 * max(1.0, float(np.abs(a[k]).max())),
+            # two backwards of one forward differ only in float-atomic summation order
+            np.testing.assert_allclose(b[k], a[k], rtol=1e-4, atol=1e-5 * max(1.0, float(np.abs(a[k]).max())),
                                        err_msg=k)
