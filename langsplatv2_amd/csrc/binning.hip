@@ -709,12 +709,22 @@ __global__ void __launch_bounds__(BB) k_bin_scatter(Cam c, int P, int chunk, int
 // the chunk count for the same ~512 blocks — a smaller B x T table and longer
 // per-(chunk, tile) key runs: bin_count 0.0756 -> 0.0691 ms, scatter +0.002 (r02
 // A/B; cfg2 count -10 %; cfg5 already has 34-row bands, 24 / 17 were slower).
+// Below 4M Gaussians up to 68 rows in up to 2 x LSR_BAND_LDS (r05: cfg3 is then
+// one band, its ~512 blocks 512 chunks, and the scatter's blocks twice as many:
+// bin_scatter 0.0806 -> 0.0586 ms, whole step 1.1085 -> 1.0984 ms; at cfg5 68-row
+// bands were slower, count 0.313 -> 0.363 ms; profiles/r05s3_ab_bands_cfg*.txt).
 #ifndef LSR_BAND_ROWS
 #define LSR_BAND_ROWS 34
 #endif
-static int bin_band_rows(const Cam& c)
+#ifndef LSR_BAND_ROWS_SMALL
+#define LSR_BAND_ROWS_SMALL 68
+#endif
+static int bin_band_rows(const Cam& c, int P)
 {
-    return std::max(1, std::min(std::min(c.gy, LSR_BAND_ROWS), LSR_BAND_LDS / (4 * c.gx)));
+    const bool big = P >= (4 << 20);
+    const int cap = big ? LSR_BAND_ROWS : LSR_BAND_ROWS_SMALL;
+    const int lds = big ? LSR_BAND_LDS : 2 * LSR_BAND_LDS;
+    return std::max(1, std::min(std::min(c.gy, cap), lds / (4 * c.gx)));
 }
 
 // Tile rows per scatter band: the largest band whose LDS bases fit
@@ -751,7 +761,7 @@ int bin_blocks(int P, const Cam& c, int& chunk)
 {
     // ~512 (chunk x band) blocks, 2 per CU, of >= 1024 Gaussians; fewer
     // chunks when there are several bands keeps the B x T table small
-    const int rows = bin_band_rows(c);
+    const int rows = bin_band_rows(c, P);
     const int S = (c.gy + rows - 1) / rows;
     // twice the blocks from 4M Gaussians up: cfg5 (5M) bin_scatter 1.20 ->
     // 1.02 ms; at cfg3 (1M) 1024 blocks make the count + table pass slower
@@ -772,7 +782,7 @@ hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t
                             uint32_t* cls_cnt, uint32_t* cls_list, uint64_t* host_slot, uint32_t seq, hipStream_t st)
 {
     const int T = c.gx * c.gy;
-    const int rows = bin_band_rows(c);
+    const int rows = bin_band_rows(c, P);
     const int S = (c.gy + rows - 1) / rows;
     const dim3 grid(LSR_COUNT_XCD ? B * S : B, LSR_COUNT_XCD ? 1 : S);
     const size_t lds = (size_t)rows * c.gx * 4;
