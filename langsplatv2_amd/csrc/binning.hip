@@ -751,10 +751,10 @@ int bin_scatter_rows(const Cam& c)
     return std::max(1, std::min(c.gy, LSR_SCATTER_LDS / (4 * c.gx)));
 }
 
-// Threads per (chunk, band) block: 16 waves below 4M Gaussians (cfg3
-// bin_count 0.070 -> 0.061 ms: the LDS histogram's clear and flush loops
-// halve), 8 waves from 4M up (16 measured slower at cfg5: count 0.60 -> 0.66,
-// scatter 0.98 -> 1.11 ms).
+// Threads per (chunk, band) scatter block (and the chunk granule): 16 waves
+// below 4M Gaussians, 8 waves from 4M up (16 measured slower at cfg5: scatter
+// 0.98 -> 1.11 ms).  The count runs 8-wave blocks at every size (r05; in r02
+// 16 waves had been faster for the count at cfg3 with 34-row bands).
 int bin_block(int P) { return P >= (4 << 20) ? 512 : 1024; }
 
 int bin_blocks(int P, const Cam& c, int& chunk)
@@ -788,15 +788,15 @@ hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t
     const size_t lds = (size_t)rows * c.gx * 4;
     if (lds > 65536) {
         (void)hipFuncSetAttribute((const void*)k_bin_count<512>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        (void)hipFuncSetAttribute((const void*)k_bin_count<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         (void)hipFuncSetAttribute((const void*)k_bin_scatter<512>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         (void)hipFuncSetAttribute((const void*)k_bin_scatter<1024>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
     if (B > 0) {
-        if (bin_block(P) == 1024)
-            k_bin_count<1024><<<grid, 1024, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt);
-        else
-            k_bin_count<512><<<grid, 512, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt);
+        // 8-wave count blocks at every size (r05, with the 68-row bands and the
+        // colour pass beside it: cfg3 bin_count 0.104 -> 0.077 ms, step -1.3 / -1.7 %
+        // in both A/B orders, profiles/r05s3_ab_tune{2,3}_cfg3.txt); the scatter keeps
+        // bin_block's 16 waves below 4M
+        k_bin_count<512><<<grid, 512, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt);
         BinPublish pb{tpart, cls_cnt + LSR_TICKET_WORD, tile_start + T, host_slot, seq};
         const int G = (T + TBL_TILES - 1) / TBL_TILES, Tp = table_stride(T);
         if (B <= 16 * TBL_RPT)
