@@ -599,23 +599,32 @@ int lsr_profile_query(const char** names, double* ms, int64_t* calls, int max_st
 
 // ------------------------------------------- split preprocess: colour stream
 // One non-blocking stream and two events per host thread and device (created
-// on first use, never destroyed: like a BLAS handle).  The SH colour pass runs
-// there behind the geometry pass while the caller's stream bins.
+// on first use, never destroyed: like a BLAS handle), on the device of the
+// caller's stream (not the thread's current device: a caller may pass another
+// device's stream).  The SH colour pass runs there behind the geometry pass
+// while the caller's stream bins.
 struct ColourStream {
     hipStream_t stream = nullptr;
     hipEvent_t geom_done = nullptr, colour_done = nullptr;
 };
 
-static ColourStream* colour_stream()
+static ColourStream* colour_stream(hipStream_t st)
 {
     thread_local ColourStream tab[16];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+    hipDevice_t sdev = 0;
+    int cur = 0;
+    if (hipStreamGetDevice(st, &sdev) != hipSuccess || hipGetDevice(&cur) != hipSuccess) return nullptr;
+    const int dev = (int)sdev;
+    if (dev < 0 || dev >= 16) return nullptr;
     ColourStream& cs = tab[dev];
     if (!cs.stream) {
-        if (hipStreamCreateWithFlags(&cs.stream, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&cs.geom_done, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&cs.colour_done, hipEventDisableTiming) != hipSuccess) {
+        // streams and events belong to the device current at their creation
+        if (dev != cur && hipSetDevice(dev) != hipSuccess) return nullptr;
+        const bool ok = hipStreamCreateWithFlags(&cs.stream, hipStreamNonBlocking) == hipSuccess &&
+                        hipEventCreateWithFlags(&cs.geom_done, hipEventDisableTiming) == hipSuccess &&
+                        hipEventCreateWithFlags(&cs.colour_done, hipEventDisableTiming) == hipSuccess;
+        if (dev != cur) (void)hipSetDevice(cur);
+        if (!ok) {
             cs.stream = nullptr;
             return nullptr;
         }
@@ -792,7 +801,7 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     // profiles/r05s3_ab_split_cfg*.txt, r05s3_ab_split_start_cfg*.txt)
     if (g_split_pre.load(std::memory_order_relaxed) && !s->debug && P >= kSplitPreMinP && in->shs &&
         !in->colors_precomp) {
-        colour = colour_stream();
+        colour = colour_stream(st);
         if (!colour) return LSR_EHIP;
     }
     ColourJoin join{colour, st};   // every return after the launch leaves `st` behind the colour pass
