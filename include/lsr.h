@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 11  /* 11 (r05): LSR_INDEX_PACKED, lsr_quick_pack_codes;
+#define LSR_ABI_VERSION 11  /* 11 (r05): LSR_INDEX_PACKED, lsr_quick_pack_codes, LSR_OPT_SPLIT_PREPROCESS;
                                10 (r05): lsr_settings.quick_layout, lsr_quick_decode_run weight_layout;
                                9 (r05): LSR_OPT_LISTS_MAX_MB; LSR_BIN_ORDERED removed */
 
