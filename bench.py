@@ -525,10 +525,15 @@ def main() -> int:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     if args.dry_run:
         return dry_run(world, rank, args.config)
+    # rehearsal only (a multi-rank run on a one-GPU box): LSR_BENCH_BACKEND=gloo and
+    # LSR_BENCH_SAME_DEVICE=1 put every rank on cuda:0 with a gloo exchange; the
+    # driver's runs use neither (RCCL, one GPU per rank)
     if world > 1:
-        dist.init_process_group("nccl")
+        dist.init_process_group(os.environ.get("LSR_BENCH_BACKEND", "nccl"))
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"bench.py: RCCL sees {dist.get_world_size()} ranks, expected {args.gpus}")
+    if os.environ.get("LSR_BENCH_SAME_DEVICE") == "1":
+        local = 0
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     _lib.load()
