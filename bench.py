@@ -436,10 +436,28 @@ def main_forward_replicas(args, world, rank, dev) -> int:
     _lib.profile_enable(False)
     _lib.profile_stages(None)
     dom_ms_s, dom_calls = _lib.profile_query()[dom]
+    # the same forwards over a stream of views, two in flight (view_stream.ViewStream):
+    # reported beside `value`, which is one view at a time
+    from langsplatv2_amd.view_stream import ViewStream
+    vs = ViewStream(dev)
+    for _ in range(3):
+        vs.push(step)
+    vs.flush()
+    torch.cuda.synchronize()
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.barrier()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        vs.push(step)
+    vs.flush()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed_stream = time.perf_counter() - t1
+    if world > 1:
+        t = torch.tensor([elapsed, elapsed_stream], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)   # timing only, not on the data path
-        elapsed = float(t.item())
+        elapsed, elapsed_stream = float(t[0].item()), float(t[1].item())
     if rank == 0:
         S = 3 * (deg + 1) ** 2 if deg is not None else 0
         bytes_, info = algorithmic_bytes(g, rs, D, S)
@@ -491,6 +509,9 @@ def main_forward_replicas(args, world, rank, dev) -> int:
             "stages_ms": {k: round(v, 4) for k, v in per_stage.items()},
             "stage_bytes": {k: int(bytes_[k]) for k in fwd_keys if k in bytes_},
             "workload_stats": info,
+            "view_stream_fps": round(world * args.steps / elapsed_stream, 3),
+            "view_stream_note": "the same forwards over a stream of views, two in flight on alternating "
+                                "HIP streams (langsplatv2_amd.view_stream.ViewStream); `value` is one view at a time",
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cam, gcpu, D, cfg_name=f"cfg{args.config}", backward=False,

@@ -352,6 +352,13 @@ int lsr_abi_version(void);
 int lsr_set_option(int option, int64_t value);
 int lsr_get_option(int option, int64_t* value);
 
+/* A non-blocking HIP stream on the current device (no implicit
+ * synchronisation with the legacy default stream), created with the HIP
+ * runtime this library uses; for callers that overlap renders across streams
+ * (langsplatv2_amd.view_stream).  lsr_stream_destroy releases it. */
+int lsr_stream_create(void** stream);
+int lsr_stream_destroy(void* stream);
+
 /* Dense language channel sets compiled into this build (ascending; D is
  * rounded up to the next set).  Returns the largest supported D. */
 int lsr_max_lang_dim(void);

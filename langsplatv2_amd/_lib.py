@@ -129,7 +129,7 @@ EXPORTS = ("lsr_forward", "lsr_backward", "lsr_mark_visible", "lsr_quick_decode"
            "lsr_quick_decode_prepare", "lsr_quick_decode_run", "lsr_quick_pack_codes", "lsr_topk_code_forward",
            "lsr_topk_code_backward", "lsr_topk_code_backward_sparse", "lsr_knn_dist2", "lsr_lang_loss_forward", "lsr_lang_loss_backward", "lsr_adam_step", "lsr_sh_grad_from_views", "lsr_strerror",
            "lsr_abi_version", "lsr_max_lang_dim", "lsr_profile_enable", "lsr_profile_stages", "lsr_profile_reset",
-           "lsr_profile_query", "lsr_set_option", "lsr_get_option")
+           "lsr_profile_query", "lsr_set_option", "lsr_get_option", "lsr_stream_create", "lsr_stream_destroy")
 
 _lib = None
 
@@ -164,6 +164,11 @@ def load(path: str | None = None):
     lib.lsr_quick_decode_run.argtypes = [_vp, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float, _vp, _vp]
     lib.lsr_quick_decode_run.restype = ctypes.c_int
+    if hasattr(lib, "lsr_stream_create"):      # (older A/B builds lack it)
+        lib.lsr_stream_create.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+        lib.lsr_stream_create.restype = ctypes.c_int
+        lib.lsr_stream_destroy.argtypes = [ctypes.c_void_p]
+        lib.lsr_stream_destroy.restype = ctypes.c_int
     if hasattr(lib, "lsr_quick_pack_codes"):   # (older A/B builds lack it)
         lib.lsr_quick_pack_codes.argtypes = [_vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, _vp, _vp]
         lib.lsr_quick_pack_codes.restype = ctypes.c_int
@@ -261,6 +266,24 @@ def set_split_preprocess(on: bool) -> bool:
     check(lib.lsr_get_option(LSR_OPT_SPLIT_PREPROCESS, ctypes.byref(prev)), "lsr_get_option")
     check(lib.lsr_set_option(LSR_OPT_SPLIT_PREPROCESS, 1 if on else 0), "lsr_set_option")
     return bool(prev.value)
+
+
+def nonblocking_stream(device) -> "torch.cuda.ExternalStream":
+    """A torch stream object over a non-blocking HIP stream of `device` (no
+    implicit synchronisation with the legacy default stream, which
+    torch.cuda.Stream() pool streams keep), created by the library's HIP
+    runtime (lsr_stream_create).  Kept for the process's lifetime."""
+    import torch
+    dev = torch.device(device)
+    with torch.cuda.device(dev):
+        p = ctypes.c_void_p(0)
+        check(load().lsr_stream_create(ctypes.byref(p)), "lsr_stream_create")
+    s = torch.cuda.ExternalStream(p.value, device=dev)
+    _STREAMS.append(s)
+    return s
+
+
+_STREAMS = []
 
 
 def profile_enable(on: bool = True):

@@ -548,6 +548,21 @@ int lsr_get_option(int option, int64_t* value)
 
 int lsr_max_lang_dim(void) { return 64; }
 
+int lsr_stream_create(void** stream)
+{
+    if (!stream) return LSR_EINVAL;
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return LSR_EHIP;
+    *stream = (void*)s;
+    return LSR_OK;
+}
+
+int lsr_stream_destroy(void* stream)
+{
+    if (!stream) return LSR_EINVAL;
+    return hipStreamDestroy((hipStream_t)stream) == hipSuccess ? LSR_OK : LSR_EHIP;
+}
+
 void lsr_profile_enable(int on)
 {
     g_prof.on.store(on != 0);

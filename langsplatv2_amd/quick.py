@@ -115,7 +115,8 @@ class QuickFeatureStream:
 
     def __init__(self, codebooks: torch.Tensor, normalize: bool = True, eps: float = 1e-10):
         self.codebooks, self.normalize, self.eps = codebooks, bool(normalize), float(eps)
-        self._decode_stream = torch.cuda.Stream(codebooks.device)
+        from ._lib import nonblocking_stream
+        self._decode_stream = nonblocking_stream(codebooks.device)   # no implicit sync with the default stream
         self._pending = None
 
     def push(self, render_fn) -> torch.Tensor | None:
