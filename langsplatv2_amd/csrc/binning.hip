@@ -151,6 +151,7 @@ __global__ void k_publish_total(const uint64_t* __restrict__ total, uint32_t* __
         uint32_t* h = (uint32_t*)(host_slot + 1);
 #pragma unroll
         for (int k = 0; k < SORT_NCLS; k++) h[k] = cls_cnt[k];
+        __atomic_store_n(host_slot + LSR_CLS_SLOT, ((uint64_t)seq << 32) | m32, __ATOMIC_RELEASE);
     }
     __atomic_store_n(host_slot, ((uint64_t)seq << 32) | m32, __ATOMIC_RELEASE);
 }
@@ -406,10 +407,11 @@ template <int BB>
 __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int rows, int S,
                                                          const uint8_t* __restrict__ geom,
                                                          const int32_t* __restrict__ radii, uint32_t* __restrict__ table,
-                                                         uint32_t* __restrict__ cls_cnt)
+                                                         uint32_t* __restrict__ cls_cnt, uint64_t* host_slot, uint32_t seq)
 {
     extern __shared__ uint32_t hist[];
     __shared__ WaveSpans wss[BB / 64];
+    __shared__ uint64_t s_tot;
     const int T = c.gx * c.gy;
 #if LSR_COUNT_XCD
     // chunk-major, XCD-aware (as k_bin_scatter): a chunk's bands share an L2
@@ -424,6 +426,7 @@ __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int r
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < SORT_NCLS) cls_cnt[threadIdx.x] = 0;
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) cls_cnt[LSR_TICKET_WORD] = 0;
     for (int k = threadIdx.x; k < bd.nt; k += BB) hist[k] = 0;
+    if (threadIdx.x == 0) s_tot = 0;
     __syncthreads();
     WaveSpans& ws = wss[threadIdx.x >> 6];
     const int lane = threadIdx.x & 63;
@@ -452,6 +455,7 @@ __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int r
     // straight into the block's table row; one wave per row, 64 columns a step
     uint32_t* row = table + (size_t)blk * table_stride(T) + bd.t0;
     const int nrows = bd.ty1 - bd.ty0;
+    uint64_t mine = 0;   // the lane's share of the block's instances
     for (int r = threadIdx.x >> 6; r < nrows; r += BB / 64) {
         uint32_t carry = 0;
         for (int x0 = 0; x0 < c.gx; x0 += 64) {
@@ -462,8 +466,31 @@ __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int r
                 const uint32_t t = __shfl_up(v, d, 64);
                 if (lane >= d) v += t;
             }
-            if (x < c.gx) row[r * c.gx + x] = carry + v;
+            if (x < c.gx) {
+                row[r * c.gx + x] = carry + v;
+                mine += carry + v;
+            }
             carry += __shfl(v, 63, 64);
+        }
+    }
+    // M = the sum of every block's counts, published here rather than by
+    // k_bin_table: the host sizes and launches the scatter while the column
+    // scan runs (the sort classes follow from k_bin_table).  One agent-scope
+    // add per block carries the block total and, in bits 44+, its arrival; the
+    // block whose add completes the grid holds M.  The sum word is zeroed by
+    // the preprocess (the launch before us).
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) mine += __shfl_xor(mine, d, 64);
+    if (lane == 0 && mine) atomicAdd((unsigned long long*)&s_tot, (unsigned long long)mine);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint64_t add = s_tot + (1ull << 44);
+        const uint64_t prev = __hip_atomic_fetch_add((uint64_t*)(cls_cnt + LSR_COUNT_WORD), add, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+        if ((prev >> 44) == (uint64_t)gridDim.x * gridDim.y - 1) {
+            const uint64_t m = (prev + add) & ((1ull << 44) - 1);
+            const uint32_t m32 = m >= 0xffffffffull ? 0xffffffffu : (uint32_t)m;
+            __hip_atomic_store(host_slot, ((uint64_t)seq << 32) | m32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
@@ -479,9 +506,9 @@ __global__ void __launch_bounds__(BB) k_bin_count(Cam c, int P, int chunk, int r
 // every block stores its group total write-through (sc1) and takes a ticket
 // (agent-scope add after every wave drained its stores, behind a workgroup
 // barrier); the block holding the last ticket scans the group totals (sc1
-// loads, in place), writes tile_start[T] = M and publishes M plus the sort
-// class counts to the pinned host word (what k_publish_total does on the
-// B = 0 path).  k_tile_start_apply then adds each group's base to the
+// loads, in place), writes tile_start[T] = M and publishes the sort class
+// counts with M to the pinned host line (word LSR_CLS_SLOT; k_bin_count
+// published M alone in word 0 one launch earlier).  k_tile_start_apply then adds each group's base to the
 // in-group scan.  This replaces three scan launches and the publish launch.
 // The ticket is zeroed by k_bin_count (the preceding launch).
 #define TBL_TILES 64   // tiles per k_bin_table block (and per tile group)
@@ -490,7 +517,7 @@ struct BinPublish {
     uint64_t* gpart;      // per tile group: total, then (last block) exclusive base; [G] = M
     uint32_t* ticket;     // arrival counter, zero on entry
     uint32_t* tile_end;   // tile_start + T
-    uint64_t* host_slot;  // pinned host word (+ class counts after it)
+    uint64_t* host_slot;  // pinned host word LSR_CLS_SLOT (the class counts are words 1..3)
     uint32_t seq;
 };
 __device__ __forceinline__ uint32_t u4_get(const uint4& v, int j) { return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w; }
@@ -605,7 +632,7 @@ __global__ void __launch_bounds__(16 * SEGS) k_bin_table(int T, int Tp, int B, u
             const uint32_t m32 = carry >= 0xffffffffull ? 0xffffffffu : (uint32_t)carry;
             pb.gpart[G] = carry;
             *pb.tile_end = m32;
-            uint32_t* h = (uint32_t*)(pb.host_slot + 1);
+            uint32_t* h = (uint32_t*)(pb.host_slot - LSR_CLS_SLOT + 1);
 #pragma unroll
             for (int k = 0; k < SORT_NCLS; k++) __hip_atomic_store(&h[k], cv[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             // the counts are written through (system scope) and acknowledged
@@ -796,8 +823,9 @@ hipError_t launch_bin_count(const Cam& c, int P, int chunk, int B, const uint8_t
         // colour pass beside it: cfg3 bin_count 0.104 -> 0.077 ms, step -1.3 / -1.7 %
         // in both A/B orders, profiles/r05s3_ab_tune{2,3}_cfg3.txt); the scatter keeps
         // bin_block's 16 waves below 4M
-        k_bin_count<512><<<grid, 512, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt);
-        BinPublish pb{tpart, cls_cnt + LSR_TICKET_WORD, tile_start + T, host_slot, seq};
+        if ((size_t)grid.x * grid.y >= (1u << 20)) return hipErrorInvalidValue;   // arrivals field (bits 44+)
+        k_bin_count<512><<<grid, 512, lds, st>>>(c, P, chunk, rows, S, geom, radii, table, cls_cnt, host_slot, seq);
+        BinPublish pb{tpart, cls_cnt + LSR_TICKET_WORD, tile_start + T, host_slot + LSR_CLS_SLOT, seq};
         const int G = (T + TBL_TILES - 1) / TBL_TILES, Tp = table_stride(T);
         if (B <= 16 * TBL_RPT)
             k_bin_table<16><<<G, 256, 0, st>>>(T, Tp, B, table, tile_cnt, cls_cnt, cls_list, pb);

@@ -664,8 +664,10 @@ struct ColourJoin {
 };
 
 // ------------------------------------------------- host-visible scan total
-// One coherent pinned word per host thread: k_publish_total stores
-// (seq << 32 | M) into it and the host spins until the sequence matches.
+// One coherent pinned line per host thread: word 0 receives (seq << 32 | M)
+// from k_bin_count (k_publish_total on the global-atomic path), words 1..3 the
+// tile-sort class counts and word LSR_CLS_SLOT (seq << 32 | M) once those are
+// out (k_bin_table); the host spins until a word's sequence matches.
 struct HostSlot {
     uint64_t* word = nullptr;   // host view
     uint64_t* dev = nullptr;    // device view of the same word
@@ -693,9 +695,9 @@ static HostSlot& host_slot()
 // Spin on the published word; every 4096 polls ask the runtime whether the
 // stream has drained (which also covers a stream the runtime has not
 // submitted yet, and reports a faulted stream instead of spinning forever).
-static int wait_published(HostSlot& hs, uint32_t seq, hipStream_t st, uint64_t* M)
+static int wait_published(HostSlot& hs, uint32_t seq, hipStream_t st, uint64_t* M, int slot = 0)
 {
-    volatile uint64_t* w = hs.word;
+    volatile uint64_t* w = hs.word + slot;
     for (uint64_t it = 1;; it++) {
         uint64_t v = __atomic_load_n((uint64_t*)w, __ATOMIC_ACQUIRE);
         if ((uint32_t)(v >> 32) == seq) {
@@ -825,7 +827,8 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
         // Jacobian the preprocess backward needs (48 B instead of the 192-B SH row)
         const bool jac = (out->grad_ws_request & LSR_GWS_GEOM) != 0 && !s->quick_render;
         StageScope sc(ST_PRE, st);
-        LSR_HIP(launch_preprocess(c, *in, geom, out->radii, jac, st, colour != nullptr));
+        LSR_HIP(launch_preprocess(c, *in, geom, out->radii, jac, st, colour != nullptr,
+                                  priv ? (uint64_t*)(cls_cnt + LSR_COUNT_WORD) : nullptr));
         if (colour && !LSR_SPLIT_AFTER_COUNT)
             LSR_HIP(launch_preprocess_colour(c, *in, geom, out->radii, jac, st, colour->stream, colour->geom_done,
                                              colour->colour_done));
@@ -876,10 +879,6 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     if (M >= 0xffffffffull) return LSR_EOVERFLOW;
     out->num_rendered = (int64_t)M;
     hs.last_m = M;
-    // the privatised path published the tile-sort class counts with M
-    uint32_t host_cls[SORT_NCLS];
-    if (priv)
-        for (int k = 0; k < SORT_NCLS; k++) host_cls[k] = ((volatile uint32_t*)(hs.word + 1))[k];
 
     // 3. binning workspace + scatter into tile buckets
     const BinLayout BL = bin_layout((size_t)M);
@@ -910,6 +909,21 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
                                (uint64_t*)(bin + BL.keys), st));
     }
     LSR_DEBUG_SYNC(s, st, "scatter");
+    // the privatised path's tile-sort class counts: published by the column
+    // scan (k_bin_table) with its own M, after the count published M -- the
+    // scatter above was launched in between
+    uint32_t host_cls[SORT_NCLS];
+    if (priv) {
+        uint64_t M2 = 0;
+        rc = wait_published(hs, seq, st, &M2, LSR_CLS_SLOT);
+        if (rc != LSR_OK) return rc;
+        if (M2 != M) {
+            fprintf(stderr, "[lsr] tile count and column scan disagree on M (%llu vs %llu)\n",
+                    (unsigned long long)M, (unsigned long long)M2);
+            return LSR_EHIP;
+        }
+        for (int k = 0; k < SORT_NCLS; k++) host_cls[k] = ((volatile uint32_t*)(hs.word + 1))[k];
+    }
     {
         StageScope sc(ST_SORT, st);
         LSR_HIP(launch_tile_sort(T, tile_start, (uint64_t*)(bin + BL.keys), (uint32_t*)(bin + BL.point_list), cls_cnt,

@@ -567,7 +567,8 @@ __host__ __device__ inline ImageLayout image_layout(size_t P, size_t T)
     L.tile_cnt = o;   o += align256(T * 4);
     L.tile_start = o; o += align256((T + 1) * 4);   // exclusive scan, [T] = num_rendered
     L.tile_part = o;  o += align256(((T + 63) / 64 + 1) * 8);   // scan partials / 64-tile group bases
-    L.cls_cnt = o;    o += 256;                        // per-class tile counts (tile-sort classes); word 32: ticket
+    L.cls_cnt = o;    o += 512;                        // per-class tile counts (tile-sort classes); word 32: ticket;
+                                                       // words 64-65: the tile count's total + arrivals
     L.cls_list = o;   o += align256(T * 6 * 4);        // per-class tile lists, T slots each
     L.total = o;
     return L;

@@ -22,7 +22,7 @@ struct Cam {
 // geom_only (SH inputs): the geometry pass only; the SH colour pass is
 // launch_preprocess_colour, on a second stream (lsr_api.hip, split preprocess)
 hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, int32_t* radii, bool jac,
-                             hipStream_t st, bool geom_only = false);
+                             hipStream_t st, bool geom_only = false, uint64_t* zero_word = nullptr);
 hipError_t launch_preprocess_colour(const Cam& c, const lsr_inputs& in, uint8_t* geom, const int32_t* radii, bool jac,
                                     hipStream_t st, hipStream_t colour_st, hipEvent_t ready, hipEvent_t done);
 hipError_t launch_sh_grad_from_views(int64_t N, int M, int deg, const float* means3D, int R, const float* campos,
@@ -40,6 +40,9 @@ hipError_t launch_scan_u32(const uint32_t* in, uint32_t* out, uint64_t* part, si
 // and lists live in the image workspace (cls_cnt, cls_list).
 #define SORT_NCLS 6
 #define LSR_TICKET_WORD 32   // cls_cnt word k_bin_table counts arrivals in (own 128-B line)
+#define LSR_COUNT_WORD 64    // cls_cnt words (one u64) k_bin_count sums M and arrivals in (own line;
+                             // zeroed by the preprocess)
+#define LSR_CLS_SLOT 4       // pinned host word (u64 index) k_bin_table publishes the class counts under
 hipError_t launch_publish_total(const uint64_t* total, uint32_t* tile_end, uint64_t* host_slot, uint32_t seq,
                                 const uint32_t* cls_cnt, hipStream_t st);
 hipError_t launch_duplicate(const Cam& c, int P, const uint8_t* geom, const int32_t* radii, uint32_t* tile_cnt,

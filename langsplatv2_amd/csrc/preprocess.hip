@@ -319,10 +319,11 @@ __device__ __forceinline__ void preprocess_one(const Cam& c, const lsr_inputs& i
 
 template <bool SH16, bool COV, int PART = 0>
 __global__ void __launch_bounds__(256) k_preprocess(Cam c, lsr_inputs in, uint8_t* __restrict__ geom,
-                                                    int32_t* __restrict__ radii, int jac)
+                                                    int32_t* __restrict__ radii, int jac, uint64_t* zero_word)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (PART == 0 && i == 0) ((uint32_t*)(geom + geom_layout(in.P).flags))[0] = jac ? 1u : 0u;
+    if (zero_word && i == 0) *zero_word = 0;   // the tile count's total (k_bin_count, next on the stream)
     if (i >= in.P) return;
     preprocess_one<SH16, COV, PART>(c, in, geom, radii, i, nullptr, jac != 0);
 }
@@ -381,7 +382,7 @@ hipError_t launch_preprocess_colour(const Cam& c, const lsr_inputs& in, uint8_t*
 }
 
 hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, int32_t* radii, bool jac,
-                             hipStream_t st, bool geom_only)
+                             hipStream_t st, bool geom_only, uint64_t* zero_word)
 {
     if (in.P == 0) return hipSuccess;
     const bool sh16 = in.shs && in.max_coeffs == 16 && ((uintptr_t)in.shs % 16 == 0);
@@ -391,14 +392,14 @@ hipError_t launch_preprocess(const Cam& c, const lsr_inputs& in, uint8_t* geom, 
     if (geom_only && in.shs && !in.colors_precomp) {
         // split: the geometry only (what the binning needs); the caller launches
         // the SH colour pass (launch_preprocess_colour) on its second stream
-        if (cov) k_preprocess<false, true, 1><<<g, 256, 0, st>>>(c, in, geom, radii, j);
-        else k_preprocess<false, false, 1><<<g, 256, 0, st>>>(c, in, geom, radii, j);
+        if (cov) k_preprocess<false, true, 1><<<g, 256, 0, st>>>(c, in, geom, radii, j, zero_word);
+        else k_preprocess<false, false, 1><<<g, 256, 0, st>>>(c, in, geom, radii, j, zero_word);
         return hipGetLastError();
     }
-    if (sh16 && cov) k_preprocess<true, true><<<g, 256, 0, st>>>(c, in, geom, radii, j);
-    else if (sh16) k_preprocess<true, false><<<g, 256, 0, st>>>(c, in, geom, radii, j);
-    else if (cov) k_preprocess<false, true><<<g, 256, 0, st>>>(c, in, geom, radii, j);
-    else k_preprocess<false, false><<<g, 256, 0, st>>>(c, in, geom, radii, j);
+    if (sh16 && cov) k_preprocess<true, true><<<g, 256, 0, st>>>(c, in, geom, radii, j, zero_word);
+    else if (sh16) k_preprocess<true, false><<<g, 256, 0, st>>>(c, in, geom, radii, j, zero_word);
+    else if (cov) k_preprocess<false, true><<<g, 256, 0, st>>>(c, in, geom, radii, j, zero_word);
+    else k_preprocess<false, false><<<g, 256, 0, st>>>(c, in, geom, radii, j, zero_word);
     return hipGetLastError();
 }
 
