@@ -510,6 +510,9 @@ static std::atomic<int64_t> g_split_pre{1};
 #ifndef LSR_SPLIT_MIN_P
 #define LSR_SPLIT_MIN_P (1 << 19)
 #endif
+#ifndef LSR_COLOUR_EVENT_FLAGS
+#define LSR_COLOUR_EVENT_FLAGS hipEventDisableTiming   // A/B: | hipEventReleaseToDevice
+#endif
 #ifndef LSR_SPLIT_AFTER_COUNT
 #define LSR_SPLIT_AFTER_COUNT 0   // 1: the colour pass starts behind the tile count instead of the geometry
 #endif
@@ -636,8 +639,8 @@ static ColourStream* colour_stream(hipStream_t st)
         // streams and events belong to the device current at their creation
         if (dev != cur && hipSetDevice(dev) != hipSuccess) return nullptr;
         const bool ok = hipStreamCreateWithFlags(&cs.stream, hipStreamNonBlocking) == hipSuccess &&
-                        hipEventCreateWithFlags(&cs.geom_done, hipEventDisableTiming) == hipSuccess &&
-                        hipEventCreateWithFlags(&cs.colour_done, hipEventDisableTiming) == hipSuccess;
+                        hipEventCreateWithFlags(&cs.geom_done, LSR_COLOUR_EVENT_FLAGS) == hipSuccess &&
+                        hipEventCreateWithFlags(&cs.colour_done, LSR_COLOUR_EVENT_FLAGS) == hipSuccess;
         if (dev != cur) (void)hipSetDevice(cur);
         if (!ok) {
             cs.stream = nullptr;
