@@ -287,12 +287,15 @@ def fwd_fps(g, dev, sh_degree, D, W=1280, H=800, iters=20):
 def quick_fps(N, dev, W=1280, H=800, iters=20):
     """The evaluation path behind the reference's "450+ FPS" (README.md:1, eval_lerf.py:210-220):
     quick render of 3 levels x top-4 codes into 192 channels, then the 3 x 64 x 512 codebook
-    decode + L2 normalise, at 1.0 Mpix.  The headline fields time the map in the pixel-major
-    layout (language_feature_layout="hwc": the same values, a (192,H,W) view the reference's
-    .view(3, 64, H, W).view(3, 64, H*W) + einsum accept unchanged; tests/test_quick_layout.py);
-    `reference_layout` times the reference's contiguous (192,H,W) map.  render_decode_fps is
-    one view at a time (render, then decode); render_decode_stream_fps is the throughput over a
-    stream of views with each decode overlapping the next render (quick.QuickFeatureStream)."""
+    decode + L2 normalise, at 1.0 Mpix.  The headline fields use DEFAULT settings, exactly as the
+    reference's unchanged caller builds them (no language_feature_layout: the map is the
+    pixel-major (192,H,W) view, which the reference's .view(3, 64, H, W).view(3, 64, H*W) +
+    einsum accept unchanged; tests/test_quick_layout.py).  `reference_layout` times the
+    contiguous map (language_feature_layout="chw").  render_decode_fps is one view at a time
+    (render, then this package's decode); render_decode_stream_fps is the throughput over a
+    stream of views with each decode overlapping the next render (quick.QuickFeatureStream);
+    `reference_consumer` times the reference's own decode on the same map, torch.einsum +
+    /(norm + 1e-10) exactly as eval_lerf.py:214-218."""
     from langsplatv2_amd import quick
     cam = make_camera(W, H)
     g = make_gaussians(N, cam, seed=0, sh_degree=3, quick_k=4)
@@ -300,7 +303,7 @@ def quick_fps(N, dev, W=1280, H=800, iters=20):
     z = torch.zeros_like(t["means3D"])
     cb = torch.randn(3, 64, 512, device=dev)
 
-    def measure(layout):
+    def measure(layout, consumer=False):
         r = GaussianRasterizer(settings(cam, dev, 3, False, quick=True, quick_layout=layout))
 
         def render():
@@ -320,13 +323,28 @@ def quick_fps(N, dev, W=1280, H=800, iters=20):
             fs.push(render)
         s_stream = timeit(streamed, iters)
         fs.flush()
-        return dict(render_fps=round(1.0 / s_render, 1), render_decode_fps=round(1.0 / s_total, 1),
-                    render_ms=round(s_render * 1e3, 4), decode_ms=round((s_total - s_render) * 1e3, 4),
-                    render_decode_stream_fps=round(1.0 / s_stream, 1))
+        res = dict(render_fps=round(1.0 / s_render, 1), render_decode_fps=round(1.0 / s_total, 1),
+                   render_ms=round(s_render * 1e3, 4), decode_ms=round((s_total - s_render) * 1e3, 4),
+                   render_decode_stream_fps=round(1.0 / s_stream, 1))
+        if consumer:
+            cbt = cb.permute(0, 2, 1)
+
+            def reference_consumer():
+                with torch.no_grad():
+                    m = render()
+                    D, Hh, Ww = m.shape
+                    m = m.view(3, 64, Hh, Ww).view(3, 64, Hh * Ww)
+                    f = torch.einsum('ldk,lkn->ldn', cbt, m).view(3, 512, Hh, Ww)
+                    return f / (f.norm(dim=1, keepdim=True) + 1e-10)
+            s_ref = timeit(reference_consumer, iters)
+            res["reference_consumer"] = dict(
+                what="render + the reference's torch.einsum decode + /(norm+1e-10) (eval_lerf.py:214-218)",
+                render_decode_fps=round(1.0 / s_ref, 1), decode_ms=round((s_ref - s_render) * 1e3, 4))
+        return res
     out = dict(workload=f"{N} Gaussians {W}x{H}, quick 3x top-4 -> 192 ch + 3x64x512 decode + L2 norm",
-               layout="hwc (pixel-major quick map, language_feature_layout='hwc')")
-    out.update(measure("hwc"))
-    out["reference_layout"] = measure(None)
+               layout="default settings (pixel-major quick map view; language_feature_layout unset)")
+    out.update(measure(None, consumer=True))
+    out["reference_layout"] = measure("chw")
     return out
 
 

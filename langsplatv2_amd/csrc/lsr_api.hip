@@ -617,13 +617,24 @@ int lsr_profile_query(const char** names, double* ms, int64_t* calls, int max_st
 
 // ------------------------------------------- split preprocess: colour stream
 // One non-blocking stream and two events per host thread and device (created
-// on first use, never destroyed: like a BLAS handle), on the device of the
+// on first use, destroyed when the thread exits), on the device of the
 // caller's stream (not the thread's current device: a caller may pass another
 // device's stream).  The SH colour pass runs there behind the geometry pass
-// while the caller's stream bins.
+// while the caller's stream bins.  When no colour stream can be had (device
+// index >= 16, creation failure) the forward runs the fused preprocess, which
+// gives identical results.
 struct ColourStream {
     hipStream_t stream = nullptr;
     hipEvent_t geom_done = nullptr, colour_done = nullptr;
+    void release()
+    {
+        if (colour_done) (void)hipEventDestroy(colour_done);
+        if (geom_done) (void)hipEventDestroy(geom_done);
+        if (stream) (void)hipStreamDestroy(stream);
+        stream = nullptr;
+        geom_done = colour_done = nullptr;
+    }
+    ~ColourStream() { release(); }
 };
 
 static ColourStream* colour_stream(hipStream_t st)
@@ -643,7 +654,7 @@ static ColourStream* colour_stream(hipStream_t st)
                         hipEventCreateWithFlags(&cs.colour_done, LSR_COLOUR_EVENT_FLAGS) == hipSuccess;
         if (dev != cur) (void)hipSetDevice(cur);
         if (!ok) {
-            cs.stream = nullptr;
+            cs.release();
             return nullptr;
         }
     }
@@ -821,8 +832,7 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     // profiles/r05s3_ab_split_cfg*.txt, r05s3_ab_split_start_cfg*.txt)
     if (g_split_pre.load(std::memory_order_relaxed) && !s->debug && P >= kSplitPreMinP && in->shs &&
         !in->colors_precomp) {
-        colour = colour_stream(st);
-        if (!colour) return LSR_EHIP;
+        colour = colour_stream(st);   // nullptr: the fused preprocess below (same results)
     }
     ColourJoin join{colour, st};   // every return after the launch leaves `st` behind the colour pass
     {

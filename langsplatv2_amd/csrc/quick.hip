@@ -735,6 +735,7 @@ hipError_t launch_quick_decode_run(const float* wmap, const float* cb, int L, in
 {
     if (L == 0 || H == 0 || W == 0) return hipSuccess;
 #ifdef LSR_DECODE_F32
+    if (hwc) return hipErrorInvalidValue;   // this A/B variant reads the channel-major map only
     const unsigned nb = (unsigned)(((W + 15) / 16) * ((H + 3) / 4));
     k_quick_decode<64><<<nb, 64, 0, st>>>(wmap, L, Df, W, H, cb, (const float*)ws, out, eps, normalize);
 #else

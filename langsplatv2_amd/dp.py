@@ -24,6 +24,13 @@ messages, not one per tensor.  Two buckets, by when their gradients are final:
 Zero-copy: `ViewShardedExchange.sink()` hands the rasterizer backward the
 buckets' views as its output buffers (rasterizer.GradSink), so gradients are
 written straight into the all-reduce buffers (no ~300 MB pack copy).
+The early all-reduce is started from a gradient hook on each language leaf,
+which autograd calls once with the leaf's TOTAL gradient (every path summed):
+when that is the bucket view itself (the rasterizer is the only path) the
+all-reduce waits on the library's lang-ready event and overlaps the preprocess
+backward; when another path also reaches the leaf (a regulariser, a second
+use) the hook first packs the sum into the view.  So a multi-path gradient is
+never dropped or raced, in any mode.
 
 View-factored SH gradient (zero-copy path, SH inputs): the SH coefficient
 gradient of a view is an outer product, dL/dsh_k = basis_k(dir) * dL/dRGB
@@ -35,20 +42,17 @@ rank rebuilds the summed SH gradient locally in view order
 (lsr_sh_grad_from_views) — identical on all ranks, equal to the all-reduced
 sum up to fp32 summation order.  Per GPU the exchange moves
 2(R-1)/R * 29 + (R-1)/R * 3R floats per Gaussian instead of 2(R-1)/R * 77:
--47 % at R = 8, -57 % at R = 2.
+-47 % at R = 8, -57 % at R = 2.  The backward hands autograd an expanded zero
+as the SH gradient (GradSink.sh_return), so a second path into the SH leaf
+arrives at its hook as exactly that path's own gradient; the exchange
+all-reduces it and adds it to the rebuilt sum.
 """
 from __future__ import annotations
-
-import os
 
 import torch
 import torch.distributed as dist
 
 
-
-def _debug() -> bool:
-    """LSR_DP_DEBUG=1: extra consistency checks in the exchange (they synchronise)."""
-    return os.environ.get("LSR_DP_DEBUG", "0") not in ("", "0")
 
 def rank_yaw(rank: int, world: int, spread_deg: float = 40.0) -> float:
     """Camera yaw of the view rank `rank` renders in the synthetic benchmark:
@@ -197,8 +201,14 @@ class ViewShardedExchange:
         self.cuda = params[0].is_cuda
         self._params = list(params)
         self._sink = None
+        self._hooks = []
+        self._early_seen = set()   # early indices whose view holds the leaf's total gradient
+        self._early_packed = False
+        self._sh_extra = None      # another path's gradient into the factored SH leaf
+        self._sh_zero = None
         if self.cuda and self.early is not None and self.collective:
             self._ev = torch.cuda.Event()
+            self._ev_pack = torch.cuda.Event()
             self._side = torch.cuda.Stream(device=params[0].device)
 
     @property
@@ -220,34 +230,78 @@ class ViewShardedExchange:
             out[self.sh_idx] = self.sh_grad
         return out
 
-    def _on_lang_ready(self, sink):
-        """GradSink callback: start the early all-reduce only when the backward
-        wrote every early bucket view itself (otherwise finish() packs them first).
-        The condition depends only on which inputs need grad, so every rank
-        decides the same way."""
-        if all(self.names[i] in sink.used for i in self.early_idx):
-            self._launch_early()
+    def _early_hook(self, i, view):
+        """Gradient hook of early leaf i: `g` is the leaf's total gradient.  The view
+        itself: the rasterizer wrote it and nothing else reaches the leaf.  Anything
+        else (a multi-path sum, or a gradient that never went through the sink) is
+        packed into the view first, on the stream that produced it."""
+        def hook(g):
+            packed = False
+            if g is None:
+                view.zero_()
+                packed = True
+            elif g.data_ptr() != view.data_ptr():
+                view.copy_(g.reshape(view.shape))
+                packed = True
+            self._early_seen.add(i)
+            self._early_packed = self._early_packed or packed
+            if len(self._early_seen) == len(self.early_idx):
+                self._launch_early(after_pack=self._early_packed)
+        return hook
 
-    def _launch_early(self):
+    def _sh_hook(self, g):
+        """Gradient hook of the factored SH leaf: the rasterizer returns an expanded
+        zero (GradSink.sh_return), so anything else is another path's own gradient."""
+        if g is not None and g.data_ptr() != self._sh_zero.data_ptr():
+            self._sh_extra = g
+
+    def _launch_early(self, after_pack: bool = True):
         if not self.collective or self.early is None or self._early_work is not None:
             return
         if self._side is not None:
-            self._side.wait_event(self._ev)
+            # the library's lang-ready event (before the preprocess backward) when the
+            # views are the backward's own output; after a pack, a fresh event
+            ev = self._ev
+            if after_pack or not ev.cuda_event:
+                ev = self._ev_pack
+                ev.record(torch.cuda.current_stream(self.early.flat.device))
+            self._side.wait_event(ev)
             with torch.cuda.stream(self._side):
                 self._early_work = self.early.allreduce(self.group, async_op=True)
         else:
             self._early_work = self.early.allreduce(self.group, async_op=True)
 
+    def _remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
     def sink(self):
-        """rasterizer.GradSink writing this rank's gradients into the buckets and
-        starting the early (language) all-reduce once the library marks it final."""
+        """rasterizer.GradSink writing this rank's gradients into the buckets; the
+        early (language) all-reduce starts from the language leaves' gradient hooks."""
         from .rasterizer import GradSink
-        bufs = {nm: v for nm, v in zip(self.names, self._views()) if nm is not None}
+        self._remove_hooks()
+        views = self._views()
+        bufs = {nm: v for nm, v in zip(self.names, views) if nm is not None}
         self._early_work = None
+        self._early_seen = set()
+        self._early_packed = False
+        self._sh_extra = None
+        if self.collective:
+            for i in self.early_idx:
+                p = self._params[i]
+                if p.requires_grad:
+                    self._hooks.append(p.register_hook(self._early_hook(i, views[i])))
+        if self.sh_idx is not None:
+            p = self._params[self.sh_idx]
+            if self._sh_zero is None:
+                self._sh_zero = torch.zeros((1, 1, 1), dtype=torch.float32, device=p.device).expand(tuple(p.shape))
+            if p.requires_grad:
+                self._hooks.append(p.register_hook(self._sh_hook))
         self._sink = GradSink(bufs, lang_ready=self._ev,
-                              on_lang_ready=self._on_lang_ready if self._ev is not None else None,
                               rgb_sh=self.rgb_mine if self.sh_idx is not None else None,
-                              params={nm: p for nm, p in zip(self.names, self._params) if nm is not None})
+                              params={nm: p for nm, p in zip(self.names, self._params) if nm is not None},
+                              sh_return=self._sh_zero)
         return self._sink
 
     def _factored_sh(self, campos, means3D, sh_degree):
@@ -281,42 +335,27 @@ class ViewShardedExchange:
         and `sh_degree` (the rasterizer settings') are required."""
         views = self._views()
         used = self._sink.used if self._sink is not None else set()
+        self._remove_hooks()
         # factored SH only when the backward wrote dL/dRGB for the bucketed SH leaf;
         # otherwise (e.g. shs = cat(f_dc, f_rest)) the SH gradient is all-reduced as is
         factored = self.sh_idx is not None and "shs" in used
         if grads is not None:
             for i, (g, v) in enumerate(zip(grads, views)):
                 if i == self.sh_idx and factored:
-                    continue   # filled by _factored_sh below
+                    continue   # rebuilt by _factored_sh below (+ another path's part, _sh_hook)
+                if i in self._early_seen:
+                    continue   # the hook left the leaf's total gradient in the view
                 if g is not None and g.data_ptr() == v.data_ptr():
                     continue
-                if self.names[i] in used:
-                    # the backward wrote this bucket view itself.  `grads` may hold
-                    # a copy of it (loss.backward() inside `with ex.sink():` leaves
-                    # AccumulateGrad's copy in p.grad) or, when the leaf also gets
-                    # gradient through another path (a regulariser, a second use),
-                    # autograd's SUM: packing g is right in both cases (ADVICE r04)
-                    # -- except on an early-bucket view whose all-reduce is already
-                    # in flight, where packing would race (ADVICE r03): there the
-                    # view must already be the whole gradient (checked with
-                    # LSR_DP_DEBUG=1).
-                    if g is None:
-                        continue
-                    if i in self.early_idx and self._early_work is not None:
-                        if _debug() and not torch.equal(g.reshape(v.shape), v):
-                            raise RuntimeError(f"finish: {self.names[i]} has gradient from outside the rasterizer, "
-                                               "but its early all-reduce already started")
-                        continue
-                    v.copy_(g.reshape(v.shape))
-                    continue
-                if i in self.early_idx and self._early_work is not None:
-                    # the early all-reduce is in flight on this view: packing it now would race
-                    raise RuntimeError("finish: an early-bucket gradient did not land in its bucket view, "
-                                       "but its all-reduce already started")
+                # the backward wrote this view and `grads` holds a copy (loss.backward()
+                # inside `with ex.sink():` leaves AccumulateGrad's copy in p.grad) or
+                # autograd's multi-path SUM: packing g is right in both cases; a view
+                # the backward did not write is packed too (None -> zeros)
                 if g is None:
-                    v.zero_()
-                else:
-                    v.copy_(g.reshape(v.shape))
+                    if self.names[i] not in used:
+                        v.zero_()
+                    continue
+                v.copy_(g.reshape(v.shape))
         elif self.sh_idx is not None and not factored:
             raise ValueError("finish: the SH gradient was not factored by the backward; pass grads")
         if self.with_stats:
@@ -329,6 +368,11 @@ class ViewShardedExchange:
             work = self.main.allreduce(self.group, async_op=True)
             if factored:
                 self._factored_sh(campos, means3D, sh_degree)
+                if self._sh_extra is not None:
+                    # another path into the SH leaf (its own gradient, see _sh_hook)
+                    extra = self._sh_extra.reshape(self.sh_grad.shape).contiguous()
+                    dist.all_reduce(extra, op=dist.ReduceOp.SUM, group=self.group)
+                    self.sh_grad.add_(extra)
             elif self.sh_idx is not None:
                 dist.all_reduce(self.sh_grad, op=dist.ReduceOp.SUM, group=self.group)
             if radii is not None:
@@ -339,6 +383,7 @@ class ViewShardedExchange:
                 self._early_work.wait()
             self._early_work = None
         self._sink = None
+        self._sh_extra = None
         return views, self.main.stats(), max_radii
 
     def exchange(self, grads, means2D_grad=None, radii=None):

@@ -5,13 +5,15 @@ Surface (what gaussian_renderer/__init__.py:15,37-54,108-119 uses):
                                  gaussian_renderer/__init__.py:37-52, plus an
                                  optional trailing `language_feature_dim`
                                  (quick-path output channels, default 192) and
-                                 `language_feature_layout` ("chw", the default
-                                 and the reference's layout, or "hwc": the
-                                 quick map stored pixel-major, returned as a
-                                 (Dq,H,W) view with strides (1, Dq*W, Dq);
-                                 values identical, and the reference's
-                                 consumers' .view(3, 64, H, W).view(3, 64, H*W)
-                                 + einsum run on it unchanged).
+                                 `language_feature_layout` of the quick map:
+                                 None (default) = "hwc" whenever the 12-code,
+                                 192-channel kernel applies, else "chw";
+                                 "hwc" = stored pixel-major and returned as a
+                                 (Dq,H,W) view with strides (1, Dq*W, Dq)
+                                 (values identical; the reference's consumers'
+                                 .view(3, 64, H, W).view(3, 64, H*W) + einsum
+                                 and .view(D, -1) run on it unchanged);
+                                 "chw" = the reference's contiguous (Dq,H,W).
   GaussianRasterizer(raster_settings)  nn.Module;
       forward(means3D, means2D, opacities, shs=None, colors_precomp=None,
               language_feature_precomp=None,
@@ -47,6 +49,7 @@ from __future__ import annotations
 
 import ctypes
 import threading
+import weakref
 from typing import NamedTuple, Optional
 
 import torch
@@ -81,6 +84,10 @@ class GradSink:
                   buffers["shs"] as the SH gradient, which the caller fills
                   after the exchange (lsr_sh_grad_from_views).  Used only when
                   buffers has "shs" and the SH input needs a gradient.
+      sh_return   optional tensor autograd receives as the SH gradient of a
+                  factored backward instead of buffers["shs"] (dp.py passes an
+                  expanded zero: a second gradient path into the SH leaf then
+                  sums to exactly its own contribution, which the exchange adds).
 
       params      optional {input name: leaf tensor}: a buffer is used only when
                   the rasterizer's input of that name IS this tensor (the bucketed
@@ -95,11 +102,12 @@ class GradSink:
     Input names: means3D, means2D, shs, colors_precomp, language_feature_precomp,
     language_feature_weights_quick, opacities, scales, rotations, cov3D_precomp."""
 
-    def __init__(self, buffers=None, lang_ready=None, on_lang_ready=None, rgb_sh=None, params=None):
+    def __init__(self, buffers=None, lang_ready=None, on_lang_ready=None, rgb_sh=None, params=None, sh_return=None):
         self.buffers = dict(buffers or {})
         self.lang_ready = lang_ready
         self.on_lang_ready = on_lang_ready
         self.rgb_sh = rgb_sh
+        self.sh_return = sh_return
         self.params = dict(params) if params is not None else None
         self.used: set = set()
 
@@ -153,10 +161,14 @@ class GaussianRasterizationSettings(NamedTuple):
     language_feature_layout: Optional[str] = None
 
 
-def _quick_layout(rs) -> int:
-    """LSR_LAYOUT_* of the quick map ("chw" / None: the reference's (Dq,H,W); "hwc": pixel-major)."""
+def _quick_layout(rs, hwc_ok: bool = False) -> int:
+    """LSR_LAYOUT_* of the quick map: "chw" the reference's contiguous (Dq,H,W); "hwc"
+    pixel-major; None (the default) pixel-major when `hwc_ok` (the inputs fit the kernel
+    that writes it: 12 codes, 192 channels, 16-B aligned rows), else "chw"."""
     lay = rs.language_feature_layout if len(rs) > 15 else None
-    if lay is None or lay == "chw":
+    if lay is None:
+        return _lib.LSR_LAYOUT_HWC if (hwc_ok and rs.quick_render) else _lib.LSR_LAYOUT_CHW
+    if lay == "chw":
         return _lib.LSR_LAYOUT_CHW
     if lay == "hwc":
         if not rs.quick_render:
@@ -199,7 +211,7 @@ class _Alloc:
         self.fn = _lib.ALLOC_FN(cb)
 
 
-def _settings_struct(rs: GaussianRasterizationSettings, dev) -> tuple:
+def _settings_struct(rs: GaussianRasterizationSettings, dev, layout: int = 0) -> tuple:
     bg = _f32(rs.bg, "bg")
     view = _f32(rs.viewmatrix, "viewmatrix")
     proj = _f32(rs.projmatrix, "projmatrix")
@@ -208,7 +220,7 @@ def _settings_struct(rs: GaussianRasterizationSettings, dev) -> tuple:
     s = _lib.Settings(int(rs.image_height), int(rs.image_width), float(rs.tanfovx), float(rs.tanfovy),
                       bg.data_ptr(), float(rs.scale_modifier), view.data_ptr(), proj.data_ptr(),
                       int(rs.sh_degree), campos.data_ptr(), int(bool(rs.prefiltered)), int(bool(rs.debug)),
-                      int(bool(rs.include_feature)), int(bool(rs.quick_render)), int(qdim), _quick_layout(rs))
+                      int(bool(rs.include_feature)), int(bool(rs.quick_render)), int(qdim), int(layout))
     return s, (bg, view, proj, campos)
 
 
@@ -226,9 +238,13 @@ def _index_dtype(t: torch.Tensor) -> int:
 # reference's fp32 indices (u5: round half up, range check) is per candidate and
 # frame work, so the forward hands the library packed rows (LSR_INDEX_PACKED,
 # lsr_quick_pack_codes) converted once per indices tensor and kept while that
-# tensor is unchanged (same object, same version counter; the entry holds the
-# tensor, so its storage cannot be reused under the key).  False: the forward
-# passes the indices as they are (A/B, tests).
+# tensor is unchanged (same object, same version counter).  An entry holds only
+# a weak reference to the indices tensor (a dropped tensor's rows are not pinned;
+# a freed tensor's reused storage cannot match: the referent is gone), and the
+# packed rows are marked as used on every stream that reads them (record_stream),
+# so an eviction never returns their block to one stream's pool while a render on
+# another stream still reads it.  False: the forward passes the indices as they
+# are (A/B, tests).
 QUICK_PACKED_CODES = True
 _PACKED = {}
 _PACKED_MAX = 2
@@ -239,19 +255,23 @@ def _packed_codes(qi: torch.Tensor, Dq: int) -> torch.Tensor:
         ver = qi._version
     except RuntimeError:   # an inference tensor tracks no version: convert every call
         ver = None
+    stream = torch.cuda.current_stream(qi.device)
     key = (qi.data_ptr(), qi.device, tuple(qi.shape), qi.dtype, int(Dq))
     hit = _PACKED.get(key)
-    if ver is not None and hit is not None and hit[0] is qi and hit[1] == ver:
-        return hit[2]
+    if ver is not None and hit is not None and hit[0]() is qi and hit[1] == ver:
+        packed = hit[2]
+        if stream != hit[3]:
+            packed.record_stream(stream)
+        return packed
     packed = torch.empty((qi.shape[0], 4), dtype=torch.int32, device=qi.device)
     _lib.check(_lib.load().lsr_quick_pack_codes(qi.data_ptr(), _index_dtype(qi), int(qi.shape[0]), int(qi.shape[1]),
-                                                int(Dq), packed.data_ptr(), _stream(qi.device)),
+                                                int(Dq), packed.data_ptr(), stream.cuda_stream),
                "lsr_quick_pack_codes")
     if ver is not None:
         _PACKED.pop(key, None)
         while len(_PACKED) >= _PACKED_MAX:
             _PACKED.pop(next(iter(_PACKED)))
-        _PACKED[key] = (qi, ver, packed)
+        _PACKED[key] = (weakref.ref(qi), ver, packed, stream)
     return packed
 
 
@@ -309,15 +329,18 @@ def _run_forward(means3D, sh, colors_precomp, language_feature_precomp, language
     Dout = Dq if quick else D
     H, W = int(rs.image_height), int(rs.image_width)
 
-    s, keep = _settings_struct(rs, dev)
     qi_fwd, qi_dt = qi_c, (_index_dtype(qi_c) if qi_c is not None else 0)
     if quick and _use_packed(qw_c, qi_c, Dq):
         qi_fwd, qi_dt = _packed_codes(qi_c, Dq), _lib.LSR_INDEX_PACKED
+    # the quick map's layout: pixel-major by default where its kernel applies (lsr_api validate)
+    layout = _quick_layout(rs, quick and K == 12 and Dq == 192 and qw_c.data_ptr() % 16 == 0
+                           and qi_fwd.data_ptr() % 16 == 0)
+    s, keep = _settings_struct(rs, dev, layout)
     ins = _lib.Inputs(N, M, D, K, qi_dt,
                       means3D_c.data_ptr(), _ptr(sh_c), _ptr(col_c), opac_c.data_ptr(), _ptr(sc_c), _ptr(rot_c),
                       _ptr(cov_c), _ptr(lang_c), _ptr(qw_c), _ptr(qi_fwd))
     color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
-    if quick and _quick_layout(rs) == _lib.LSR_LAYOUT_HWC:
+    if layout == _lib.LSR_LAYOUT_HWC:
         lang_out = torch.empty((H, W, Dout), dtype=torch.float32, device=dev).permute(2, 0, 1)
     else:
         lang_out = torch.empty((Dout, H, W), dtype=torch.float32, device=dev)
@@ -411,7 +434,8 @@ class _RasterizeGaussians(torch.autograd.Function):
         elif quick and grad_lang is not None:
             # the quick channels take part in the backward only when a gradient reaches them
             gl = grad_lang.contiguous()
-        s, keep = _settings_struct(rs, dev)
+        # (the backward reads the contiguous upstream gradient: the map's layout plays no part)
+        s, keep = _settings_struct(rs, dev, _lib.LSR_LAYOUT_CHW)
         ins = _lib.Inputs(N, M, D, K if quick else 0, _index_dtype(qi) if quick else 0, means3D.data_ptr(), _ptr(sh),
                           _ptr(col), opac.data_ptr(), _ptr(sc), _ptr(rot), _ptr(cov), _ptr(lang),
                           _ptr(qw) if quick else None, _ptr(qi) if quick else None)
@@ -480,6 +504,8 @@ class _RasterizeGaussians(torch.autograd.Function):
             _lib.check(rc, "rasterize_gaussians_backward")
         if sink is not None and sink.on_lang_ready is not None:
             sink.on_lang_ready(sink)
+        if rgb_sh is not None and sink.sh_return is not None:
+            g_sh = sink.sh_return
         return (g_means3D if need[0] else None, g_means2D if need[1] else None, g_sh, g_col, g_lang, g_qw, None,
                 g_opac if need[7] else None, g_sc, g_rot, g_cov, None)
 

@@ -129,7 +129,8 @@ def gpu_inputs(case, device, requires_grad=True):
 
 def run_gpu_forward(case, device, lang_layout=None):
     """Forward through the library with workspace buffers decoded (lang_layout:
-    the quick map's language_feature_layout, None = the reference's (Dq,H,W))."""
+    the quick map's language_feature_layout: "chw" the reference's (Dq,H,W), None the
+    default (pixel-major where the 12-code kernel applies), "hwc" pixel-major)."""
     from langsplatv2_amd import layout, rasterizer
     rs = settings_for(case, device, lang_layout)
     t = gpu_inputs(case, device, requires_grad=False)

@@ -173,108 +173,166 @@ def test_grad_sink_leaf_identity_and_reuse():
     assert s2.take("means3D", (4, 3), dev, 12345) is buf
 
 
-def test_early_allreduce_only_when_backward_wrote_the_early_bucket():
-    """The early (language) all-reduce is launched from the sink callback only
-    when every early-bucket view was written by the backward."""
+class _FakeRaster(torch.autograd.Function):
+    """What the rasterizer backward does with a GradSink (rasterizer.py backward):
+    each input's gradient (2 x upstream) goes into the sink's buffer for that leaf
+    when the sink has one, the lang-ready callback runs, and with a factored SH
+    sink the colour part goes to rgb_sh and autograd receives sink.sh_return."""
+
+    @staticmethod
+    def forward(ctx, names, *xs):
+        ctx.names = names
+        ctx.ids = [id(x) for x in xs]
+        return tuple(x * 2.0 for x in xs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        from langsplatv2_amd import rasterizer
+        sink = rasterizer._sink()
+        out = [None]
+        for nm, xid, g in zip(ctx.names, ctx.ids, gs):
+            val = 2.0 * g
+            buf = sink.take(nm, tuple(g.shape), g.device, xid) if sink is not None else None
+            if buf is not None and nm == "shs" and sink.rgb_sh is not None:
+                sink.rgb_sh.copy_(val.sum(1))          # the "colour gradient" of this view
+                out.append(sink.sh_return if sink.sh_return is not None else buf)
+                continue
+            if buf is None:
+                out.append(val)
+            else:
+                buf.copy_(val)
+                out.append(buf)
+        if sink is not None and sink.on_lang_ready is not None:
+            sink.on_lang_ready(sink)
+        return tuple(out)
+
+
+def _step(params, names, local, reg, mode):
+    """One backward through _FakeRaster whose gradient w.r.t. params[i] is local[i],
+    plus (reg not None) a second path adding reg[i]; returns the gradients the
+    caller hands finish() (autograd.grad's, or p.grad after loss.backward())."""
+    ys = _FakeRaster.apply(names, *params)
+    loss = sum((y * (loc / 2.0)).sum() for y, loc in zip(ys, local))
+    if reg is not None:
+        loss = loss + sum((p * r).sum() for p, r in zip(params, reg))
+    if mode == "grad":
+        return list(torch.autograd.grad(loss, params))
+    for p in params:
+        p.grad = None
+    loss.backward()
+    return [p.grad for p in params]
+
+
+def test_early_allreduce_starts_from_the_leaf_hook():
+    """The early (language) all-reduce starts from the language leaf's gradient
+    hook, i.e. only once autograd has the leaf's total gradient, and never
+    without a collective."""
     names = ["means3D", "language_feature_precomp"]
-    params = [torch.zeros(5, 3), torch.zeros(5, 16)]
+    params = [torch.zeros(5, 3, requires_grad=True), torch.zeros(5, 16, requires_grad=True)]
     ex = dp.ViewShardedExchange(params, with_stats=False, names=names)
+    assert not ex.collective
+    with ex.sink():
+        _step(params, names, [torch.ones(5, 3), torch.ones(5, 16)], None, "grad")
+    assert ex._early_work is None and ex._hooks == []   # world 1: no hooks, no collective
+    ex.collective = True                                # as with force_collectives, minus the process group
     launched = []
-    ex._launch_early = lambda: launched.append(1)
-    sink = ex.sink()
-    ex._on_lang_ready(sink)                       # language input had no grad: nothing written
-    assert launched == []
-    sink.used.add("language_feature_precomp")
-    ex._on_lang_ready(sink)
-    assert launched == [1]
+    ex._launch_early = lambda after_pack=True: launched.append(after_pack)
+    loc = [torch.ones(5, 3), torch.full((5, 16), 3.0)]
+    with ex.sink():
+        g = _step(params, names, loc, None, "grad")
+    assert launched == [False]                           # the view itself: no pack, the lang-ready event
+    assert torch.equal(ex._views()[1], loc[1]) and g[1].data_ptr() == ex._views()[1].data_ptr()
+    with ex.sink():
+        _step(params, names, loc, [torch.zeros(5, 3), torch.ones(5, 16)], "grad")
+    assert launched == [False, True]                     # a second path: the sum packed first
+    assert torch.equal(ex._views()[1], loc[1] + 1.0)
+    ex._remove_hooks()
 
 
-def _backward_pattern_worker(rank, world, port):
-    """loss.backward() inside `with ex.sink():` -- the backward writes
-    the bucket views through the sink (and the early all-reduce starts from the
-    lang-ready callback), but AccumulateGrad leaves COPIES of the views in
-    p.grad, so finish() receives gradients that are not the views.  It must take
-    the views (not raise, not re-pack over the running all-reduce)."""
+def _hook_worker(rank, world, port):
+    """the zero-copy exchange with loss.backward() or
+    autograd.grad, with and without a second gradient path into every bucketed
+    leaf (a regulariser).  The early all-reduce starts inside the backward (from
+    the language leaf's hook), and every reduced gradient equals the sum over
+    ranks of (rasterizer part + regulariser part), in every mode, without any
+    debug switch."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         names = ["means3D", "opacities", "language_feature_precomp"]
-        params = [torch.zeros(7, 3), torch.zeros(7, 1), torch.zeros(7, 16)]
+        params = [torch.zeros(7, 3, requires_grad=True), torch.zeros(7, 1, requires_grad=True),
+                  torch.zeros(7, 16, requires_grad=True)]
         ex = dp.ViewShardedExchange(params, with_stats=False, names=names)
-        g = torch.Generator().manual_seed(10 + rank)
-        local = [torch.randn(p.shape, generator=g) for p in params]
-        sink = ex.sink()
-        for nm, p, loc in zip(names, params, local):      # what the rasterizer backward does
-            buf = sink.take(nm, tuple(p.shape), p.device, id(p))
-            assert buf is not None
-            buf.copy_(loc)
-        ex._on_lang_ready(sink)                           # early (language) all-reduce starts now
-        assert ex._early_work is not None
-        copies = [loc.clone() for loc in local]           # AccumulateGrad's copies in p.grad
-        red, _, _ = ex.finish(None, None, copies)
-        exp = [torch.zeros_like(p) for p in params]
-        for r in range(world):
+
+        def parts(r):
             gr = torch.Generator().manual_seed(10 + r)
-            for i, p in enumerate(params):
-                exp[i] += torch.randn(p.shape, generator=gr)
-        for i in range(3):
-            assert torch.allclose(red[i], exp[i], rtol=0, atol=1e-6), names[i]
+            loc = [torch.randn(p.shape, generator=gr) for p in params]
+            reg = [torch.randn(p.shape, generator=gr) for p in params]
+            return loc, reg
+        for mode in ("grad", "backward"):
+            for multipath in (False, True):
+                loc, reg = parts(rank)
+                with ex.sink():
+                    grads = _step(params, names, loc, reg if multipath else None, mode)
+                assert ex._early_work is not None, (mode, multipath)   # started inside the backward
+                red, _, _ = ex.finish(None, None, grads)
+                for i in range(3):
+                    exp = torch.zeros_like(params[i])
+                    for r in range(world):
+                        lo, rg = parts(r)
+                        exp += lo[i] + (rg[i] if multipath else 0.0)
+                    assert torch.allclose(red[i], exp, rtol=0, atol=1e-5), (mode, multipath, names[i])
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-def test_exchange_finish_after_backward_pattern_gloo_world2():
-    mp.spawn(_backward_pattern_worker, args=(2, _free_port()), nprocs=2, join=True)
+def test_exchange_hooks_multipath_gloo_world2():
+    mp.spawn(_hook_worker, args=(2, _free_port()), nprocs=2, join=True)
 
 
-def _multipath_worker(rank, world, port):
-    """a bucketed leaf that ALSO gets gradient from outside the
-    rasterizer (a regulariser): autograd hands finish() the SUM, while the
-    bucket view holds only the rasterizer's part.  finish() must pack the sum for
-    the main bucket; for an early-bucket view whose all-reduce is already in
-    flight it cannot, and LSR_DP_DEBUG=1 makes that an error instead of a silent
-    drop."""
+def _factored_worker(rank, world, port):
+    """The view-factored SH leaf with a second gradient path: the backward hands
+    autograd an expanded zero (GradSink.sh_return), so the leaf's hook sees exactly
+    the other path's gradient, which finish() all-reduces and adds to the rebuilt
+    sum (dp.py:_sh_hook).  sh_grad_from_views is replaced by a host stand-in
+    (the kernel is GPU code; tests/test_sh_factored.py covers it on the GPU)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        names = ["means3D", "opacities", "language_feature_precomp"]
-        params = [torch.zeros(5, 3), torch.zeros(5, 1), torch.zeros(5, 16)]
-        ex = dp.ViewShardedExchange(params, with_stats=False, names=names)
-        g = torch.Generator().manual_seed(20 + rank)
-        local = [torch.randn(p.shape, generator=g) for p in params]
-        reg = [torch.randn(p.shape, generator=g) for p in params]
-        sink = ex.sink()
-        for nm, p, loc in zip(names, params, local):
-            sink.take(nm, tuple(p.shape), p.device, id(p)).copy_(loc)
-        # no early all-reduce started (e.g. the language input took no lang-ready
-        # callback): every view may be packed with autograd's sums
-        sums = [loc + rg for loc, rg in zip(local, reg)]
-        red, _, _ = ex.finish(None, None, sums)
-        exp = [torch.zeros_like(p) for p in params]
-        for r in range(world):
-            gr = torch.Generator().manual_seed(20 + r)
-            lo = [torch.randn(p.shape, generator=gr) for p in params]
-            rg = [torch.randn(p.shape, generator=gr) for p in params]
-            for i in range(3):
-                exp[i] += lo[i] + rg[i]
-        for i in range(3):
-            assert torch.allclose(red[i], exp[i], rtol=0, atol=1e-5), names[i]
-        # the early bucket in flight + a foreign contribution: an error in debug mode
-        sink = ex.sink()
-        for nm, p, loc in zip(names, params, local):
-            sink.take(nm, tuple(p.shape), p.device, id(p)).copy_(loc)
-        ex._on_lang_ready(sink)
-        assert ex._early_work is not None
-        os.environ["LSR_DP_DEBUG"] = "1"
-        with pytest.raises(RuntimeError, match="early all-reduce already started"):
-            ex.finish(None, None, sums)
-        ex._early_work.wait()
+        def fake_rebuild(means3D, campos, drgb, deg, out):
+            out.copy_(drgb.sum(0).unsqueeze(1).expand(out.shape))
+            return out
+        dp.sh_grad_from_views = fake_rebuild
+        names = ["means3D", "shs"]
+        params = [torch.zeros(6, 3, requires_grad=True), torch.zeros(6, 4, 3, requires_grad=True)]
+        ex = dp.ViewShardedExchange(params, with_stats=False, names=names, factor_sh=True)
+
+        def parts(r):
+            gr = torch.Generator().manual_seed(40 + r)
+            return [torch.randn(p.shape, generator=gr) for p in params], [torch.randn(p.shape, generator=gr)
+                                                                          for p in params]
+        for multipath in (False, True):
+            loc, reg = parts(rank)
+            with ex.sink() as sink:
+                grads = _step(params, names, loc, reg if multipath else None, "grad")
+            assert "shs" in sink.used
+            red, _, _ = ex.finish(None, None, grads, campos=torch.zeros(3), means3D=params[0].detach(), sh_degree=1)
+            exp_sh = torch.zeros(6, 4, 3)
+            exp_m = torch.zeros(6, 3)
+            for r in range(world):
+                lo, rg = parts(r)
+                exp_sh += lo[1].sum(1, keepdim=True).expand(6, 4, 3)
+                exp_m += lo[0]
+                if multipath:
+                    exp_sh += rg[1]
+                    exp_m += rg[0]
+            assert torch.allclose(red[1], exp_sh, rtol=0, atol=1e-5), multipath
+            assert torch.allclose(red[0], exp_m, rtol=0, atol=1e-5), multipath
         dist.barrier()
     finally:
-        os.environ.pop("LSR_DP_DEBUG", None)
         dist.destroy_process_group()
 
 
-def test_exchange_finish_packs_multipath_sums_gloo_world2():
-    mp.spawn(_multipath_worker, args=(2, _free_port()), nprocs=2, join=True)
+def test_factored_sh_second_path_gloo_world2():
+    mp.spawn(_factored_worker, args=(2, _free_port()), nprocs=2, join=True)

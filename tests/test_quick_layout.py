@@ -1,5 +1,6 @@
 """The quick map's pixel-major layout (language_feature_layout="hwc",
-lsr_settings.quick_layout = LSR_LAYOUT_HWC) and the decode reading it.
+lsr_settings.quick_layout = LSR_LAYOUT_HWC; the default whenever the 12-code,
+192-channel kernel applies) and the decode reading it.
 
 The reference returns the quick weight map as a contiguous (192, H, W) tensor
 (gaussian_renderer/__init__.py:108-129) and its consumers reshape it with
@@ -27,6 +28,12 @@ def test_layout_setting_validation():
                 viewmatrix=torch.eye(4), projmatrix=torch.eye(4), sh_degree=0, campos=torch.zeros(3),
                 prefiltered=False, debug=False)
     assert rasterizer._quick_layout(GaussianRasterizationSettings(**base)) == _lib.LSR_LAYOUT_CHW
+    # the default (None): pixel-major for a quick render whose inputs fit its kernel, else channel-major
+    assert rasterizer._quick_layout(GaussianRasterizationSettings(**base, quick_render=True), True) == _lib.LSR_LAYOUT_HWC
+    assert rasterizer._quick_layout(GaussianRasterizationSettings(**base, quick_render=True), False) == _lib.LSR_LAYOUT_CHW
+    assert rasterizer._quick_layout(GaussianRasterizationSettings(**base), True) == _lib.LSR_LAYOUT_CHW
+    assert rasterizer._quick_layout(GaussianRasterizationSettings(**base, quick_render=True,
+                                                                  language_feature_layout="chw"), True) == _lib.LSR_LAYOUT_CHW
     assert rasterizer._quick_layout(GaussianRasterizationSettings(**base, quick_render=True,
                                                                   language_feature_layout="hwc")) == _lib.LSR_LAYOUT_HWC
     with pytest.raises(ValueError, match="quick_render map only"):
@@ -52,7 +59,7 @@ def _render_quick(case, gpu, layout):
 def test_hwc_map_equals_reference_layout_and_oracle(gpu, W, H):
     from oracle import oracle as O
     case = make_case(**dict(QUICK, W=W, H=H))
-    c0, m0, r0 = _render_quick(case, gpu, None)
+    c0, m0, r0 = _render_quick(case, gpu, "chw")
     c1, m1, r1 = _render_quick(case, gpu, "hwc")
     assert m0.is_contiguous() and m1.shape == m0.shape == (192, H, W)
     assert m1.stride() == (1, 192 * W, 192)
@@ -71,7 +78,7 @@ def test_hwc_decode_bit_exact_with_reference_layout(gpu):
     from langsplatv2_amd import quick
     from test_quick_decode import DEC_ATOL, ref_decode
     case = make_case(**QUICK)
-    _, m0, _ = _render_quick(case, gpu, None)
+    _, m0, _ = _render_quick(case, gpu, "chw")
     _, m1, _ = _render_quick(case, gpu, "hwc")
     cb = torch.randn(3, 64, 512, generator=torch.Generator().manual_seed(4)).to(gpu)
     for normalize in (False, True):
@@ -96,10 +103,50 @@ def test_hwc_decode_synthetic_ragged(gpu):
 
 @pytest.mark.gpu
 def test_hwc_unsupported_shapes_raise(gpu):
-    """The pixel-major map is written by the 12-code, 192-channel kernel only."""
+    """The pixel-major map is written by the 12-code, 192-channel kernel only:
+    asked for explicitly on other inputs it raises, and the default falls back
+    to the reference's contiguous map."""
     case = make_case(**dict(QUICK, quick_k=2))   # 3 levels x top-2 = 6 codes
     with pytest.raises(RuntimeError):
         _render_quick(case, gpu, "hwc")
+    _, m_def, _ = _render_quick(case, gpu, None)
+    _, m_chw, _ = _render_quick(case, gpu, "chw")
+    assert m_def.is_contiguous() and torch.equal(m_def, m_chw)
+
+
+def _consumers(m, cb, H, W):
+    """The reference's consumer patterns of the quick weight map, verbatim in shape:
+    eval_lerf.py:213-218 (eval_3d_ovs.py:279-283, eval_mip_nerf360.py:171-175,
+    demo_prompt.py:24-36 and backend_renderer.py / debug_renderer.py:19-33 are the
+    same .view + einsum + norm), and compute_final_feature_map's .view(D, -1) matmul
+    (scene/gaussian_model.py:545-550; layer / per-level slices :520-543)."""
+    out = {}
+    D, h, w = m.shape
+    wm = m.view(3, 64, h, w).view(3, 64, h * w)
+    f = torch.einsum("ldk,lkn->ldn", cb.permute(0, 2, 1), wm).view(3, 512, h, w)
+    out["einsum"] = f
+    out["einsum_norm"] = f / (f.norm(dim=1, keepdim=True) + 1e-10)
+    flat = m.view(D, -1)
+    out["final"] = (cb.reshape(-1, 512).T @ flat).view(512, h, w)
+    out["levels"] = torch.stack([cb[i].T @ flat[i * 64:(i + 1) * 64] for i in range(3)])
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,H", [(128, 96), (45, 37)])
+def test_default_layout_serves_every_reference_consumer(gpu, W, H):
+    """With default settings (no language_feature_layout) the quick map is the
+    pixel-major view, and every consumer pattern of the reference gives the
+    same result on it as on the reference's contiguous map."""
+    case = make_case(**dict(QUICK, W=W, H=H))
+    _, m_def, _ = _render_quick(case, gpu, None)
+    _, m_chw, _ = _render_quick(case, gpu, "chw")
+    assert m_def.stride() == (1, 192 * W, 192) and m_chw.is_contiguous()
+    assert torch.equal(m_def, m_chw)
+    cb = torch.randn(3, 64, 512, generator=torch.Generator().manual_seed(11)).to(gpu)
+    a, b = _consumers(m_def, cb, H, W), _consumers(m_chw, cb, H, W)
+    for k in a:
+        torch.testing.assert_close(a[k], b[k], rtol=1e-5, atol=1e-5, msg=k)
 
 
 @pytest.mark.gpu

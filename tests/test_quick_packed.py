@@ -81,7 +81,7 @@ def _render(case, gpu, layout=None, qi=None, packed=True, w=None):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("layout", [None, "hwc"])
+@pytest.mark.parametrize("layout", ["chw", None])
 @pytest.mark.parametrize("W,H", [(128, 96), (45, 37)])
 def test_packed_render_equals_index_render(gpu, layout, W, H):
     from langsplatv2_amd import rasterizer
@@ -114,6 +114,29 @@ def test_packed_rows_follow_in_place_changes(gpu):
     _, m0, _ = _render(case, gpu, None, qi, packed=False)
     assert torch.equal(m1, m0) and not torch.equal(m1, m_again)
     assert len(rasterizer._PACKED) <= rasterizer._PACKED_MAX
+
+
+@pytest.mark.gpu
+def test_packed_cache_holds_no_indices_tensor(gpu):
+    """a cache entry references its indices tensor weakly, so a tensor
+    the caller drops is freed (and its packed rows can never be reused for
+    another tensor that lands in the same storage)."""
+    import gc
+    import weakref
+    from langsplatv2_amd import rasterizer
+    case = make_case(**QUICK)
+    qi = case["g"]["language_feature_indices"].to(gpu).clone()
+    rasterizer._PACKED.clear()
+    _render(case, gpu, None, qi)
+    w = weakref.ref(qi)
+    del qi
+    gc.collect()
+    assert w() is None
+    assert len(rasterizer._PACKED) == 1 and next(iter(rasterizer._PACKED.values()))[0]() is None
+    qi2 = case["g"]["language_feature_indices"].to(gpu).clone()
+    _, m2, _ = _render(case, gpu, None, qi2)
+    _, m0, _ = _render(case, gpu, None, qi2, packed=False)
+    assert torch.equal(m2, m0)
 
 
 @pytest.mark.gpu

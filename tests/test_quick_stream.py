@@ -27,7 +27,7 @@ def _renderer(case, gpu, layout):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("layout", [None, "hwc"])
+@pytest.mark.parametrize("layout", ["chw", None])
 def test_stream_equals_view_by_view(gpu, layout):
     from langsplatv2_amd import quick
     renders = [_renderer(make_case(**dict(QUICK, yaw=y)), gpu, layout) for y in (0.0, 6.0, -9.0, 3.0)]

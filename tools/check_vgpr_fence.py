@@ -23,13 +23,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LLVM = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 HI = re.compile(r"\bv(\d+)\b|\bv\[(\d+):(\d+)\]")
 
-# the inline-asm forms allowed to name v63 and above (render.hip)
+# the inline-asm forms allowed to name v63 and above (render.hip); each form also
+# pins which operands may be high: addresses and offsets below v63, data only in
+# the channel registers v64..v255 (a compiler-made store with a spilled address
+# or data in the fence, the overrun this tool exists to catch, is rejected)
 ALLOWED = [
     re.compile(r"^v_fma_f32 v63, v(\d+), v(\d+), v63$"),                 # LSR_QV_WORD (index mode)
     re.compile(r"^v_mov_b32(_e32)? v63, 0$"),                             # accumulator zeroing (index mode)
     re.compile(r"^v_mov_b32(_e32)? v(\d+), v64$"),                        # index-mode read (epilogue loop)
-    re.compile(r"^global_store_dwordx4 v\[\d+:\d+\], v\[(\d+):(\d+)\], off( offset:\d+)?$"),   # LSR_QHWC
-    re.compile(r"^buffer_store_dword v(\d+), v\d+, s\[\d+:\d+\], s\d+ offen$"),               # LSR_QEPI
+    re.compile(r"^global_store_dwordx4 v\[(\d+):(\d+)\], v\[(\d+):(\d+)\], off( offset:\d+)?$"),   # LSR_QHWC
+    re.compile(r"^buffer_store_dword v(\d+), v(\d+), s\[\d+:\d+\], s\d+ offen$"),                   # LSR_QEPI
 ]
 
 
@@ -44,15 +47,21 @@ def _regs(text):
 
 
 def _allowed(ins):
-    for p in ALLOWED:
+    for k, p in enumerate(ALLOWED):
         m = p.match(ins)
         if not m:
             continue
-        if p is ALLOWED[0]:
+        if k == 0:
             return int(m.group(1)) < 63 and int(m.group(2)) < 63
-        if p is ALLOWED[2]:
+        if k == 1:
+            return True
+        if k == 2:
             return int(m.group(2)) < 63
-        return True
+        if k == 3:   # address pair below v63, data a 4-aligned quad inside v64..v255
+            a0, a1, d0, d1 = (int(m.group(i)) for i in range(1, 5))
+            return a1 == a0 + 1 and a1 < 63 and d0 >= 64 and d0 % 4 == 0 and d1 == d0 + 3 and d1 <= 255
+        if k == 4:   # data one channel register, offset register below v63
+            return 64 <= int(m.group(1)) <= 255 and int(m.group(2)) < 63
     return False
 
 
