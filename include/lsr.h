@@ -42,7 +42,8 @@
 extern "C" {
 #endif
 
-#define LSR_ABI_VERSION 11  /* 11 (r05): LSR_INDEX_PACKED, lsr_quick_pack_codes, LSR_OPT_SPLIT_PREPROCESS;
+#define LSR_ABI_VERSION 12  /* 12 (r06): LSR_OPT_DETERMINISTIC;
+                               11 (r05): LSR_INDEX_PACKED, lsr_quick_pack_codes, LSR_OPT_SPLIT_PREPROCESS;
                                10 (r05): lsr_settings.quick_layout, lsr_quick_decode_run weight_layout;
                                9 (r05): LSR_OPT_LISTS_MAX_MB; LSR_BIN_ORDERED removed */
 
@@ -119,7 +120,7 @@ typedef struct lsr_inputs {
 typedef void* (*lsr_alloc_fn)(void* ctx, size_t bytes, int which);
 enum { LSR_BUF_GEOM = 0, LSR_BUF_BINNING = 1, LSR_BUF_IMAGE = 2, LSR_BUF_GRAD = 3, LSR_BUF_DECODE = 4,
        LSR_BUF_KNN = 5, LSR_BUF_LOSS = 6, LSR_BUF_GUARD = 7, LSR_BUF_SPARSE = 8, LSR_BUF_GRAD_LANG = 9,
-       LSR_BUF_LISTS = 10 };
+       LSR_BUF_LISTS = 10, LSR_BUF_DET = 11 /* LSR_OPT_DETERMINISTIC: bounds + fixed-point accumulators */ };
 
 typedef struct lsr_fwd_out {
     float* out_color;     /* (3,H,W)  caller-allocated */
@@ -346,6 +347,19 @@ int lsr_abi_version(void);
  * binning needs stays on the caller's stream, and the render waits for both);
  * 0: one fused preprocess kernel on the caller's stream.  Results identical. */
 #define LSR_OPT_SPLIT_PREPROCESS 3
+/* LSR_OPT_DETERMINISTIC (default 0): 1 makes lsr_backward bit-reproducible.
+ * The render backward's cross-block sums (every per-Gaussian gradient is a sum
+ * of per-8x8-block partials, added by atomics in whatever order the blocks
+ * finish) are accumulated as 64-bit fixed-point integers, whose addition is
+ * associative: one binary exponent per (Gaussian, gradient column) chosen from
+ * an a-priori bound (the launch's max |dL/dout| and max |feature|, the
+ * Gaussian's radius, the image size), so the sum cannot overflow, and each
+ * block partial is rounded once to 2^-s (s is 30-60 bits below the bound).
+ * Two backwards of the same inputs give identical bits.  A non-finite input or
+ * term turns every gradient of that call into NaN (never a silently wrong
+ * value).  Costs one bound pass, a zeroed 8-B-per-value accumulator, 64-bit
+ * atomics (twice the atomic bytes) and one conversion pass. */
+#define LSR_OPT_DETERMINISTIC 4
 #define LSR_BIN_AUTO 0
 #define LSR_BIN_SORTED_TILES 1
 #define LSR_BIN_ORDERED 2

@@ -18,7 +18,7 @@ LSR_EINVAL = 1
 LSR_ENONFINITE = 6
 LSR_ELISTS = 7
 LSR_BUF_GEOM, LSR_BUF_BINNING, LSR_BUF_IMAGE, LSR_BUF_GRAD, LSR_BUF_DECODE, LSR_BUF_KNN, LSR_BUF_LOSS = 0, 1, 2, 3, 4, 5, 6
-LSR_BUF_GUARD, LSR_BUF_SPARSE, LSR_BUF_GRAD_LANG, LSR_BUF_LISTS = 7, 8, 9, 10
+LSR_BUF_GUARD, LSR_BUF_SPARSE, LSR_BUF_GRAD_LANG, LSR_BUF_LISTS, LSR_BUF_DET = 7, 8, 9, 10, 11
 LSR_INDEX_F32, LSR_INDEX_I32, LSR_INDEX_I64, LSR_INDEX_PACKED = 0, 1, 2, 3
 LSR_GWS_GEOM, LSR_GWS_LANG = 1, 2
 LSR_LAYOUT_CHW, LSR_LAYOUT_HWC = 0, 1
@@ -266,6 +266,37 @@ def set_split_preprocess(on: bool) -> bool:
     check(lib.lsr_get_option(LSR_OPT_SPLIT_PREPROCESS, ctypes.byref(prev)), "lsr_get_option")
     check(lib.lsr_set_option(LSR_OPT_SPLIT_PREPROCESS, 1 if on else 0), "lsr_set_option")
     return bool(prev.value)
+
+
+LSR_OPT_DETERMINISTIC = 4
+
+
+def set_deterministic(on: bool) -> bool:
+    """Bit-reproducible backward (lsr_set_option LSR_OPT_DETERMINISTIC, default
+    off): the render backward's cross-block gradient sums in 64-bit fixed point
+    (include/lsr.h).  Returns the previous setting."""
+    lib = load()
+    prev = ctypes.c_int64(0)
+    check(lib.lsr_get_option(LSR_OPT_DETERMINISTIC, ctypes.byref(prev)), "lsr_get_option")
+    check(lib.lsr_set_option(LSR_OPT_DETERMINISTIC, 1 if on else 0), "lsr_set_option")
+    return bool(prev.value)
+
+
+class deterministic:
+    """Context manager: `with deterministic(): loss.backward()` (restores the
+    previous setting on exit; process-wide, like torch.use_deterministic_algorithms)."""
+
+    def __init__(self, on: bool = True):
+        self.on = on
+        self.prev = None
+
+    def __enter__(self):
+        self.prev = set_deterministic(self.on)
+        return self
+
+    def __exit__(self, *exc):
+        set_deterministic(self.prev)
+        return False
 
 
 def nonblocking_stream(device) -> "torch.cuda.ExternalStream":

@@ -53,9 +53,10 @@ struct Status {
 // when enabled, each stage is bracketed by two events recorded on the
 // caller's stream; lsr_profile_query sums their elapsed times.
 enum Stage { ST_PRE, ST_SCAN, ST_DUP, ST_SCAN_T, ST_SCATTER, ST_SORT, ST_RENDER, ST_GZERO, ST_RENDER_BWD,
-             ST_PRE_BWD, ST_N };
+             ST_PRE_BWD, ST_DET_BOUNDS, ST_DET_FINISH, ST_N };
 const char* kStageNames[ST_N] = {"preprocess", "scan_tiles", "bin_count", "scan_tile_counts", "bin_scatter",
-                                 "tile_sort", "render_fwd", "grad_zero", "render_bwd", "preprocess_bwd"};
+                                 "tile_sort", "render_fwd", "grad_zero", "render_bwd", "preprocess_bwd",
+                                 "det_bounds", "det_finish"};
 
 // Process-wide (the autograd engine runs backward on its own thread, and the
 // caller enables timing on its thread), thread-safe: the switch and mask are
@@ -507,6 +508,9 @@ static std::atomic<int64_t> g_lists_max_mb{2048};
 // LSR_OPT_SPLIT_PREPROCESS: the SH colour pass on a second stream, concurrent
 // with the binning (preprocess.hip k_preprocess_colour).
 static std::atomic<int64_t> g_split_pre{1};
+// LSR_OPT_DETERMINISTIC: the render backward's cross-block sums as 64-bit
+// fixed-point atomics (render.hip det_shift), converted back by k_det_finish
+static std::atomic<int64_t> g_det{0};
 #ifndef LSR_SPLIT_MIN_P
 #define LSR_SPLIT_MIN_P (1 << 19)
 #endif
@@ -533,6 +537,10 @@ int lsr_set_option(int option, int64_t value)
             if (value != 0 && value != 1) return LSR_EINVAL;
             g_split_pre.store(value, std::memory_order_relaxed);
             return LSR_OK;
+        case LSR_OPT_DETERMINISTIC:
+            if (value != 0 && value != 1) return LSR_EINVAL;
+            g_det.store(value, std::memory_order_relaxed);
+            return LSR_OK;
         default:
             return LSR_EINVAL;
     }
@@ -545,6 +553,7 @@ int lsr_get_option(int option, int64_t* value)
         case LSR_OPT_BIN_MODE: *value = g_bin_mode.load(std::memory_order_relaxed); return LSR_OK;
         case LSR_OPT_LISTS_MAX_MB: *value = g_lists_max_mb.load(std::memory_order_relaxed); return LSR_OK;
         case LSR_OPT_SPLIT_PREPROCESS: *value = g_split_pre.load(std::memory_order_relaxed); return LSR_OK;
+        case LSR_OPT_DETERMINISTIC: *value = g_det.load(std::memory_order_relaxed); return LSR_OK;
         default: return LSR_EINVAL;
     }
 }
@@ -1057,7 +1066,9 @@ static int backward_quick(const lsr_settings* s, const lsr_inputs* in, const lsr
         LSR_HIP(hipMemsetAsync(dw, 0, (size_t)P * in->quick_k * 4, st));
         return record_lang_ready(out, st);
     }
-    if (dw && !geom) {
+    // (deterministic mode: the expansion path below, whose dense language-only
+    // backward sums in fixed point; the sparse gather adds floats in any order)
+    if (dw && !geom && !g_det.load(std::memory_order_relaxed)) {
         if (lang_set_for(Dq) < 0) return LSR_EUNSUPPORTED;
         const Cam c = make_cam(s);
         RenderBwdArgs rb;
@@ -1151,6 +1162,29 @@ int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* 
     return backward_dense(s, in, b, out, alloc, ctx, st, guard);
 }
 
+// LSR_OPT_DETERMINISTIC: the bounds word ({max |dL/dout|, max |feature|,
+// flags}) and the zeroed 64-bit fixed-point twins of the accumulators the
+// render backward adds into (rb.grad_acc's (P, VP) rows, and with lang_direct
+// the (P, D) language rows); rb.radii must be set.
+static int det_prepare(RenderBwdArgs& rb, bool lang_direct, lsr_alloc_fn alloc, void* ctx, hipStream_t st)
+{
+    const size_t P = (size_t)rb.f.P;
+    const size_t rows = align256(P * (size_t)rb.VP * 8);
+    const size_t lang = lang_direct ? align256(P * (size_t)rb.f.D * 8) : 0;
+    uint8_t* ws = (uint8_t*)alloc(ctx, 256 + rows + lang, LSR_BUF_DET);
+    if (!ws) return LSR_ENOMEM;
+    rb.det_bounds = (float*)ws;
+    rb.det_rows = (long long*)(ws + 256);
+    rb.det_lang = lang_direct ? (long long*)(ws + 256 + rows) : nullptr;
+    {
+        StageScope sc(ST_GZERO, st);
+        LSR_HIP(hipMemsetAsync(ws, 0, 256 + rows + lang, st));
+    }
+    StageScope sc(ST_DET_BOUNDS, st);
+    LSR_HIP(launch_det_bounds(rb, rb.det_bounds, st));
+    return LSR_OK;
+}
+
 // The dense-input backward (lsr_backward's body past validation; also the
 // geometry path of the quick input, with that call's guard).
 static int backward_dense(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* b, lsr_bwd_out* out,
@@ -1171,6 +1205,7 @@ static int backward_dense(const lsr_settings* s, const lsr_inputs* in, const lsr
     const bool ws_kind = W.kind != 0 && b->grad_ws_kind == W.kind;
     const bool ws_ok = ws_kind && W.rows_bytes > 0 && b->grad_ws && b->grad_ws_bytes >= W.rows_bytes;
     const bool ws_lang = ws_kind && W.lang_bytes > 0 && b->grad_ws_lang && out->dL_dlang == (float*)b->grad_ws_lang;
+    const bool det = g_det.load(std::memory_order_relaxed) != 0;
     if (lang_only) {
         RenderBwdArgs rb;
         rb.f = make_render_args(s, in, c, (const uint8_t*)b->geom, (const uint8_t*)b->binning,
@@ -1183,8 +1218,15 @@ static int backward_dense(const lsr_settings* s, const lsr_inputs* in, const lsr
         rb.dout_lang = b->dL_dout_lang;
         rb.grad_acc = out->dL_dlang;
         rb.VP = Dd;
-        if (!ws_lang) { StageScope sc(ST_GZERO, st); LSR_HIP(hipMemsetAsync(out->dL_dlang, 0, (size_t)P * Dd * 4, st)); }
+        if (det) {
+            rc = det_prepare(rb, false, alloc, ctx, st);
+            if (rc != LSR_OK) return rc;
+        } else if (!ws_lang) {
+            StageScope sc(ST_GZERO, st);
+            LSR_HIP(hipMemsetAsync(out->dL_dlang, 0, (size_t)P * Dd * 4, st));
+        }
         { StageScope sc(ST_RENDER_BWD, st); LSR_HIP(launch_render_bwd_lang(rb, st)); }
+        if (det) { StageScope sc(ST_DET_FINISH, st); LSR_HIP(launch_det_finish(rb, true, nullptr, out->dL_dlang, st)); }
         LSR_DEBUG_SYNC(s, st, "render_bwd_lang");
         rc = record_lang_ready(out, st);
         if (rc != LSR_OK) return rc;
@@ -1199,7 +1241,8 @@ static int backward_dense(const lsr_settings* s, const lsr_inputs* in, const lsr
     const int VP = lang_direct ? 16 : grad_row_width(Dd);
     float* gacc = ws_ok ? (float*)b->grad_ws : (float*)alloc(ctx, (size_t)P * VP * 4, LSR_BUF_GRAD);
     if (!gacc) return LSR_ENOMEM;
-    if (!ws_ok || (lang_direct && !ws_lang)) {
+    // (deterministic: k_det_finish writes every element of gacc and dL/dlang)
+    if (!det && (!ws_ok || (lang_direct && !ws_lang))) {
         StageScope sc(ST_GZERO, st);
         if (!ws_ok) LSR_HIP(hipMemsetAsync(gacc, 0, (size_t)P * VP * 4, st));
         if (lang_direct && !ws_lang) LSR_HIP(hipMemsetAsync(out->dL_dlang, 0, (size_t)P * Dd * 4, st));
@@ -1217,7 +1260,15 @@ static int backward_dense(const lsr_settings* s, const lsr_inputs* in, const lsr
     rb.grad_acc = gacc;
     rb.VP = VP;
     rb.lang_acc = lang_direct ? out->dL_dlang : nullptr;
+    if (det) {
+        rc = det_prepare(rb, lang_direct, alloc, ctx, st);
+        if (rc != LSR_OK) return rc;
+    }
     { StageScope sc(ST_RENDER_BWD, st); LSR_HIP(launch_render_bwd(rb, st)); }
+    if (det) {
+        StageScope sc(ST_DET_FINISH, st);
+        LSR_HIP(launch_det_finish(rb, false, gacc, lang_direct ? out->dL_dlang : nullptr, st));
+    }
     LSR_DEBUG_SYNC(s, st, "render_bwd");
     // the language gradient is final here unless preprocess_bwd copies it out
     if (lang_direct || !out->dL_dlang) {

@@ -115,6 +115,14 @@ struct RenderBwdArgs {
     // the sparse input f.qw / f.qi, accumulated with the channel gradient
     // gathered at each Gaussian's codes (zeroed by the caller)
     float* qw_acc = nullptr;
+    // LSR_OPT_DETERMINISTIC: the atomics add 64-bit fixed-point twins of grad_acc
+    // (det_rows, same (P, VP) indexing) and lang_acc (det_lang, (P, D)), each value
+    // scaled by 2^det_shift(...) (render.hip); det_bounds = {max |dL/dout|,
+    // max |feature|, flag bits} from launch_det_bounds, radii the forward's
+    long long* det_rows = nullptr;
+    long long* det_lang = nullptr;
+    float* det_bounds = nullptr;
+    const int32_t* radii = nullptr;
 };
 bool bwd_lang_direct(int D);  // D for which the full backward supports lang_acc
 int grad_row_width(int D);   // VP for a dense language dim
@@ -126,6 +134,16 @@ hipError_t launch_render_bwd_lang(const RenderBwdArgs& a, hipStream_t st);
 // the Dq-channel gradient (Dq must be a compiled channel set, <= 64)
 hipError_t launch_render_bwd_lang_sparse(const RenderBwdArgs& a, hipStream_t st);
 int lang_set_for(int D);     // compiled channel set >= D, or -1
+// LSR_OPT_DETERMINISTIC: bounds = {max |dL/dout| over the 3 + D planes,
+// max |feature| over the visible Gaussians' colours and dense language rows,
+// flag} (bounds zeroed by the caller; flag bit 0: a non-finite value)
+hipError_t launch_det_bounds(const RenderBwdArgs& b, float* bounds, hipStream_t st);
+// the fixed-point sums back to fp32: rows (P, VP) -> grad_out (every element
+// written; VP = 16 with lang_direct), lang (P, D) -> lang_out; lang_only: rows
+// is the (P, D) language accumulator and lang_out its output.  A flagged
+// bounds word writes NaN everywhere.
+hipError_t launch_det_finish(const RenderBwdArgs& b, bool lang_only, float* grad_out, float* lang_out,
+                             hipStream_t st);
 
 // quick.hip
 hipError_t launch_topk_code_fwd(const float* logits, int64_t N, int L, int K, int k, float* dense, float* sw,

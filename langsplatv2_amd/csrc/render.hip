@@ -51,6 +51,13 @@ __device__ __forceinline__ int wave_max_i(int v)
     return v;
 }
 
+__device__ __forceinline__ float wave_max_f(float v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = fmaxf(v, __shfl_xor(v, d, 64));
+    return v;
+}
+
 // ---------------------------------------------------------- forward -------
 // Lane -> pixel mapping: wave w of the tile owns the 8x8 block
 // (w & 1, w >> 1); lane l owns pixel (l & 7, l >> 3) of it.
@@ -1500,8 +1507,8 @@ struct WaveStageL {
 };
 // waves per SIMD the MFMA backward is compiled for: 4 for the list-driven
 // D = 16 kernel (the headline's), the launch-bounds floor otherwise
-template <int NL, bool LD, bool LST>
-constexpr int bwd_waves() { return (LST && LD && NL == 16) ? 4 : LSR_MF_WAVES; }
+template <int NL, bool LD, bool LST, bool DET = false>
+constexpr int bwd_waves() { return (LST && LD && NL == 16 && !DET) ? 4 : LSR_MF_WAVES; }
 
 // LDS-DMA of one 16-B row part per lane: lane l's bytes land at lds + 16 l (an
 // LDS-DMA writes wave-uniform M0 + lane x size).  Inline asm with M0 saved and
@@ -1617,6 +1624,53 @@ __device__ __forceinline__ void dot_features(const RenderArgs& a, uint32_t gid, 
 }
 
 #define BWD_MFMA(a, b_, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b_), (c), 0, 0, 0)
+
+// ---------------------------------- deterministic backward (LSR_OPT_DETERMINISTIC)
+// Every per-Gaussian gradient is a sum over the 8x8 blocks the Gaussian is
+// staged in of a per-block partial (the block's 64 pixels summed in a fixed
+// order by its wave); only the order in which the blocks' atomics land varies.
+// DET adds the partials as 64-bit fixed-point integers instead (associative:
+// the same bits in any order).  The exponent of (Gaussian i, column class) is
+// chosen from an a-priori bound of the partials (64 pixels x the per-pixel
+// bound) and of how many blocks can contribute (the radius rect, nb =
+// (r/4 + 2)^2 blocks), so the sum cannot overflow:
+//   class 0 colour / language  aT |dL/dout|                        <= Dm
+//   class 1 opacity            G |dL/dalpha|                       <= Am
+//   class 2 mean2D (NDC)       0.5 W o G |conic d| |dL/dalpha|     <= 0.554 max(W,H) Am
+//                              (|conic| <= 1/0.3 from the 0.3 dilation; sup sqrt(q) e^(-q/2) = e^(-1/2))
+//   class 3 conic              0.5 o G |d|^2 |dL/dalpha|           <= 0.041 r^2 Am
+//                              (G |d|^2 <= (2/e) lambda_max(cov2D) <= (2/e) (r/3)^2)
+// with Dm = max |dL/dout| and Am = (2 C Fm + |bg|_1) Dm >= |dL/dalpha|
+// (|dot|, |S| <= C Fm Dm for Fm = max |feature|, T <= 1, T_final / (1 - alpha) <= T).
+// s = 61 - e(nb) - e(bound): every partial and every sum stays below 2^61 in
+// fixed units (frexp exponent e: x < 2^e); one rounding per partial, at 2^-s.
+__device__ __forceinline__ int det_class_of(int f)
+{
+    return f < 2 ? 2 : (f < 5 ? 3 : (f == 5 ? 1 : 0));
+}
+
+__device__ __forceinline__ int det_shift(int cls, int r, float Dm, float Am, float WH)
+{
+    const float rr = (float)max(r, 1);
+    const float q = fmaf(0.25f, rr, 2.f);
+    const float B = cls == 0 ? 64.f * Dm : (cls == 1 ? 64.f * Am : (cls == 2 ? 40.f * WH * Am : 3.f * rr * rr * Am));
+    int en = 0, eb = 0;
+    (void)frexpf(q * q, &en);
+    (void)frexpf(fmaxf(B, 1e-30f), &eb);
+    return min(max(61 - en - eb, -100), 100);
+}
+
+// adds v at 2^s; a value outside the bound (never, by the analysis above) or a
+// non-finite one flags the call instead (the conversion then writes NaN)
+__device__ __forceinline__ void det_add(long long* p, float v, int s, uint32_t* flag)
+{
+    const float x = ldexpf(v, s);
+    if (!(fabsf(x) < 0x1p61f)) {
+        atomicOr(flag, 1u);
+        return;
+    }
+    atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__float2ll_rn(x));
+}
 // LO (language only): the autograd call needs dL/dlanguage alone (feature-mode
 // training: geometry frozen, scene/gaussian_model.py:238-243, and means2D not
 // requiring grad).  Then dL/dlang[j][c] = sum_p aT[j][p] dL/dout[c][p] is all
@@ -1630,10 +1684,11 @@ __device__ __forceinline__ void dot_features(const RenderArgs& a, uint32_t gid, 
 // lcount) instead of being re-staged from the tile list: no ids -> records
 // gathers, no block tests, no compaction; the list chunks arrive by LDS-DMA one
 // chunk ahead.  The same candidates in the same order: results unchanged.
-template <int NL, bool LO = false, bool LD = false, bool SP = false, bool LST = false>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_waves<NL, LD, LST>()))) k_render_bwd_mf(RenderBwdArgs b)
+template <int NL, bool LO = false, bool LD = false, bool SP = false, bool LST = false, bool DET = false>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_waves<NL, LD, LST, DET>()))) k_render_bwd_mf(RenderBwdArgs b)
 {
     static_assert(!(LST && SP), "the sparse-input backward follows the quick forward (no lists)");
+    static_assert(!(DET && SP), "the deterministic backward expands the sparse input (lsr_api backward_quick)");
     static_assert(!LO || NL > 0, "language-only backward needs D > 0");
     static_assert(!SP || LO, "the sparse-input gradient is a language-only backward");
     static_assert(!LD || (!LO && NL % 16 == 0), "direct dL/dlang needs whole 16-channel lines");
@@ -1847,7 +1902,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_wav
         const uint32_t* SG;
         if constexpr (LST) {
             const int off = (c0 / CH & 1) * CH;
-            if (c0 == 0 || !buf_atom) wait_vmcnt<0>();
+            // (DET: conditional 64-bit atomics, so no count of them: drain)
+            if (c0 == 0 || !buf_atom || DET) wait_vmcnt<0>();
             else wait_vmcnt<CHUNK_OPS>();
             if (c0 + CH < cend) list_dma(c0 + CH, CH - off);
             n = nfull = min(CH, cend - c0);
@@ -2162,7 +2218,36 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_wav
                         else
                             vq[h][q] = sGr[slot_of(q) * GRS + 16 * h + li];
                     }
-                if (buf_atom) {
+                if constexpr (DET) {
+                    // fixed-point twins of the rows (det_shift above): the same
+                    // values, order-independent sums
+                    uint32_t* const dflag = reinterpret_cast<uint32_t*>(b.det_bounds + 2);
+                    const float dDm = b.det_bounds[0];
+                    const float dAm = (2.f * (float)(3 + D) * b.det_bounds[1] + (fabsf(c.bg[0]) + fabsf(c.bg[1]) + fabsf(c.bg[2]))) * dDm;
+                    const float dWH = (float)max(c.W, c.H);
+                    int rq[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) rq[q] = slot_of(q) < kn ? b.radii[gq[q]] : 1;
+#pragma unroll
+                    for (int h = 0; h < GRL; h++) {
+                        const int f = 16 * h + li;
+                        const bool fcol = LO ? (f < D)
+                                          : LD ? (h == 0 ? (f < 9) : (f - 16 < D))
+                                               : ((f < 9) | ((f >= LSR_GROW_LANG) & (f < LSR_GROW_LANG + D)));
+                        const int cls = LO ? 0 : ((LD && h > 0) ? 0 : det_class_of(f));
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const float v = vq[h][q];
+                            if (fcol & (slot_of(q) < kn) & (v != 0.f)) {
+                                const int sh = det_shift(cls, rq[q], dDm, dAm, dWH);
+                                if (LD && h > 0)
+                                    det_add(b.det_lang + (size_t)gq[q] * D + (f - 16), v, sh, dflag);
+                                else
+                                    det_add(b.det_rows + (size_t)gq[q] * VP + f, v, sh, dflag);
+                            }
+                        }
+                    }
+                } else if (buf_atom) {
                     // buffer atomics: 32-bit offsets, and a lane with nothing
                     // to add gets an offset past the buffer (the range check
                     // drops it: tools/micro/buf_oob_atomic.hip) instead of an
@@ -2228,9 +2313,12 @@ hipError_t launch_render_bwd_lang(const RenderBwdArgs& b, hipStream_t st)
 {
     const int T = b.f.cam.gx * b.f.cam.gy;
     if (T == 0) return hipSuccess;
-    // LST: the forward's per-block candidate lists (RenderArgs::listA)
-#define LSR_BWD_LO(NL) (b.f.listA ? k_render_bwd_mf<NL, true, false, false, true><<<4 * T, 64, 0, st>>>(b) \
-                                   : k_render_bwd_mf<NL, true><<<4 * T, 64, 0, st>>>(b))
+    // LST: the forward's per-block candidate lists (RenderArgs::listA); DET: fixed-point sums
+#define LSR_BWD_LO(NL)                                                                                           \
+    (b.det_rows ? (b.f.listA ? k_render_bwd_mf<NL, true, false, false, true, true><<<4 * T, 64, 0, st>>>(b)     \
+                             : k_render_bwd_mf<NL, true, false, false, false, true><<<4 * T, 64, 0, st>>>(b))   \
+                : (b.f.listA ? k_render_bwd_mf<NL, true, false, false, true><<<4 * T, 64, 0, st>>>(b)           \
+                             : k_render_bwd_mf<NL, true><<<4 * T, 64, 0, st>>>(b)))
     switch (lang_set_for(b.f.D)) {
         case 4: LSR_BWD_LO(4); break;
         case 8: LSR_BWD_LO(8); break;
@@ -2271,19 +2359,31 @@ hipError_t launch_render_bwd(const RenderBwdArgs& b, hipStream_t st)
     if (T == 0) return hipSuccess;
     // LST: the forward's per-block candidate lists (RenderArgs::listA)
     const bool lst = b.f.listA != nullptr;
+    const bool det = b.det_rows != nullptr;
+    if (det && (!b.det_bounds || !b.radii || ((b.lang_acc != nullptr) != (b.det_lang != nullptr))))
+        return hipErrorInvalidValue;
     if (b.lang_acc) {
         if (!bwd_lang_direct(b.f.D) || (uintptr_t)b.f.lang % 16 != 0) return hipErrorInvalidValue;
         if (b.f.D == 16) {
-            if (lst) k_render_bwd_mf<16, false, true, false, true><<<4 * T, 64, 0, st>>>(b);
+            if (det) {
+                if (lst) k_render_bwd_mf<16, false, true, false, true, true><<<4 * T, 64, 0, st>>>(b);
+                else k_render_bwd_mf<16, false, true, false, false, true><<<4 * T, 64, 0, st>>>(b);
+            } else if (lst) k_render_bwd_mf<16, false, true, false, true><<<4 * T, 64, 0, st>>>(b);
             else k_render_bwd_mf<16, false, true><<<4 * T, 64, 0, st>>>(b);
         } else {
-            if (lst) k_render_bwd_mf<32, false, true, false, true><<<4 * T, 64, 0, st>>>(b);
+            if (det) {
+                if (lst) k_render_bwd_mf<32, false, true, false, true, true><<<4 * T, 64, 0, st>>>(b);
+                else k_render_bwd_mf<32, false, true, false, false, true><<<4 * T, 64, 0, st>>>(b);
+            } else if (lst) k_render_bwd_mf<32, false, true, false, true><<<4 * T, 64, 0, st>>>(b);
             else k_render_bwd_mf<32, false, true><<<4 * T, 64, 0, st>>>(b);
         }
         return hipGetLastError();
     }
-#define LSR_BWD_FULL(NL) (lst ? k_render_bwd_mf<NL, false, false, false, true><<<4 * T, 64, 0, st>>>(b) \
-                              : k_render_bwd_mf<NL><<<4 * T, 64, 0, st>>>(b))
+#define LSR_BWD_FULL(NL)                                                                                 \
+    (det ? (lst ? k_render_bwd_mf<NL, false, false, false, true, true><<<4 * T, 64, 0, st>>>(b)          \
+                : k_render_bwd_mf<NL, false, false, false, false, true><<<4 * T, 64, 0, st>>>(b))        \
+         : (lst ? k_render_bwd_mf<NL, false, false, false, true><<<4 * T, 64, 0, st>>>(b)                \
+                : k_render_bwd_mf<NL><<<4 * T, 64, 0, st>>>(b)))
     switch (lang_set_for(b.f.D)) {
         case 0: LSR_BWD_FULL(0); break;
         case 4: LSR_BWD_FULL(4); break;
@@ -2297,5 +2397,120 @@ hipError_t launch_render_bwd(const RenderBwdArgs& b, hipStream_t st)
     return hipGetLastError();
 }
 
-}  // namespace lsr
 
+// ------------------------------------------ deterministic backward: bounds
+// max |dL/dout| over the 3 + D upstream planes and max |feature| over the
+// visible Gaussians' colours and dense language rows (order-independent:
+// atomicMax on the bits of non-negative floats); bit 0 of word 2 flags a
+// non-finite value
+__global__ void __launch_bounds__(256) k_det_bounds(const float* __restrict__ dc, const float* __restrict__ dl,
+                                                    size_t HW, int D, const float* __restrict__ rgb,
+                                                    const float* __restrict__ lang, const int32_t* __restrict__ radii,
+                                                    int P, float* bounds)
+{
+    float md = 0.f, mf = 0.f;
+    bool bad = false;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t nd = HW * (size_t)(3 + D);
+    for (size_t e = t0; e < nd; e += stride) {
+        const float v = e < 3 * HW ? dc[e] : dl[e - 3 * HW];
+        bad |= !isfinite(v);
+        md = fmaxf(md, fabsf(v));
+    }
+    const int C = 3 + D;
+    const size_t nf = (size_t)P * (size_t)C;
+    for (size_t e = t0; e < nf; e += stride) {
+        const size_t i = e / (size_t)C;
+        const int ch = (int)(e - i * (size_t)C);
+        if (radii[i] <= 0) continue;
+        const float v = ch < 3 ? rgb[3 * i + ch] : lang[i * (size_t)D + (ch - 3)];
+        bad |= !isfinite(v);
+        mf = fmaxf(mf, fabsf(v));
+    }
+    md = wave_max_f(md);
+    mf = wave_max_f(mf);
+    const bool wbad = wave_ballot(bad) != 0u;
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(reinterpret_cast<unsigned int*>(bounds), __float_as_uint(md));
+        atomicMax(reinterpret_cast<unsigned int*>(bounds + 1), __float_as_uint(mf));
+        if (wbad) atomicOr(reinterpret_cast<unsigned int*>(bounds + 2), 1u);
+    }
+}
+
+hipError_t launch_det_bounds(const RenderBwdArgs& b, float* bounds, hipStream_t st)
+{
+    const size_t HW = (size_t)b.f.cam.W * b.f.cam.H;
+    const int D = b.f.D;
+    if (D > 0 && (!b.dout_lang || !b.f.lang)) return hipErrorInvalidValue;
+    const size_t n = HW * (size_t)(3 + D) > (size_t)b.f.P * (size_t)(3 + D) ? HW * (size_t)(3 + D)
+                                                                            : (size_t)b.f.P * (size_t)(3 + D);
+    const unsigned nb = (unsigned)std::min<size_t>((n + 255) / 256, 4096);
+    if (nb == 0) return hipSuccess;
+    k_det_bounds<<<nb, 256, 0, st>>>(b.dout_color, b.dout_lang, HW, D, b.f.rgb, b.f.lang, b.radii, b.f.P, bounds);
+    return hipGetLastError();
+}
+
+// ---------------------------------------- deterministic backward: to fp32
+// mode 0: rows (P, VP) generic layout ([0..8] geometry + colour, [12, 12 + D)
+// language) -> gout; mode 1 (lang_direct): rows (P, 16) -> gout, lang (P, D)
+// -> lout; mode 2 (language only): rows (P, D) -> lout.  Every element of the
+// outputs is written (unused row slots 0).
+__global__ void __launch_bounds__(256) k_det_finish(const long long* __restrict__ rows,
+                                                    const long long* __restrict__ lang,
+                                                    const int32_t* __restrict__ radii,
+                                                    const float* __restrict__ bounds, int P, int VP, int D, int mode,
+                                                    const float* __restrict__ bg, float WH, float* __restrict__ gout,
+                                                    float* __restrict__ lout)
+{
+    const int ncols = mode == 2 ? D : VP + (mode == 1 ? D : 0);
+    const size_t n = (size_t)P * (size_t)ncols;
+    const float Dm = bounds[0];
+    // the render backward's Am, the same expression (the exponents must agree bit for bit)
+    const float Am = (2.f * (float)(3 + D) * bounds[1] + (fabsf(bg[0]) + fabsf(bg[1]) + fabsf(bg[2]))) * Dm;
+    const bool bad = (__float_as_uint(bounds[2]) & 1u) != 0u;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+        const size_t i = e / (size_t)ncols;
+        const int col = (int)(e - i * (size_t)ncols);
+        const int r = radii[i];
+        long long acc = 0;
+        int cls = 0;
+        bool used = true;
+        float* dst;
+        if (mode == 2) {
+            acc = rows[i * (size_t)D + col];
+            dst = lout + i * (size_t)D + col;
+        } else if (col < VP) {
+            used = col < 9 || (mode == 0 && col >= LSR_GROW_LANG && col < LSR_GROW_LANG + D);
+            cls = det_class_of(col);
+            acc = used ? rows[i * (size_t)VP + col] : 0;
+            dst = gout + i * (size_t)VP + col;
+        } else {
+            const int k = col - VP;
+            acc = lang[i * (size_t)D + k];
+            dst = lout + i * (size_t)D + k;
+        }
+        float v = 0.f;
+        if (acc != 0) v = (float)ldexp((double)acc, -det_shift(cls, r, Dm, Am, WH));
+        *dst = bad ? __builtin_nanf("") : v;
+    }
+}
+
+hipError_t launch_det_finish(const RenderBwdArgs& b, bool lang_only, float* grad_out, float* lang_out, hipStream_t st)
+{
+    const int P = b.f.P, D = b.f.D;
+    const int mode = lang_only ? 2 : (b.det_lang ? 1 : 0);
+    if (!b.det_rows || !b.det_bounds || !b.radii || (mode == 0 && !grad_out) || (mode != 0 && !lang_out) ||
+        (mode == 1 && !grad_out))
+        return hipErrorInvalidValue;
+    const size_t ncols = mode == 2 ? (size_t)D : (size_t)b.VP + (mode == 1 ? (size_t)D : 0);
+    const size_t n = (size_t)P * ncols;
+    if (n == 0) return hipSuccess;
+    const Cam& c = b.f.cam;
+    const unsigned nb = (unsigned)std::min<size_t>((n + 255) / 256, 8192);
+    k_det_finish<<<nb, 256, 0, st>>>(b.det_rows, b.det_lang, b.radii, b.det_bounds, P, b.VP, D, mode, c.bg,
+                                     (float)std::max(c.W, c.H), grad_out, lang_out);
+    return hipGetLastError();
+}
+}  // namespace lsr

@@ -746,6 +746,163 @@ void lso_render_bwd(const lso_settings* s, const lso_inputs* in, const lso_geom*
     free(tiles);
 }
 
+/* ------------------------------------------- render bwd: error bounds -- */
+/* A-priori bound of |GPU - oracle| for every render-gradient element, for the
+ * product's deterministic backward (include/lsr.h LSR_OPT_DETERMINISTIC), by a
+ * running forward-error analysis of both evaluations of Appendix A.4 along the
+ * oracle's own traversal.  Units: u = 2^-24 (fp32 unit roundoff); the result is
+ * u x (sum over the element's per-pixel terms of their error bounds).
+ *
+ * Per contributing pair, back to front at one pixel:
+ *   G:      the power is the same fp32 bits on both sides (the forward is
+ *           bit-exact); GPU 2^(power log2e) (product u|power|, v_exp_f32 2u),
+ *           oracle lso_expf (2u), |power| <= ln 255 for a contributing pair
+ *           => |dG|/G <= 10u; alpha = min(0.99, o G): |dalpha|/alpha <= 12u.
+ *   T:      T <- T / (1 - alpha) from the bit-identical final T; d(1-alpha) =
+ *           dalpha, so each step adds 12u alpha/(1-alpha) plus 4u (GPU rcp +
+ *           mul, oracle divide): eT.
+ *   aT:     eT + 14u; colour / language term aT dL/dout: + 2u.
+ *   dot:    sum over C = 3 + D channels (GPU MFMA, oracle fmaf chain):
+ *           2 C u sum_c |f_c dL/dout_c|.
+ *   S:      S <- alpha dot + (1 - alpha) S with the errors above: eS
+ *           (absolute) carried like S itself.
+ *   dL/dalpha = (dot - S) T - T_final/(1-alpha) bg.dL/dout:
+ *           T (2 C u |f.dout| + eS) + |dot - S| T (eT + 2u)
+ *           + |bg term| (12u alpha/(1-alpha) + 4u) + 2u |dL/dalpha|.
+ *   opacity G dL/dalpha; mean2D / conic o G dL/dalpha x (dx, dy polynomial):
+ *           value error o |poly| (G e(dL/dalpha) + 12u G |dL/dalpha|).
+ *   GPU pixel sums: each 8x8 block's 64 terms summed in fp32 (MFMA K chain
+ *           or a 16-term VALU chain + 2 reduction levels, then the moment
+ *           combination): <= 72u sum |term|, where a geometry term's magnitude
+ *           is that of its factorised form, |u| (|X|+|lx|)^k (|Y|+|ly|)^m with
+ *           X = mean - block centre, lx = pixel - block centre (the product
+ *           sums u lx^k ly^m per block and combines with X, Y afterwards).
+ * Not included (added by the caller): the fixed-point rounding of each block
+ * partial (2^-(s+1), s from the product's det_shift) and the final fp32
+ * roundings of the two results (u |value| each); the oracle's fp64 sums are
+ * exact to 2^-53 relative. */
+static void render_tile_bwd_bound(const lso_settings* s, const lso_inputs* in, const lso_geom* g,
+                                  const uint32_t* point_list, const uint32_t* ranges, int tile,
+                                  const float* final_Ts, const uint32_t* n_contrib,
+                                  const float* dout_color, const float* dout_lang, dacc_t* A, int atomic)
+{
+    const int W = s->W, H = s->H;
+    const int gx = (W + TILE - 1) / TILE;
+    const int tx = tile % gx, ty = tile / gx;
+    const int D = s->include_feature ? in->D : 0;
+    const double C2 = 2.0 * (3 + D);
+    const uint32_t start = ranges[2 * tile];
+    const double hW = 0.5 * (double)W, hH = 0.5 * (double)H;
+    float* Gl = (float*)malloc(sizeof(float) * (size_t)(D > 0 ? D : 1));
+    for (int py = ty * TILE; py < ty * TILE + TILE && py < H; py++)
+        for (int px = tx * TILE; px < tx * TILE + TILE && px < W; px++) {
+            const size_t pix = (size_t)py * W + px;
+            const float pfx = (float)px, pfy = (float)py;
+            const double cx = (double)(px & ~7) + 3.5, cy = (double)(py & ~7) + 3.5;
+            const double alx = fabs((double)px - cx), aly = fabs((double)py - cy);
+            const float T_final = final_Ts[pix];
+            const uint32_t last = n_contrib[pix];
+            float Gc[3];
+            for (int ch = 0; ch < 3; ch++) Gc[ch] = dout_color[(size_t)ch * H * W + pix];
+            for (int k = 0; k < D; k++) Gl[k] = dout_lang[(size_t)k * H * W + pix];
+            const float bg_dot = s->bg[0] * Gc[0] + s->bg[1] * Gc[1] + s->bg[2] * Gc[2];
+            float T = T_final;
+            float last_alpha = 0.f, last_dot = 0.f, rec = 0.f;
+            double eT = 0.0, eS = 0.0, last_dabs = 0.0;
+            for (int64_t p = (int64_t)last - 1; p >= 0; p--) {
+                const uint32_t j = point_list[start + p];
+                const float* co = g->conic_opacity + 4 * j;
+                float dx = g->xy[2 * j] - pfx, dy = g->xy[2 * j + 1] - pfy;
+                float power = fmaf(-0.5f, fmaf(co[0] * dx, dx, (co[2] * dy) * dy), -((co[1] * dx) * dy));
+                if (power > 0.0f) continue;
+                float G = lso_expf(power);
+                float alpha = fminf(0.99f, co[3] * G);
+                if (alpha < 1.0f / 255.0f) continue;
+                T = T / (1.f - alpha);
+                const double ra = (double)alpha / (1.0 - (double)alpha);
+                eT += 12.0 * ra + 4.0;
+                const double aT = (double)alpha * (double)T;
+                float dot = g->rgb[3 * j] * Gc[0];
+                dot = fmaf(g->rgb[3 * j + 1], Gc[1], dot);
+                dot = fmaf(g->rgb[3 * j + 2], Gc[2], dot);
+                double dabs = fabs((double)g->rgb[3 * j] * Gc[0]) + fabs((double)g->rgb[3 * j + 1] * Gc[1]) +
+                              fabs((double)g->rgb[3 * j + 2] * Gc[2]);
+                const float* f = D ? in->lang + (size_t)j * in->D : NULL;
+                for (int k = 0; k < D; k++) {
+                    dot = fmaf(f[k], Gl[k], dot);
+                    dabs += fabs((double)f[k] * Gl[k]);
+                }
+                /* S absorbs the previous (nearer-the-back) pair, as the oracle's rec */
+                eS = 12.0 * last_alpha * (fabs((double)last_dot) + fabs((double)rec)) + last_alpha * C2 * last_dabs +
+                     (1.0 - last_alpha) * eS +
+                     3.0 * (last_alpha * fabs((double)last_dot) + (1.0 - last_alpha) * fabs((double)rec));
+                rec = fmaf(last_alpha, last_dot, (1.f - last_alpha) * rec);
+                float dL_dalpha = (dot - rec) * T;
+                const float bgt = -T_final / (1.f - alpha) * bg_dot;
+                dL_dalpha = fmaf(-T_final / (1.f - alpha), bg_dot, dL_dalpha);
+                const double EdLa = (double)T * (C2 * dabs + eS) + fabs((double)dot - rec) * T * (eT + 2.0) +
+                                    fabs((double)bgt) * (12.0 * ra + 4.0) + 2.0 * fabs((double)dL_dalpha);
+                last_alpha = alpha;
+                last_dot = dot;
+                last_dabs = dabs;
+                const double eaT = eT + 16.0 + 72.0;   /* + the product and the block sum */
+                for (int ch = 0; ch < 3; ch++) acc_add(&A->dcolor[3 * (size_t)j + ch], eaT * fabs(aT * Gc[ch]), atomic);
+                for (int k = 0; k < D; k++) acc_add(&A->dlang[(size_t)j * D + k], eaT * fabs(aT * Gl[k]), atomic);
+                const double o = co[3];
+                const double Ub = (double)G * fabs((double)dL_dalpha);
+                acc_add(&A->dopacity[j], (double)G * EdLa + (14.0 + 72.0) * Ub, atomic);
+                const double VE = o * ((double)G * EdLa + 12.0 * Ub);     /* per unit of the pair's polynomial */
+                const double adx = fabs((double)dx), ady = fabs((double)dy);
+                const double AX = fabs((double)g->xy[2 * j] - cx) + alx, AY = fabs((double)g->xy[2 * j + 1] - cy) + aly;
+                const double ca = fabs((double)co[0]), cb = fabs((double)co[1]), cc = fabs((double)co[2]);
+                acc_add(&A->dmean2D[3 * (size_t)j + 0], hW * (VE * (ca * adx + cb * ady) + 72.0 * o * Ub * (ca * AX + cb * AY)),
+                        atomic);
+                acc_add(&A->dmean2D[3 * (size_t)j + 1], hH * (VE * (cb * adx + cc * ady) + 72.0 * o * Ub * (cb * AX + cc * AY)),
+                        atomic);
+                acc_add(&A->dconic[3 * (size_t)j + 0], 0.5 * (VE * adx * adx + 72.0 * o * Ub * AX * AX), atomic);
+                acc_add(&A->dconic[3 * (size_t)j + 1], VE * adx * ady + 72.0 * o * Ub * AX * AY, atomic);
+                acc_add(&A->dconic[3 * (size_t)j + 2], 0.5 * (VE * ady * ady + 72.0 * o * Ub * AY * AY), atomic);
+            }
+        }
+    free(Gl);
+}
+
+void lso_render_bwd_bound_tiles_mt(const lso_settings* s, const lso_inputs* in, const lso_geom* g,
+                                   const uint32_t* point_list, const uint32_t* ranges, const int32_t* tiles,
+                                   int ntiles, const float* final_T, const uint32_t* n_contrib,
+                                   const float* dout_color, const float* dout_lang, lso_render_grads* bound,
+                                   int nthreads)
+{
+    const int N = in->N;
+    const int D = s->include_feature ? in->D : 0;
+    const double u = 5.9604644775390625e-08; /* 2^-24 */
+    dacc_t A;
+    A.dmean2D = (double*)calloc((size_t)N * 3 + 1, sizeof(double));
+    A.dconic = (double*)calloc((size_t)N * 3 + 1, sizeof(double));
+    A.dopacity = (double*)calloc((size_t)N + 1, sizeof(double));
+    A.dcolor = (double*)calloc((size_t)N * 3 + 1, sizeof(double));
+    A.dlang = (double*)calloc((size_t)N * (D > 0 ? D : 1) + 1, sizeof(double));
+    if (nthreads <= 1) {
+        for (int k = 0; k < ntiles; k++)
+            render_tile_bwd_bound(s, in, g, point_list, ranges, tiles[k], final_T, n_contrib, dout_color, dout_lang,
+                                  &A, 0);
+    } else {
+#pragma omp parallel for schedule(dynamic, 4) num_threads(nthreads)
+        for (int k = 0; k < ntiles; k++)
+            render_tile_bwd_bound(s, in, g, point_list, ranges, tiles[k], final_T, n_contrib, dout_color, dout_lang,
+                                  &A, 1);
+    }
+    for (size_t i = 0; i < (size_t)N * 3; i++) {
+        bound->dmean2D[i] = (i % 3 == 2) ? 0.f : (float)(u * A.dmean2D[i]);
+        bound->dconic[i] = (float)(u * A.dconic[i]);
+        bound->dcolor[i] = (float)(u * A.dcolor[i]);
+    }
+    for (int i = 0; i < N; i++) bound->dopacity[i] = (float)(u * A.dopacity[i]);
+    if (bound->dlang && D)
+        for (size_t i = 0; i < (size_t)N * D; i++) bound->dlang[i] = (float)(u * A.dlang[i]);
+    free(A.dmean2D); free(A.dconic); free(A.dopacity); free(A.dcolor); free(A.dlang);
+}
+
 /* ------------------------------------------------------ preprocess bwd -- */
 /* Chain rule through A.1; conventions as the upstream 3DGS backward:
  * straight-through 0.99 clamp (render), ±1.3 tanfov clamp zeroes the

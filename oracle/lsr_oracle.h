@@ -150,6 +150,16 @@ void lso_render_bwd_tiles_mt(const lso_settings* s, const lso_inputs* in, const 
                              const float* dout_color, const float* dout_lang,
                              lso_render_grads* rg, int nthreads);
 
+/* A-priori bound of |product deterministic backward - this oracle| per
+ * render-gradient element (the same fields as lso_render_grads); see the
+ * derivation at its definition.  Excludes the fixed-point rounding and the
+ * two final fp32 roundings, which the caller adds. */
+void lso_render_bwd_bound_tiles_mt(const lso_settings* s, const lso_inputs* in, const lso_geom* g,
+                                   const uint32_t* point_list, const uint32_t* ranges, const int32_t* tiles,
+                                   int ntiles, const float* final_T, const uint32_t* n_contrib,
+                                   const float* dout_color, const float* dout_lang, lso_render_grads* bound,
+                                   int nthreads);
+
 typedef struct {
     float* dmeans3D;  /* N*3 */
     float* dsh;       /* N*M*3 or NULL */

@@ -69,6 +69,7 @@ def load():
         lib.lso_power_cut.argtypes = [ctypes.c_float]
         lib.lso_expf.restype = ctypes.c_float
         lib.lso_expf.argtypes = [ctypes.c_float]
+        lib.lso_render_bwd_bound_tiles_mt.restype = None
         _lib = lib
     return _lib
 
@@ -239,6 +240,77 @@ def backward(pb: Problem, fwd: dict, dout_color: np.ndarray, dout_lang: np.ndarr
         rows = np.repeat(np.arange(N)[:, None], qcodes.shape[1], 1)
         out["dlang_weights"] = np.where(ok, out["dlang"][rows, np.clip(qcodes, 0, D - 1)], 0.0).astype(np.float32)
         out["dlang"] = None
+    return out
+
+
+def backward_bound(pb: Problem, fwd: dict, dout_color: np.ndarray, dout_lang: np.ndarray | None = None,
+                   nthreads: int = 1) -> dict:
+    """A-priori bound of |product deterministic backward - oracle| per render-gradient
+    element (lso_render_bwd_bound_tiles_mt; dense language input): dmean2D (N,3),
+    dconic (N,3), dopacity (N,), dcolor (N,3), dlang (N,D).  Excludes the fixed-point
+    rounding of the block partials and the two final fp32 roundings."""
+    lib = load()
+    N, D = pb.N, pb.D
+    g, geom = fwd["_keep"]
+    s, i = pb._structs()
+    dcol = _np(dout_color)
+    dlang = _np(dout_lang) if (D and dout_lang is not None) else None
+    b = dict(dmean2D=np.zeros((N, 3), np.float32), dconic=np.zeros((N, 3), np.float32),
+             dopacity=np.zeros(N, np.float32), dcolor=np.zeros((N, 3), np.float32),
+             dlang=np.zeros((N, max(D, 1)), np.float32))
+    bs = _RGrads(_p(b["dmean2D"]), _p(b["dconic"]), _p(b["dopacity"]), _p(b["dcolor"]), _p(b["dlang"]) if D else None)
+    pl = np.ascontiguousarray(fwd["point_list"] if fwd["num_rendered"] > 0 else np.zeros(1, np.uint32))
+    tl = np.arange(pb.gx * pb.gy, dtype=np.int32)
+    lib.lso_render_bwd_bound_tiles_mt(ctypes.byref(s), ctypes.byref(i), ctypes.byref(geom), _p(pl), _p(fwd["ranges"]),
+                                      _p(tl), len(tl), _p(fwd["final_T"]), _p(fwd["n_contrib"]), _p(dcol), _p(dlang),
+                                      ctypes.byref(bs), int(nthreads))
+    b["dlang"] = b["dlang"][:, :D] if D else None
+    return b
+
+
+def preprocess_backward(pb: Problem, fwd: dict, rg: dict) -> dict:
+    """The oracle's preprocess backward (lso_preprocess_bwd) from GIVEN render
+    gradients rg = {dmean2D (N,3), dconic (N,3), dopacity (N,), dcolor (N,3)}:
+    the chain rule alone, e.g. applied to the product's own gradient rows."""
+    lib = load()
+    N = pb.N
+    g, geom = fwd["_keep"]
+    s, i = pb._structs()
+    r = {k: np.ascontiguousarray(rg[k], dtype=np.float32) for k in ("dmean2D", "dconic", "dopacity", "dcolor")}
+    rgs = _RGrads(_p(r["dmean2D"]), _p(r["dconic"]), _p(r["dopacity"]), _p(r["dcolor"]), None)
+    pgd = dict(dmeans3D=np.zeros((N, 3), np.float32), dcolors=np.zeros((N, 3), np.float32))
+    if pb.shs is not None:
+        pgd["dsh"] = np.zeros_like(pb.shs)
+    if pb.scales is not None:
+        pgd["dscales"] = np.zeros((N, 3), np.float32)
+        pgd["drot"] = np.zeros((N, 4), np.float32)
+    if pb.cov3D is not None:
+        pgd["dcov3D"] = np.zeros((N, 6), np.float32)
+    pgs = _PGrads(_p(pgd["dmeans3D"]), _p(pgd.get("dsh")), _p(pgd["dcolors"]), _p(pgd.get("dscales")),
+                  _p(pgd.get("drot")), _p(pgd.get("dcov3D")))
+    lib.lso_preprocess_bwd(ctypes.byref(s), ctypes.byref(i), ctypes.byref(geom), ctypes.byref(rgs), ctypes.byref(pgs))
+    return pgd
+
+
+def preprocess_backward_abs(pb: Problem, fwd: dict, rg: dict) -> dict:
+    """sum_k |J e_k| |rg_k| per output element: the chain rule's Jacobian J (per
+    Gaussian, linear in the render gradients) applied to each render-gradient slot
+    k alone (mean2D x/y, conic a/b/c, colour r/g/b), in absolute value, weighted
+    by |rg_k|: the magnitude against which the chain's fp32 rounding is bounded."""
+    N = pb.N
+    slots = [("dmean2D", 0), ("dmean2D", 1), ("dconic", 0), ("dconic", 1), ("dconic", 2),
+             ("dcolor", 0), ("dcolor", 1), ("dcolor", 2)]
+    out = None
+    for key, c in slots:
+        unit = {k: np.zeros((N, 3), np.float32) for k in ("dmean2D", "dconic", "dcolor")}
+        unit["dopacity"] = np.zeros(N, np.float32)
+        unit[key][:, c] = np.abs(np.asarray(rg[key], np.float32)[:, c])
+        pg = preprocess_backward(pb, fwd, unit)
+        if out is None:
+            out = {k: np.abs(v).astype(np.float64) for k, v in pg.items()}
+        else:
+            for k, v in pg.items():
+                out[k] += np.abs(v)
     return out
 
 

@@ -240,3 +240,49 @@ def needle_contributing_tiles(out, W, H, band=4.0):
         m = (a >= np.float32(1 / 255.0)) & (p <= 0)
         res[int(i)] = set(((ys[m] // 16) * gx + xs[m] // 16).tolist())
     return res
+
+
+def run_gpu_bwd_rows(case, device, dout_color, dout_lang=None, deterministic=True):
+    """Forward + backward through the rasterizer's own autograd function bodies
+    (rasterizer._run_forward / _RasterizeGaussians.backward), every input
+    requiring grad, keeping the backward's gradient ROWS: the forward-prepared
+    workspace the backward accumulates into (the deterministic backward's
+    conversion pass writes every element of it) -- [0,1] dL/dmeans2D (NDC),
+    [2..4] dL/dconic, [5] dL/dopacity, [6..8] dL/dcolour, lang columns per
+    layout.  Returns {"rows": (N, VP), "VP": VP, "grad_<input>": ...}."""
+    from types import SimpleNamespace
+
+    from langsplatv2_amd import _lib, rasterizer
+    rs = settings_for(case, device)
+    t = gpu_inputs(case, device, requires_grad=False)
+    e = torch.empty(0, device=device)
+    lang_on = "language_feature_precomp" in t and not case["quick"]
+    req = _lib.LSR_GWS_GEOM | (_lib.LSR_GWS_LANG if lang_on else 0)
+    prev = _lib.set_deterministic(deterministic)
+    try:
+        color, lang, radii, M, bufs, saved, dims, ws = rasterizer._run_forward(
+            t["means3D"], t.get("shs", e), t.get("colors_precomp", e), t.get("language_feature_precomp", e), e, e,
+            t["opacities"], t.get("scales", e), t.get("rotations", e), t.get("cov3D_precomp", e), rs, req)
+        assert ws is not None and ws[0] is not None
+        has = lambda k: k in t  # noqa: E731
+        need = (True, True, has("shs"), has("colors_precomp"), lang_on, False, False, True, has("scales"),
+                has("rotations"), has("cov3D_precomp"), False)
+        ctx = SimpleNamespace(raster_settings=rs, num_rendered=M, dims=dims, grad_ws=ws, needs_input_grad=need,
+                              input_ids={}, saved_tensors=(*saved, radii, bufs[_lib.LSR_BUF_GEOM],
+                                                           bufs[_lib.LSR_BUF_BINNING], bufs[_lib.LSR_BUF_IMAGE],
+                                                           bufs.get(_lib.LSR_BUF_LISTS)))
+        dl = torch.from_numpy(dout_lang).to(device) if (dout_lang is not None and lang_on) else None
+        g = rasterizer._RasterizeGaussians.backward(ctx, torch.from_numpy(dout_color).to(device), dl, None)
+        torch.cuda.synchronize()
+    finally:
+        _lib.set_deterministic(prev)
+    N = t["means3D"].shape[0]
+    VP = ws[1] // (4 * N)
+    out = dict(rows=ws[0][:N * VP * 4].view(torch.float32).view(N, VP).cpu().numpy(), VP=VP,
+               radii=radii.cpu().numpy(), num_rendered=M)
+    names = ("means3D", "means2D", "shs", "colors_precomp", "language_feature_precomp", None, None, "opacities",
+             "scales", "rotations", "cov3D_precomp")
+    for nm, v in zip(names, g):
+        if nm is not None and v is not None:
+            out["grad_" + nm] = v.cpu().numpy()
+    return out

@@ -16,7 +16,7 @@ def test_status_codes_have_text():
     lib = _lib.load()
     assert b"non-finite" in lib.lsr_strerror(_lib.LSR_ENONFINITE).lower()
     assert b"binning lists" in lib.lsr_strerror(_lib.LSR_ELISTS).lower()
-    assert lib.lsr_abi_version() == 11
+    assert lib.lsr_abi_version() == 12
 
 
 def test_options_roundtrip():
