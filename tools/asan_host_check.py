@@ -96,7 +96,7 @@ assert lib.lsr_adam_step(None, None, None, None, -1, 0.1, 0.9, 0.999, 1e-8, 0.0,
 calls += 9
 # pure host code: stage-name parsing (random strings), profiling tables, versions
 names = ["preprocess", "scan_tiles", "bin_count", "scan_tile_counts", "bin_scatter", "tile_sort", "render_fwd",
-         "grad_zero", "render_bwd", "preprocess_bwd"]
+         "grad_zero", "render_bwd", "preprocess_bwd", "det_bounds", "det_finish"]
 for _ in range(2000):
     parts = [rng.choice(names + ["", "x", "render", "render_bwdx", "a" * rng.randint(0, 300)]) for _ in
              range(rng.randint(0, 6))]
@@ -131,7 +131,11 @@ for mb in (0, 4096, 2048):   # LSR_OPT_LISTS_MAX_MB
     assert lib.lsr_set_option(2, mb) == 0
     assert lib.lsr_get_option(2, ctypes.byref(v)) == 0 and v.value == mb
     calls += 2
-for opt, val in ((1, 2), (1, 3), (1, -1), (2, -5), (0, 0), (77, 1)):
+for on in (1, 0):             # LSR_OPT_DETERMINISTIC
+    assert lib.lsr_set_option(4, on) == 0
+    assert lib.lsr_get_option(4, ctypes.byref(v)) == 0 and v.value == on
+    calls += 2
+for opt, val in ((1, 2), (1, 3), (1, -1), (2, -5), (0, 0), (77, 1), (4, 2), (4, -1)):
     assert lib.lsr_set_option(opt, val) != 0
     calls += 1
 assert lib.lsr_get_option(1, None) != 0
