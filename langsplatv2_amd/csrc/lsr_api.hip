@@ -1165,9 +1165,11 @@ int lsr_backward(const lsr_settings* s, const lsr_inputs* in, const lsr_bwd_in* 
 // LSR_OPT_DETERMINISTIC: the bounds word ({max |dL/dout|, max |feature|,
 // flags}) and the zeroed 64-bit fixed-point twins of the accumulators the
 // render backward adds into (rb.grad_acc's (P, VP) rows, and with lang_direct
-// the (P, D) language rows); rb.radii must be set.
-static int det_prepare(RenderBwdArgs& rb, bool lang_direct, lsr_alloc_fn alloc, void* ctx, hipStream_t st)
+// the (P, D) language rows); rb.radii = the forward's radii.
+static int det_prepare(RenderBwdArgs& rb, const int32_t* radii, bool lang_direct, lsr_alloc_fn alloc, void* ctx,
+                       hipStream_t st)
 {
+    rb.radii = radii;
     const size_t P = (size_t)rb.f.P;
     const size_t rows = align256(P * (size_t)rb.VP * 8);
     const size_t lang = lang_direct ? align256(P * (size_t)rb.f.D * 8) : 0;
@@ -1219,7 +1221,7 @@ static int backward_dense(const lsr_settings* s, const lsr_inputs* in, const lsr
         rb.grad_acc = out->dL_dlang;
         rb.VP = Dd;
         if (det) {
-            rc = det_prepare(rb, false, alloc, ctx, st);
+            rc = det_prepare(rb, b->radii, false, alloc, ctx, st);
             if (rc != LSR_OK) return rc;
         } else if (!ws_lang) {
             StageScope sc(ST_GZERO, st);
@@ -1261,7 +1263,7 @@ static int backward_dense(const lsr_settings* s, const lsr_inputs* in, const lsr
     rb.VP = VP;
     rb.lang_acc = lang_direct ? out->dL_dlang : nullptr;
     if (det) {
-        rc = det_prepare(rb, lang_direct, alloc, ctx, st);
+        rc = det_prepare(rb, b->radii, lang_direct, alloc, ctx, st);
         if (rc != LSR_OK) return rc;
     }
     { StageScope sc(ST_RENDER_BWD, st); LSR_HIP(launch_render_bwd(rb, st)); }
