@@ -348,6 +348,35 @@ def quick_fps(N, dev, W=1280, H=800, iters=20):
     return out
 
 
+def deterministic_cost(step, steps):
+    """The same fwd+bwd step with the deterministic backward (LSR_OPT_DETERMINISTIC:
+    fixed-point cross-block sums, include/lsr.h): its time per step and per stage
+    (outside the headline's timed region), and whether two steps' gradients are
+    bit-identical."""
+    with _lib.deterministic(True):
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        _lib.profile_stages(None)
+        _lib.profile_reset()
+        _lib.profile_enable(True)
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        _lib.profile_enable(False)
+        st = {k: round(ms / c, 4) for k, (ms, c) in _lib.profile_query().items() if c}
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        a, b = step(), step()
+        same = all(torch.equal(x, y) for x, y in zip(a, b) if x is not None)
+    return dict(what="fwd+bwd step with lsr_set_option(LSR_OPT_DETERMINISTIC, 1)",
+                ms_per_step=round(el / steps * 1e3, 4), frames_per_s=round(steps / el, 1), stages_ms=st,
+                bit_identical_runs=bool(same))
+
+
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -552,6 +581,7 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fwd-1mpix", action="store_true")
     ap.add_argument("--no-quick", action="store_true")
+    ap.add_argument("--no-det", action="store_true", help="skip the deterministic-backward sub-line")
     ap.add_argument("--dry-run", action="store_true", help="bring the ranks up on gloo and exit (no GPU)")
     args = ap.parse_args()
 
@@ -738,6 +768,8 @@ def main() -> int:
             "stage_bytes": {k: int(v) for k, v in bytes_.items()},
             "workload_stats": info,
         }
+        if world == 1 and args.config == 3 and not args.no_det:
+            out["deterministic"] = deterministic_cost(step, args.steps)
         if world == 1 and not args.no_fwd_1mpix and args.config == 3:
             out["fwd_fps_1mpix"] = round(fwd_fps({k: v.detach() for k, v in g.items()}, dev, deg, D), 1)
         if world == 1 and not args.no_quick and args.config == 3:

@@ -2,7 +2,7 @@
 the number of staged (candidate, 8x8-block) pairs k_render_bwd_mf<., LST> walks,
 i.e. the sum of the per-block list counts the forward wrote (lsr_fwd_out.lists:
 listA, listB, then lcount[4T] at 2 x align256(4 M x 16), csrc/lsr_api.hip
-set_block_lists).  Prints the integer (tools/r05_pass.sh feeds it to
+set_block_lists).  Prints the integer (tools/pass.py pmc feeds it to
 tools/pmc_issue.py --units)."""
 import os
 import sys

@@ -1,5 +1,5 @@
 """Issue-rate roofline of the render kernels from two rocprofv3 SQ passes
-(tools/pmc_sq.sh: P1 = instruction counts + SQ_BUSY_CYCLES + SQ_WAVE_CYCLES,
+(tools/pass.py pmc: P1 = instruction counts + SQ_BUSY_CYCLES + SQ_WAVE_CYCLES,
 P2 = wait / active / MFMA-busy cycles), per kernel, averaged per dispatch.
 
 Units (MI355X_MICROARCH.md, rocprofv3 PMC + cycle-constants rows):
@@ -102,7 +102,7 @@ def main():
                         d[nm] = round(c[ck] / u, 2)
         res[k] = {"dispatches": min(a[k]["dispatches"], b[k]["dispatches"]),
                   "counters": {ck: round(v) for ck, v in sorted(c.items())}, "derived": d}
-    doc = {"method": "rocprofv3 --pmc, two SQ passes (tools/pmc_sq.sh) over tools/pmc_step.py; per-dispatch averages; "
+    doc = {"method": "rocprofv3 --pmc, two SQ passes (tools/pass.py pmc) over tools/pmc_step.py; per-dispatch averages; "
                      "see tools/pmc_issue.py for the units", "kernels": res}
     with open(out, "w") as f:
         json.dump(doc, f, indent=1)

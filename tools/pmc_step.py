@@ -22,7 +22,7 @@ if os.environ.get("LSR_QUICK", "0") == "1":
         image_height=H, image_width=W, tanfovx=cam["tanfovx"], tanfovy=cam["tanfovy"], bg=torch.zeros(3, device=dev),
         scale_modifier=1.0, viewmatrix=cam["viewmatrix"].to(dev), projmatrix=cam["projmatrix"].to(dev), sh_degree=3,
         campos=cam["campos"].to(dev), prefiltered=False, debug=False, include_feature=False, quick_render=True,
-        language_feature_layout=os.environ.get("LSR_QUICK_LAYOUT", "hwc"))
+        language_feature_layout=os.environ.get("LSR_QUICK_LAYOUT"))   # unset: the default (pixel-major)
     r = GaussianRasterizer(rs)
     z = torch.zeros_like(t["means3D"])
     from langsplatv2_amd import quick

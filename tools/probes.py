@@ -1,6 +1,6 @@
-"""Round-4 A/B variants of liblsr.so (tools/variant.py: patched copies of csrc).
+"""A/B variants and timing probes of liblsr.so (tools/variant.py: patched copies of csrc).
 Timing probes marked (probe) compute wrong results and exist only to price a
-piece of work; the others are candidate changes.  Usage: python tools/r04_variants.py [NAME ...]"""
+piece of work; the others are candidate changes.  Usage: python tools/probes.py [NAME ...]"""
 import subprocess
 import sys
 
