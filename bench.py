@@ -158,6 +158,33 @@ def atomic_floor(stage, ms_per_launch, prefix="r"):
             "note": "all of the kernel's HBM writes are buffer/global_atomic_add_f32 into gradient rows; "
                     "rate from MI355X_MICROARCH.md (global float atomics, chip-wide)"}
 
+def rocprof_avg(stage):
+    """The stage kernel's average duration under rocprofv3 --kernel-trace --stats from the
+    newest committed profile of the cfg3 step ALONE (profiles/r*_kernel_stats.md written by
+    `tools/pass.py TAG prof`, title "(cfg3 step alone)"): the HIP-event roofline time's
+    cross-check."""
+    import glob
+    import re
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_kernel_stats.md")),
+                   key=lambda f: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(f))])
+    kn = STAGE_KERNEL.get(stage, "k_" + stage)
+    for fn in reversed(files):
+        with open(fn) as f:
+            lines = f.read().splitlines()
+        if not lines or "(cfg3 step alone)" not in lines[0]:
+            continue
+        rows = []
+        for ln in lines:
+            m = re.match(r"\| `(?:lsr::)?([^`]+)` \| (\d+) \| ([\d.]+) \| ([\d.]+) \|", ln)
+            if m and (m.group(1) == kn or m.group(1).startswith(kn + "<")):
+                rows.append((float(m.group(3)), m.group(1), int(m.group(2)), float(m.group(4))))
+        if rows:
+            tot, name, calls, avg = max(rows)
+            return {"kernel": name, "avg_ms": round(avg / 1e3, 4), "calls": calls,
+                    "source": os.path.relpath(fn, ROOT)}
+    return None
+
+
 STAGE_KERNEL = {"render_bwd": "k_render_bwd_mf", "render_fwd": "k_render_fwd", "preprocess": "k_preprocess",
                 "preprocess_bwd": "k_preprocess_bwd", "bin_scatter": "k_bin_scatter", "bin_count": "k_bin_count",
                 "tile_sort": "k_tile_sort"}
@@ -755,6 +782,8 @@ def main() -> int:
                 "bytes_formula": "SURVEY.md §8d (bench.py:algorithmic_bytes)",
                 "ms_per_launch": round(dom_ms, 4),
                 "launches_timed": dom_calls,
+                # the same kernel's average under rocprofv3 in a profile of this step alone
+                "rocprof": rocprof_avg(dom) if args.config == 3 else None,
                 # the kernel is issue/latency-bound, not HBM-bound: its SQ-counter roofline
                 "issue": pmc_issue(dom, prefix=pre),
                 # and its writes are memory-side atomics: their rate's floor

@@ -18,6 +18,9 @@ Two levels, both against the C restatement (oracle/lsr_oracle.c):
                  (|a c| + b^2) / |a c - b^2| of the 2D conic covers the one
                  cancellation in it, the determinant and 1/det^2).
 Together they bound every gradient the rasterizer returns.  u = 2^-24."""
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -26,6 +29,23 @@ from harness import gpu_inputs, make_case, oracle_problem, run_gpu_bwd_rows, set
 
 pytestmark = pytest.mark.gpu
 U = 2.0 ** -24
+LOG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "det_bounds.json")
+
+
+def record(test, res):
+    """Append one case's max |err| and max |err| / bound per quantity to
+    gpurun_out/det_bounds.json (the numbers DESIGN.md §4 quotes)."""
+    os.makedirs(os.path.dirname(LOG), exist_ok=True)
+    doc = {}
+    if os.path.exists(LOG):
+        try:
+            with open(LOG) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            doc = {}
+    doc[test] = res
+    with open(LOG, "w") as f:
+        json.dump(doc, f, indent=1, sort_keys=True)
 
 
 def _upstream(H, W, D, seed=1):
@@ -149,7 +169,7 @@ def test_deterministic_backward_within_analytic_bound(gpu, oracle_lib, name):
     got = run_gpu_bwd_rows(case, gpu, dcol, dlang)
     pb, ref, r1 = check_rows(case, got, oracle_lib, dcol, dlang)
     r2 = check_chain(pb, ref, got, oracle_lib)
-    print(name, {k: (f"{v['max_abs']:.2e}", f"{v['max_err_over_bound']:.2e}") for k, v in {**r1, **r2}.items()})
+    record(name, {"rows": r1, "chain": r2})
 
 
 def test_deterministic_language_only_backward(gpu, oracle_lib):

@@ -130,6 +130,27 @@ def test_cfg3_whole_frame_backward_bench_upstream(gpu, oracle_lib):
         assert_grad_close(k, g, r, rtol=GRAD_RTOL_FRAME)
 
 
+def test_cfg3_deterministic_backward_whole_frame(gpu, oracle_lib):
+    """The headline step's backward with LSR_OPT_DETERMINISTIC: two runs give
+    identical bits, and every render-gradient row and every returned 3-D
+    gradient is within the error bound DERIVED for it (tests/test_deterministic.py:
+    the oracle's running forward-error analysis + the fixed-point rounding; the
+    chain rule's fp32 bound), not a tolerance fitted to measurements."""
+    from harness import run_gpu_bwd_rows
+    from test_deterministic import check_chain, check_rows, record
+    case = _case(3)
+    dcol, dlang = _bench_upstream(1080, 1920, 16)
+    a = run_gpu_bwd_rows(case, gpu, dcol, dlang)
+    b = run_gpu_bwd_rows(case, gpu, dcol, dlang)
+    for k in a:
+        if isinstance(a[k], np.ndarray):
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    del b
+    pb, ref, r1 = check_rows(case, a, oracle_lib, dcol, dlang, nthreads=_threads())
+    r2 = check_chain(pb, ref, a, oracle_lib)
+    record("cfg3_whole_frame_bench_upstream", {"rows": r1, "chain": r2})
+
+
 def test_cfg2_whole_frame(gpu, oracle_lib):
     case = _case(2)
     assert case["g"]["means3D"].shape[0] == 100_000 and case["cam"]["W"] == 800 and case["cam"]["H"] == 800
