@@ -2402,38 +2402,60 @@ hipError_t launch_render_bwd(const RenderBwdArgs& b, hipStream_t st)
 // max |dL/dout| over the 3 + D upstream planes and max |feature| over the
 // visible Gaussians' colours and dense language rows (order-independent:
 // atomicMax on the bits of non-negative floats); bit 0 of word 2 flags a
-// non-finite value
+// non-finite value.  Blocks [0, nbd) stream the planes as float4; the rest take
+// one visible Gaussian's row per thread.
+__device__ __forceinline__ void det_max4(float4 v, float& m, bool& bad)
+{
+    bad |= !(isfinite(v.x) && isfinite(v.y) && isfinite(v.z) && isfinite(v.w));
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+}
+
 __global__ void __launch_bounds__(256) k_det_bounds(const float* __restrict__ dc, const float* __restrict__ dl,
-                                                    size_t HW, int D, const float* __restrict__ rgb,
-                                                    const float* __restrict__ lang, const int32_t* __restrict__ radii,
-                                                    int P, float* bounds)
+                                                    uint32_t ncol, uint32_t nlang, int nbd, int D,
+                                                    const float* __restrict__ rgb, const float* __restrict__ lang,
+                                                    const int32_t* __restrict__ radii, int P, float* bounds)
 {
     float md = 0.f, mf = 0.f;
     bool bad = false;
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t nd = HW * (size_t)(3 + D);
-    for (size_t e = t0; e < nd; e += stride) {
-        const float v = e < 3 * HW ? dc[e] : dl[e - 3 * HW];
-        bad |= !isfinite(v);
-        md = fmaxf(md, fabsf(v));
-    }
-    const int C = 3 + D;
-    const size_t nf = (size_t)P * (size_t)C;
-    for (size_t e = t0; e < nf; e += stride) {
-        const size_t i = e / (size_t)C;
-        const int ch = (int)(e - i * (size_t)C);
-        if (radii[i] <= 0) continue;
-        const float v = ch < 3 ? rgb[3 * i + ch] : lang[i * (size_t)D + (ch - 3)];
-        bad |= !isfinite(v);
-        mf = fmaxf(mf, fabsf(v));
+    if ((int)blockIdx.x < nbd) {
+        // upstream planes: colour (3 HW floats) then language (D HW), float4 where aligned
+        const uint32_t stride = (uint32_t)nbd * blockDim.x;
+        for (int part = 0; part < 2; part++) {
+            const float* src = part ? dl : dc;
+            const uint32_t n = part ? nlang : ncol;
+            if (!src || n == 0) continue;
+            const bool al = ((uintptr_t)src & 15u) == 0;
+            const uint32_t n4 = al ? n / 4 : 0;
+            for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += stride)
+                det_max4(reinterpret_cast<const float4*>(src)[e], md, bad);
+            for (uint32_t e = 4 * n4 + blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
+                const float v = src[e];
+                bad |= !isfinite(v);
+                md = fmaxf(md, fabsf(v));
+            }
+        }
+    } else {
+        const int i = ((int)blockIdx.x - nbd) * (int)blockDim.x + (int)threadIdx.x;
+        if (i < P && radii[i] > 0) {
+            for (int c = 0; c < 3; c++) {
+                const float v = rgb[3 * (size_t)i + c];
+                bad |= !isfinite(v);
+                mf = fmaxf(mf, fabsf(v));
+            }
+            const float* row = lang ? lang + (size_t)i * D : nullptr;
+            for (int c = 0; row && c < D; c++) {
+                const float v = row[c];
+                bad |= !isfinite(v);
+                mf = fmaxf(mf, fabsf(v));
+            }
+        }
     }
     md = wave_max_f(md);
     mf = wave_max_f(mf);
     const bool wbad = wave_ballot(bad) != 0u;
     if ((threadIdx.x & 63) == 0) {
-        atomicMax(reinterpret_cast<unsigned int*>(bounds), __float_as_uint(md));
-        atomicMax(reinterpret_cast<unsigned int*>(bounds + 1), __float_as_uint(mf));
+        if (md > 0.f) atomicMax(reinterpret_cast<unsigned int*>(bounds), __float_as_uint(md));
+        if (mf > 0.f) atomicMax(reinterpret_cast<unsigned int*>(bounds + 1), __float_as_uint(mf));
         if (wbad) atomicOr(reinterpret_cast<unsigned int*>(bounds + 2), 1u);
     }
 }
@@ -2443,11 +2465,12 @@ hipError_t launch_det_bounds(const RenderBwdArgs& b, float* bounds, hipStream_t 
     const size_t HW = (size_t)b.f.cam.W * b.f.cam.H;
     const int D = b.f.D;
     if (D > 0 && (!b.dout_lang || !b.f.lang)) return hipErrorInvalidValue;
-    const size_t n = HW * (size_t)(3 + D) > (size_t)b.f.P * (size_t)(3 + D) ? HW * (size_t)(3 + D)
-                                                                            : (size_t)b.f.P * (size_t)(3 + D);
-    const unsigned nb = (unsigned)std::min<size_t>((n + 255) / 256, 4096);
-    if (nb == 0) return hipSuccess;
-    k_det_bounds<<<nb, 256, 0, st>>>(b.dout_color, b.dout_lang, HW, D, b.f.rgb, b.f.lang, b.radii, b.f.P, bounds);
+    if (3 * HW >= (1ull << 32) || (size_t)D * HW >= (1ull << 32)) return hipErrorInvalidValue;
+    const int nbd = 2048;
+    const int nbf = (b.f.P + 255) / 256;
+    k_det_bounds<<<nbd + nbf, 256, 0, st>>>(b.dout_color, D > 0 ? b.dout_lang : nullptr, (uint32_t)(3 * HW),
+                                            (uint32_t)((size_t)D * HW), nbd, D, b.f.rgb, D > 0 ? b.f.lang : nullptr,
+                                            b.radii, b.f.P, bounds);
     return hipGetLastError();
 }
 
@@ -2455,7 +2478,13 @@ hipError_t launch_det_bounds(const RenderBwdArgs& b, float* bounds, hipStream_t 
 // mode 0: rows (P, VP) generic layout ([0..8] geometry + colour, [12, 12 + D)
 // language) -> gout; mode 1 (lang_direct): rows (P, 16) -> gout, lang (P, D)
 // -> lout; mode 2 (language only): rows (P, D) -> lout.  Every element of the
-// outputs is written (unused row slots 0).
+// outputs is written (unused row slots 0).  One thread per (Gaussian, 4
+// columns), 32-bit index arithmetic.
+__device__ __forceinline__ float det_value(long long acc, int cls, int r, float Dm, float Am, float WH)
+{
+    return acc != 0 ? (float)ldexp((double)acc, -det_shift(cls, r, Dm, Am, WH)) : 0.f;
+}
+
 __global__ void __launch_bounds__(256) k_det_finish(const long long* __restrict__ rows,
                                                     const long long* __restrict__ lang,
                                                     const int32_t* __restrict__ radii,
@@ -2463,37 +2492,37 @@ __global__ void __launch_bounds__(256) k_det_finish(const long long* __restrict_
                                                     const float* __restrict__ bg, float WH, float* __restrict__ gout,
                                                     float* __restrict__ lout)
 {
-    const int ncols = mode == 2 ? D : VP + (mode == 1 ? D : 0);
-    const size_t n = (size_t)P * (size_t)ncols;
+    // column quads per Gaussian: the row part, then (mode 1) the language part
+    const int wr = mode == 2 ? D : VP;
+    const int qr = (wr + 3) / 4;
+    const int ql = mode == 1 ? (D + 3) / 4 : 0;
+    const int qn = qr + ql;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t i = t / (uint32_t)qn;
+    if (i >= (uint32_t)P) return;
+    const int q = (int)(t - i * (uint32_t)qn);
     const float Dm = bounds[0];
     // the render backward's Am, the same expression (the exponents must agree bit for bit)
     const float Am = (2.f * (float)(3 + D) * bounds[1] + (fabsf(bg[0]) + fabsf(bg[1]) + fabsf(bg[2]))) * Dm;
     const bool bad = (__float_as_uint(bounds[2]) & 1u) != 0u;
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
-        const size_t i = e / (size_t)ncols;
-        const int col = (int)(e - i * (size_t)ncols);
-        const int r = radii[i];
-        long long acc = 0;
+    const int r = radii[i];
+    const bool in_rows = q < qr;
+    const int c0 = 4 * (in_rows ? q : q - qr);
+    const int w = in_rows ? wr : D;
+    const long long* src = (in_rows ? rows : lang) + (size_t)i * w;
+    float* dst = (in_rows && mode != 2 ? gout : lout) + (size_t)i * w;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int col = c0 + k;
+        if (col >= w) break;
         int cls = 0;
         bool used = true;
-        float* dst;
-        if (mode == 2) {
-            acc = rows[i * (size_t)D + col];
-            dst = lout + i * (size_t)D + col;
-        } else if (col < VP) {
+        if (in_rows && mode != 2) {
             used = col < 9 || (mode == 0 && col >= LSR_GROW_LANG && col < LSR_GROW_LANG + D);
             cls = det_class_of(col);
-            acc = used ? rows[i * (size_t)VP + col] : 0;
-            dst = gout + i * (size_t)VP + col;
-        } else {
-            const int k = col - VP;
-            acc = lang[i * (size_t)D + k];
-            dst = lout + i * (size_t)D + k;
         }
-        float v = 0.f;
-        if (acc != 0) v = (float)ldexp((double)acc, -det_shift(cls, r, Dm, Am, WH));
-        *dst = bad ? __builtin_nanf("") : v;
+        const long long acc = used ? src[col] : 0;
+        dst[col] = bad ? __builtin_nanf("") : det_value(acc, cls, r, Dm, Am, WH);
     }
 }
 
@@ -2504,13 +2533,15 @@ hipError_t launch_det_finish(const RenderBwdArgs& b, bool lang_only, float* grad
     if (!b.det_rows || !b.det_bounds || !b.radii || (mode == 0 && !grad_out) || (mode != 0 && !lang_out) ||
         (mode == 1 && !grad_out))
         return hipErrorInvalidValue;
-    const size_t ncols = mode == 2 ? (size_t)D : (size_t)b.VP + (mode == 1 ? (size_t)D : 0);
-    const size_t n = (size_t)P * ncols;
+    const int wr = mode == 2 ? D : b.VP;
+    const int qn = (wr + 3) / 4 + (mode == 1 ? (D + 3) / 4 : 0);
+    const size_t n = (size_t)P * (size_t)qn;
     if (n == 0) return hipSuccess;
+    if (n >= (1ull << 32)) return hipErrorInvalidValue;
     const Cam& c = b.f.cam;
-    const unsigned nb = (unsigned)std::min<size_t>((n + 255) / 256, 8192);
-    k_det_finish<<<nb, 256, 0, st>>>(b.det_rows, b.det_lang, b.radii, b.det_bounds, P, b.VP, D, mode, c.bg,
-                                     (float)std::max(c.W, c.H), grad_out, lang_out);
+    k_det_finish<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(b.det_rows, b.det_lang, b.radii, b.det_bounds, P, b.VP,
+                                                              D, mode, c.bg, (float)std::max(c.W, c.H), grad_out,
+                                                              lang_out);
     return hipGetLastError();
 }
 }  // namespace lsr
