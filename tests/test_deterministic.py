@@ -235,3 +235,22 @@ def test_deterministic_nonfinite_upstream_poisons_the_call(gpu):
     dcol[1, 10, 20] = np.nan
     got = run_gpu_bwd_rows(case, gpu, dcol, dlang)
     assert np.isnan(got["rows"]).all() and np.isnan(got["grad_language_feature_precomp"]).all()
+
+
+def test_deterministic_backward_independent_of_list_mode(gpu):
+    """The forward's per-block candidate lists (LSR_OPT_LISTS_MAX_MB) change how
+    the backward finds its candidates, not which ones or in what order: with
+    fixed-point cross-block sums, the list-driven and the re-staging backward
+    give the same bits."""
+    from langsplatv2_amd import _lib
+    case = make_case(**CASES["sh3_lang16_direct"])
+    dcol, dlang = _upstream(192, 256, 16)
+    a = run_gpu_bwd_rows(case, gpu, dcol, dlang)
+    prev = _lib.set_lists_max_mb(0)
+    try:
+        b = run_gpu_bwd_rows(case, gpu, dcol, dlang)
+    finally:
+        _lib.set_lists_max_mb(prev)
+    for k in a:
+        if isinstance(a[k], np.ndarray):
+            np.testing.assert_array_equal(a[k], b[k], err_msg=k)
