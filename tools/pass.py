@@ -17,6 +17,7 @@ Steps (run in order; outputs under gpurun_out/, named TAG_*):
     pmc            cfg3: two SQ issue passes + FETCH_SIZE / WRITE_SIZE passes over
                    tools/pmc_step.py -> TAG_pmc_issue.json, TAG_pmc_traffic.json
     pmc2 pmc5      FETCH / WRITE passes at cfg2 / cfg5 -> cfgN_TAG_pmc_traffic.json
+    rehearse2      bench.py --gpus 2 on the one-GPU box (gloo exchange, both ranks on cuda:0)
     ab:NAME=LIB,.. tools/ab.py A/B of library variants (tools/variant.py builds them)
                    in one process, both orders; LSR_CFG picks the config
 
@@ -153,6 +154,19 @@ def step(tag, s):
             subprocess.call([PY, "tools/pmc_traffic.py", fF, fW, os.path.join(OUT, f"cfg{n}_{tag}_pmc_traffic.json")],
                             cwd=ROOT, stdout=f)
         tail(txt, 12)
+    elif s == "rehearse2":
+        # bench.py's multi-rank path on the one-GPU box: two ranks on cuda:0 with a gloo
+        # exchange (rehearsal-only overrides; the driver's runs use RCCL, one GPU per rank)
+        js = os.path.join(OUT, f"{tag}_rehearse2.json")
+        env = dict(os.environ, LSR_BENCH_BACKEND="gloo", LSR_BENCH_SAME_DEVICE="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+        with open(js, "w") as f, open(js[:-5] + ".err", "w") as g:
+            rc = subprocess.call(["timeout", "-k", "10", "400", PY, "bench.py", "--gpus", "2", "--steps", "5",
+                                  "--warmup", "2", "--no-quick", "--no-fwd-1mpix", "--no-cpu-baseline", "--no-det"],
+                                 stdout=f, stderr=g, cwd=ROOT, env=env)
+        if rc != 0:
+            tail(js[:-5] + ".err", 20)
+            raise Fault(f"rehearse2 ended with status {rc}")
+        tail(js, 1)
     elif s.startswith("ab:"):
         pairs = s[3:].split(",")
         name = "_".join(p.split("=")[0] for p in pairs)
