@@ -144,6 +144,8 @@ CASES = {
     "rgb_lang4_rows_bg": dict(N=15000, W=200, H=150, sh_degree=None, lang_dim=4, seed=4, bg=(1.0, 0.5, 0.25)),
     "sh1_nolang_cov": dict(N=12000, W=160, H=120, sh_degree=1, lang_dim=0, seed=5, cov_precomp=True),
     "sh3_lang32_direct_bg": dict(N=8000, W=128, H=96, sh_degree=3, lang_dim=32, seed=6, bg=(0.2, 0.2, 0.9)),
+    "sh2_lang64_rows": dict(N=6000, W=112, H=80, sh_degree=2, lang_dim=64, seed=10),
+    "rgb_lang24_rows_scale": dict(N=7000, W=97, H=61, sh_degree=None, lang_dim=24, seed=11, scale_modifier=1.3),
 }
 
 
@@ -172,14 +174,16 @@ def test_deterministic_backward_within_analytic_bound(gpu, oracle_lib, name):
     record(name, {"rows": r1, "chain": r2})
 
 
-def test_deterministic_language_only_backward(gpu, oracle_lib):
+@pytest.mark.parametrize("D", [16, 3])
+def test_deterministic_language_only_backward(gpu, oracle_lib, D):
     """Feature-mode shape (geometry frozen, only the language input requires
     grad): the language-only kernel in fixed point, bit-reproducible and within
-    the bound; the default (float-atomic) run agrees within the same bound."""
+    the bound (D = 3: a width that is not a multiple of the conversion's column
+    quads)."""
     from diff_gaussian_rasterization import GaussianRasterizer
     from langsplatv2_amd import _lib
-    case = make_case(N=20000, W=256, H=192, sh_degree=3, lang_dim=16, seed=7)
-    dcol, dlang = _upstream(192, 256, 16, seed=2)
+    case = make_case(N=20000, W=256, H=192, sh_degree=3, lang_dim=D, seed=7)
+    dcol, dlang = _upstream(192, 256, D, seed=2)
     t = gpu_inputs(case, gpu, requires_grad=False)
     lang = t["language_feature_precomp"].clone().requires_grad_(True)
     r = GaussianRasterizer(raster_settings=settings_for(case, gpu))
