@@ -135,7 +135,7 @@ hipError_t launch_render_bwd_lang(const RenderBwdArgs& a, hipStream_t st);
 hipError_t launch_render_bwd_lang_sparse(const RenderBwdArgs& a, hipStream_t st);
 int lang_set_for(int D);     // compiled channel set >= D, or -1
 // LSR_OPT_DETERMINISTIC: bounds = {max |dL/dout| over the 3 + D planes,
-// max |feature| over the visible Gaussians' colours and dense language rows,
+// max |feature| over the visible Gaussians' colours and the dense language input,
 // flag} (bounds zeroed by the caller; flag bit 0: a non-finite value)
 hipError_t launch_det_bounds(const RenderBwdArgs& b, float* bounds, hipStream_t st);
 // the fixed-point sums back to fp32: rows (P, VP) -> grad_out (every element

@@ -2400,7 +2400,7 @@ hipError_t launch_render_bwd(const RenderBwdArgs& b, hipStream_t st)
 
 // ------------------------------------------ deterministic backward: bounds
 // max |dL/dout| over the 3 + D upstream planes and max |feature| over the
-// visible Gaussians' colours and dense language rows (order-independent:
+// visible Gaussians' colours and the dense language input (order-independent:
 // atomicMax on the bits of non-negative floats); bit 0 of word 2 flags a
 // non-finite value.  Blocks [0, nbd) stream the planes as float4; the rest take
 // one visible Gaussian's row per thread.
@@ -2411,41 +2411,38 @@ __device__ __forceinline__ void det_max4(float4 v, float& m, bool& bad)
 }
 
 __global__ void __launch_bounds__(256) k_det_bounds(const float* __restrict__ dc, const float* __restrict__ dl,
-                                                    uint32_t ncol, uint32_t nlang, int nbd, int D,
-                                                    const float* __restrict__ rgb, const float* __restrict__ lang,
-                                                    const int32_t* __restrict__ radii, int P, float* bounds)
+                                                    uint32_t ncol, uint32_t nlang, int nbd,
+                                                    const float* __restrict__ lang, uint32_t nfeat,
+                                                    const float* __restrict__ rgb, const int32_t* __restrict__ radii,
+                                                    int P, float* bounds)
 {
     float md = 0.f, mf = 0.f;
     bool bad = false;
-    if ((int)blockIdx.x < nbd) {
-        // upstream planes: colour (3 HW floats) then language (D HW), float4 where aligned
-        const uint32_t stride = (uint32_t)nbd * blockDim.x;
-        for (int part = 0; part < 2; part++) {
-            const float* src = part ? dl : dc;
-            const uint32_t n = part ? nlang : ncol;
-            if (!src || n == 0) continue;
-            const bool al = ((uintptr_t)src & 15u) == 0;
-            const uint32_t n4 = al ? n / 4 : 0;
-            for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += stride)
-                det_max4(reinterpret_cast<const float4*>(src)[e], md, bad);
-            for (uint32_t e = 4 * n4 + blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
-                const float v = src[e];
-                bad |= !isfinite(v);
-                md = fmaxf(md, fabsf(v));
-            }
+    // a flat float array's max |v| (float4 where aligned)
+    auto scan = [&](const float* src, uint32_t n, uint32_t b0, uint32_t stride, float& m) {
+        if (!src || n == 0) return;
+        const bool al = ((uintptr_t)src & 15u) == 0;
+        const uint32_t n4 = al ? n / 4 : 0;
+        for (uint32_t e = b0; e < n4; e += stride) det_max4(reinterpret_cast<const float4*>(src)[e], m, bad);
+        for (uint32_t e = 4 * n4 + b0; e < n; e += stride) {
+            const float v = src[e];
+            bad |= !isfinite(v);
+            m = fmaxf(m, fabsf(v));
         }
+    };
+    if ((int)blockIdx.x < nbd) {
+        // the upstream planes (colour, then language) and the dense language input
+        const uint32_t stride = (uint32_t)nbd * blockDim.x, b0 = blockIdx.x * blockDim.x + threadIdx.x;
+        scan(dc, ncol, b0, stride, md);
+        scan(dl, nlang, b0, stride, md);
+        scan(lang, nfeat, b0, stride, mf);
     } else {
+        // the colours of the visible Gaussians (a culled Gaussian's colour is never written)
         const int stride = ((int)gridDim.x - nbd) * (int)blockDim.x;
         for (int i = ((int)blockIdx.x - nbd) * (int)blockDim.x + (int)threadIdx.x; i < P; i += stride) {
             if (radii[i] <= 0) continue;
             for (int c = 0; c < 3; c++) {
                 const float v = rgb[3 * (size_t)i + c];
-                bad |= !isfinite(v);
-                mf = fmaxf(mf, fabsf(v));
-            }
-            const float* row = lang ? lang + (size_t)i * D : nullptr;
-            for (int c = 0; row && c < D; c++) {
-                const float v = row[c];
                 bad |= !isfinite(v);
                 mf = fmaxf(mf, fabsf(v));
             }
@@ -2479,12 +2476,13 @@ hipError_t launch_det_bounds(const RenderBwdArgs& b, float* bounds, hipStream_t 
     const size_t HW = (size_t)b.f.cam.W * b.f.cam.H;
     const int D = b.f.D;
     if (D > 0 && (!b.dout_lang || !b.f.lang)) return hipErrorInvalidValue;
-    if (3 * HW >= (1ull << 32) || (size_t)D * HW >= (1ull << 32)) return hipErrorInvalidValue;
+    const size_t nf = (size_t)b.f.P * (size_t)(D > 0 ? D : 0);
+    if (3 * HW >= (1ull << 32) || (size_t)D * HW >= (1ull << 32) || nf >= (1ull << 32)) return hipErrorInvalidValue;
     const int nbd = 1024;
-    const int nbf = std::min((b.f.P + 255) / 256, 1024);
+    const int nbf = std::min((b.f.P + 255) / 256, 256);
     k_det_bounds<<<nbd + nbf, 256, 0, st>>>(b.dout_color, D > 0 ? b.dout_lang : nullptr, (uint32_t)(3 * HW),
-                                            (uint32_t)((size_t)D * HW), nbd, D, b.f.rgb, D > 0 ? b.f.lang : nullptr,
-                                            b.radii, b.f.P, bounds);
+                                            (uint32_t)((size_t)D * HW), nbd, D > 0 ? b.f.lang : nullptr,
+                                            (uint32_t)nf, b.f.rgb, b.radii, b.f.P, bounds);
     return hipGetLastError();
 }
 
