@@ -2423,7 +2423,18 @@ __global__ void __launch_bounds__(256) k_det_bounds(const float* __restrict__ dc
         if (!src || n == 0) return;
         const bool al = ((uintptr_t)src & 15u) == 0;
         const uint32_t n4 = al ? n / 4 : 0;
-        for (uint32_t e = b0; e < n4; e += stride) det_max4(reinterpret_cast<const float4*>(src)[e], m, bad);
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        uint32_t e = b0;
+        // 8 independent loads in flight per lane (one at a time left the pass
+        // latency-bound: 0.095 ms for 0.23 GB)
+        for (; e + 7 * stride < n4; e += 8 * stride) {
+            float4 v[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) v[k] = s4[e + k * stride];
+#pragma unroll
+            for (int k = 0; k < 8; k++) det_max4(v[k], m, bad);
+        }
+        for (; e < n4; e += stride) det_max4(s4[e], m, bad);
         for (uint32_t e = 4 * n4 + b0; e < n; e += stride) {
             const float v = src[e];
             bad |= !isfinite(v);
@@ -2523,18 +2534,25 @@ __global__ void __launch_bounds__(256) k_det_finish(const long long* __restrict_
     const int w = in_rows ? wr : D;
     const long long* src = (in_rows ? rows : lang) + (size_t)i * w;
     float* dst = (in_rows && mode != 2 ? gout : lout) + (size_t)i * w;
+    float v[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int col = c0 + k;
-        if (col >= w) break;
         int cls = 0;
-        bool used = true;
+        bool used = col < w;
         if (in_rows && mode != 2) {
-            used = col < 9 || (mode == 0 && col >= LSR_GROW_LANG && col < LSR_GROW_LANG + D);
+            used = used && (col < 9 || (mode == 0 && col >= LSR_GROW_LANG && col < LSR_GROW_LANG + D));
             cls = det_class_of(col);
         }
         const long long acc = used ? src[col] : 0;
-        dst[col] = bad ? __builtin_nanf("") : det_value(acc, cls, r, Dm, Am, WH);
+        v[k] = bad ? __builtin_nanf("") : det_value(acc, cls, r, Dm, Am, WH);
+    }
+    if (c0 + 4 <= w && ((uintptr_t)(dst + c0) & 15u) == 0) {
+        *reinterpret_cast<float4*>(dst + c0) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (c0 + k < w) dst[c0 + k] = v[k];
     }
 }
 
