@@ -1173,14 +1173,17 @@ static int det_prepare(RenderBwdArgs& rb, const int32_t* radii, bool lang_direct
     const size_t P = (size_t)rb.f.P;
     const size_t rows = align256(P * (size_t)rb.VP * 8);
     const size_t lang = lang_direct ? align256(P * (size_t)rb.f.D * 8) : 0;
-    uint8_t* ws = (uint8_t*)alloc(ctx, 256 + rows + lang, LSR_BUF_DET);
+    const size_t hdr = LSR_DET_HDR + align256(P * 4);   // + the shift table
+    uint8_t* ws = (uint8_t*)alloc(ctx, hdr + rows + lang, LSR_BUF_DET);
     if (!ws) return LSR_ENOMEM;
     rb.det_bounds = (float*)ws;
-    rb.det_rows = (long long*)(ws + 256);
-    rb.det_lang = lang_direct ? (long long*)(ws + 256 + rows) : nullptr;
+    rb.det_sh = (uint32_t*)(ws + LSR_DET_HDR);
+    rb.det_rows = (long long*)(ws + hdr);
+    rb.det_lang = lang_direct ? (long long*)(ws + hdr + rows) : nullptr;
     {
+        // the header and the shift table are written whole by launch_det_bounds
         StageScope sc(ST_GZERO, st);
-        LSR_HIP(hipMemsetAsync(ws, 0, 256 + rows + lang, st));
+        LSR_HIP(hipMemsetAsync(ws + hdr, 0, rows + lang, st));
     }
     StageScope sc(ST_DET_BOUNDS, st);
     LSR_HIP(launch_det_bounds(rb, rb.det_bounds, st));

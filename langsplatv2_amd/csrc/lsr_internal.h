@@ -123,6 +123,10 @@ struct RenderBwdArgs {
     long long* det_lang = nullptr;
     float* det_bounds = nullptr;
     const int32_t* radii = nullptr;
+    // per Gaussian, the four column classes' shifts as signed bytes (class k in
+    // byte k), written by launch_det_bounds and read by the adds and the
+    // conversion alike
+    uint32_t* det_sh = nullptr;
 };
 bool bwd_lang_direct(int D);  // D for which the full backward supports lang_acc
 int grad_row_width(int D);   // VP for a dense language dim
@@ -136,7 +140,10 @@ hipError_t launch_render_bwd_lang_sparse(const RenderBwdArgs& a, hipStream_t st)
 int lang_set_for(int D);     // compiled channel set >= D, or -1
 // LSR_OPT_DETERMINISTIC: bounds = {max |dL/dout| over the 3 + D planes,
 // max |feature| over the visible Gaussians' colours and the dense language input,
-// flag} (bounds zeroed by the caller; flag bit 0: a non-finite value)
+// flag} (flag bit 0: a non-finite value).  bounds points at LSR_DET_HDR bytes:
+// the 3 words, then the per-block partials (every word written, no atomics)
+constexpr int LSR_DET_BLOCKS = 4096;
+constexpr size_t LSR_DET_HDR = 256 + 3 * 4 * LSR_DET_BLOCKS;
 hipError_t launch_det_bounds(const RenderBwdArgs& b, float* bounds, hipStream_t st);
 // the fixed-point sums back to fp32: rows (P, VP) -> grad_out (every element
 // written; VP = 16 with lang_direct), lang (P, D) -> lang_out; lang_only: rows

@@ -2222,12 +2222,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_wav
                     // fixed-point twins of the rows (det_shift above): the same
                     // values, order-independent sums
                     uint32_t* const dflag = reinterpret_cast<uint32_t*>(b.det_bounds + 2);
-                    const float dDm = b.det_bounds[0];
-                    const float dAm = (2.f * (float)(3 + D) * b.det_bounds[1] + (fabsf(c.bg[0]) + fabsf(c.bg[1]) + fabsf(c.bg[2]))) * dDm;
-                    const float dWH = (float)max(c.W, c.H);
-                    int rq[4];
+                    uint32_t sq[4];
 #pragma unroll
-                    for (int q = 0; q < 4; q++) rq[q] = slot_of(q) < kn ? b.radii[gq[q]] : 1;
+                    for (int q = 0; q < 4; q++) sq[q] = slot_of(q) < kn ? b.det_sh[gq[q]] : 0u;
 #pragma unroll
                     for (int h = 0; h < GRL; h++) {
                         const int f = 16 * h + li;
@@ -2239,7 +2236,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_wav
                         for (int q = 0; q < 4; q++) {
                             const float v = vq[h][q];
                             if (fcol & (slot_of(q) < kn) & (v != 0.f)) {
-                                const int sh = det_shift(cls, rq[q], dDm, dAm, dWH);
+                                const int sh = (int)(int8_t)(sq[q] >> (8 * cls));
                                 if (LD && h > 0)
                                     det_add(b.det_lang + (size_t)gq[q] * D + (f - 16), v, sh, dflag);
                                 else
@@ -2313,6 +2310,7 @@ hipError_t launch_render_bwd_lang(const RenderBwdArgs& b, hipStream_t st)
 {
     const int T = b.f.cam.gx * b.f.cam.gy;
     if (T == 0) return hipSuccess;
+    if (b.det_rows && (!b.det_bounds || !b.det_sh)) return hipErrorInvalidValue;
     // LST: the forward's per-block candidate lists (RenderArgs::listA); DET: fixed-point sums
 #define LSR_BWD_LO(NL)                                                                                           \
     (b.det_rows ? (b.f.listA ? k_render_bwd_mf<NL, true, false, false, true, true><<<4 * T, 64, 0, st>>>(b)     \
@@ -2360,7 +2358,7 @@ hipError_t launch_render_bwd(const RenderBwdArgs& b, hipStream_t st)
     // LST: the forward's per-block candidate lists (RenderArgs::listA)
     const bool lst = b.f.listA != nullptr;
     const bool det = b.det_rows != nullptr;
-    if (det && (!b.det_bounds || !b.radii || ((b.lang_acc != nullptr) != (b.det_lang != nullptr))))
+    if (det && (!b.det_bounds || !b.det_sh || ((b.lang_acc != nullptr) != (b.det_lang != nullptr))))
         return hipErrorInvalidValue;
     if (b.lang_acc) {
         if (!bwd_lang_direct(b.f.D) || (uintptr_t)b.f.lang % 16 != 0) return hipErrorInvalidValue;
@@ -2425,8 +2423,7 @@ __global__ void __launch_bounds__(256) k_det_bounds(const float* __restrict__ dc
         const uint32_t n4 = al ? n / 4 : 0;
         const float4* s4 = reinterpret_cast<const float4*>(src);
         uint32_t e = b0;
-        // 8 independent loads in flight per lane (one at a time left the pass
-        // latency-bound: 0.095 ms for 0.23 GB)
+        // 8 independent loads in flight per lane
         for (; e + 7 * stride < n4; e += 8 * stride) {
             float4 v[8];
 #pragma unroll
@@ -2459,8 +2456,9 @@ __global__ void __launch_bounds__(256) k_det_bounds(const float* __restrict__ dc
             }
         }
     }
-    // one atomic per block and word (same-address atomics serialise: one per
-    // wave over ~6 K blocks cost 0.3 ms)
+    // the block's partial to its own slot (same-address atomics serialise: one
+    // per wave over ~6 K blocks cost 0.3 ms, one per block over 1.3 K 0.05 ms);
+    // k_det_reduce folds the slots
     __shared__ float smd[4], smf[4];
     __shared__ uint32_t sbad[4];
     md = wave_max_f(md);
@@ -2474,11 +2472,64 @@ __global__ void __launch_bounds__(256) k_det_bounds(const float* __restrict__ dc
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        const float bm = fmaxf(fmaxf(smd[0], smd[1]), fmaxf(smd[2], smd[3]));
-        const float bf = fmaxf(fmaxf(smf[0], smf[1]), fmaxf(smf[2], smf[3]));
-        if (bm > 0.f) atomicMax(reinterpret_cast<unsigned int*>(bounds), __float_as_uint(bm));
-        if (bf > 0.f) atomicMax(reinterpret_cast<unsigned int*>(bounds + 1), __float_as_uint(bf));
-        if (sbad[0] | sbad[1] | sbad[2] | sbad[3]) atomicOr(reinterpret_cast<unsigned int*>(bounds + 2), 1u);
+        float* part = bounds + 64;
+        part[blockIdx.x] = fmaxf(fmaxf(smd[0], smd[1]), fmaxf(smd[2], smd[3]));
+        part[LSR_DET_BLOCKS + blockIdx.x] = fmaxf(fmaxf(smf[0], smf[1]), fmaxf(smf[2], smf[3]));
+        reinterpret_cast<uint32_t*>(part)[2 * LSR_DET_BLOCKS + blockIdx.x] = sbad[0] | sbad[1] | sbad[2] | sbad[3];
+    }
+}
+
+// per Gaussian, det_shift of the four column classes as signed bytes (the
+// adds and the conversion read the same table, so their exponents agree by
+// construction)
+__global__ void __launch_bounds__(256) k_det_shifts(const int32_t* __restrict__ radii, const float* __restrict__ bounds,
+                                                    int P, int D, const float* __restrict__ bg, float WH,
+                                                    uint32_t* __restrict__ sh)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const float Dm = bounds[0];
+    const float Am = (2.f * (float)(3 + D) * bounds[1] + (fabsf(bg[0]) + fabsf(bg[1]) + fabsf(bg[2]))) * Dm;
+    const int r = radii[i];
+    uint32_t w = 0u;
+#pragma unroll
+    for (int cls = 0; cls < 4; cls++) w |= ((uint32_t)det_shift(cls, r, Dm, Am, WH) & 0xffu) << (8 * cls);
+    sh[i] = w;
+}
+
+// one block: the nb partials -> bounds[0..2]
+__global__ void __launch_bounds__(1024) k_det_reduce(float* bounds, int nb)
+{
+    const float* part = bounds + 64;
+    float md = 0.f, mf = 0.f;
+    uint32_t bad = 0u;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+        md = fmaxf(md, part[i]);
+        mf = fmaxf(mf, part[LSR_DET_BLOCKS + i]);
+        bad |= reinterpret_cast<const uint32_t*>(part)[2 * LSR_DET_BLOCKS + i];
+    }
+    __shared__ float smd[16], smf[16];
+    __shared__ uint32_t sbad[16];
+    md = wave_max_f(md);
+    mf = wave_max_f(mf);
+    const bool wbad = wave_ballot(bad != 0u) != 0u;
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        smd[w] = md;
+        smf[w] = mf;
+        sbad[w] = wbad ? 1u : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int nw = (int)(blockDim.x + 63) / 64;
+        for (int k = 1; k < nw; k++) {
+            md = fmaxf(md, smd[k]);
+            mf = fmaxf(mf, smf[k]);
+            sbad[0] |= sbad[k];
+        }
+        bounds[0] = md;
+        bounds[1] = mf;
+        reinterpret_cast<uint32_t*>(bounds)[2] = sbad[0];
     }
 }
 
@@ -2487,13 +2538,20 @@ hipError_t launch_det_bounds(const RenderBwdArgs& b, float* bounds, hipStream_t 
     const size_t HW = (size_t)b.f.cam.W * b.f.cam.H;
     const int D = b.f.D;
     if (D > 0 && (!b.dout_lang || !b.f.lang)) return hipErrorInvalidValue;
+    if (!b.det_sh || !b.radii) return hipErrorInvalidValue;
     const size_t nf = (size_t)b.f.P * (size_t)(D > 0 ? D : 0);
     if (3 * HW >= (1ull << 32) || (size_t)D * HW >= (1ull << 32) || nf >= (1ull << 32)) return hipErrorInvalidValue;
+    // one Gaussian per colour thread: a strided loop over P there is a chain of
+    // dependent radius -> colour loads (256 blocks of it measured 0.096 ms)
     const int nbd = 1024;
-    const int nbf = std::min((b.f.P + 255) / 256, 256);
+    const int nbf = std::max(1, std::min((b.f.P + 255) / 256, LSR_DET_BLOCKS - nbd));
     k_det_bounds<<<nbd + nbf, 256, 0, st>>>(b.dout_color, D > 0 ? b.dout_lang : nullptr, (uint32_t)(3 * HW),
                                             (uint32_t)((size_t)D * HW), nbd, D > 0 ? b.f.lang : nullptr,
                                             (uint32_t)nf, b.f.rgb, b.radii, b.f.P, bounds);
+    k_det_reduce<<<1, 1024, 0, st>>>(bounds, nbd + nbf);
+    if (b.f.P > 0)
+        k_det_shifts<<<(b.f.P + 255) / 256, 256, 0, st>>>(b.radii, bounds, b.f.P, D, b.f.cam.bg,
+                                                          (float)std::max(b.f.cam.W, b.f.cam.H), b.det_sh);
     return hipGetLastError();
 }
 
@@ -2503,17 +2561,16 @@ hipError_t launch_det_bounds(const RenderBwdArgs& b, float* bounds, hipStream_t 
 // -> lout; mode 2 (language only): rows (P, D) -> lout.  Every element of the
 // outputs is written (unused row slots 0).  One thread per (Gaussian, 4
 // columns), 32-bit index arithmetic.
-__device__ __forceinline__ float det_value(long long acc, int cls, int r, float Dm, float Am, float WH)
+__device__ __forceinline__ float det_value(long long acc, int s)
 {
-    return acc != 0 ? (float)ldexp((double)acc, -det_shift(cls, r, Dm, Am, WH)) : 0.f;
+    return acc != 0 ? (float)ldexp((double)acc, -s) : 0.f;
 }
 
 __global__ void __launch_bounds__(256) k_det_finish(const long long* __restrict__ rows,
                                                     const long long* __restrict__ lang,
-                                                    const int32_t* __restrict__ radii,
+                                                    const uint32_t* __restrict__ shifts,
                                                     const float* __restrict__ bounds, int P, int VP, int D, int mode,
-                                                    const float* __restrict__ bg, float WH, float* __restrict__ gout,
-                                                    float* __restrict__ lout)
+                                                    float* __restrict__ gout, float* __restrict__ lout)
 {
     // column quads per Gaussian: the row part, then (mode 1) the language part
     const int wr = mode == 2 ? D : VP;
@@ -2524,11 +2581,8 @@ __global__ void __launch_bounds__(256) k_det_finish(const long long* __restrict_
     const uint32_t i = t / (uint32_t)qn;
     if (i >= (uint32_t)P) return;
     const int q = (int)(t - i * (uint32_t)qn);
-    const float Dm = bounds[0];
-    // the render backward's Am, the same expression (the exponents must agree bit for bit)
-    const float Am = (2.f * (float)(3 + D) * bounds[1] + (fabsf(bg[0]) + fabsf(bg[1]) + fabsf(bg[2]))) * Dm;
     const bool bad = (__float_as_uint(bounds[2]) & 1u) != 0u;
-    const int r = radii[i];
+    const uint32_t sw = shifts[i];   // the exponents the adds used
     const bool in_rows = q < qr;
     const int c0 = 4 * (in_rows ? q : q - qr);
     const int w = in_rows ? wr : D;
@@ -2545,7 +2599,7 @@ __global__ void __launch_bounds__(256) k_det_finish(const long long* __restrict_
             cls = det_class_of(col);
         }
         const long long acc = used ? src[col] : 0;
-        v[k] = bad ? __builtin_nanf("") : det_value(acc, cls, r, Dm, Am, WH);
+        v[k] = bad ? __builtin_nanf("") : det_value(acc, (int)(int8_t)(sw >> (8 * cls)));
     }
     if (c0 + 4 <= w && ((uintptr_t)(dst + c0) & 15u) == 0) {
         *reinterpret_cast<float4*>(dst + c0) = make_float4(v[0], v[1], v[2], v[3]);
@@ -2560,7 +2614,7 @@ hipError_t launch_det_finish(const RenderBwdArgs& b, bool lang_only, float* grad
 {
     const int P = b.f.P, D = b.f.D;
     const int mode = lang_only ? 2 : (b.det_lang ? 1 : 0);
-    if (!b.det_rows || !b.det_bounds || !b.radii || (mode == 0 && !grad_out) || (mode != 0 && !lang_out) ||
+    if (!b.det_rows || !b.det_bounds || !b.det_sh || (mode == 0 && !grad_out) || (mode != 0 && !lang_out) ||
         (mode == 1 && !grad_out))
         return hipErrorInvalidValue;
     const int wr = mode == 2 ? D : b.VP;
@@ -2568,10 +2622,8 @@ hipError_t launch_det_finish(const RenderBwdArgs& b, bool lang_only, float* grad
     const size_t n = (size_t)P * (size_t)qn;
     if (n == 0) return hipSuccess;
     if (n >= (1ull << 32)) return hipErrorInvalidValue;
-    const Cam& c = b.f.cam;
-    k_det_finish<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(b.det_rows, b.det_lang, b.radii, b.det_bounds, P, b.VP,
-                                                              D, mode, c.bg, (float)std::max(c.W, c.H), grad_out,
-                                                              lang_out);
+    k_det_finish<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(b.det_rows, b.det_lang, b.det_sh, b.det_bounds, P, b.VP,
+                                                              D, mode, grad_out, lang_out);
     return hipGetLastError();
 }
 }  // namespace lsr
