@@ -142,7 +142,7 @@ int lang_set_for(int D);     // compiled channel set >= D, or -1
 // max |feature| over the visible Gaussians' colours and the dense language input,
 // flag} (flag bit 0: a non-finite value).  bounds points at LSR_DET_HDR bytes:
 // the 3 words, then the per-block partials (every word written, no atomics)
-constexpr int LSR_DET_BLOCKS = 4096;
+constexpr int LSR_DET_BLOCKS = 32768;
 constexpr size_t LSR_DET_HDR = 256 + 3 * 4 * LSR_DET_BLOCKS;
 hipError_t launch_det_bounds(const RenderBwdArgs& b, float* bounds, hipStream_t st);
 // the fixed-point sums back to fp32: rows (P, VP) -> grad_out (every element

@@ -2398,9 +2398,10 @@ hipError_t launch_render_bwd(const RenderBwdArgs& b, hipStream_t st)
 
 // ------------------------------------------ deterministic backward: bounds
 // max |dL/dout| over the 3 + D upstream planes and max |feature| over the
-// visible Gaussians' colours and the dense language input (order-independent:
-// atomicMax on the bits of non-negative floats); bit 0 of word 2 flags a
-// non-finite value.  Blocks [0, nbd) stream the planes as float4; the rest take
+// visible Gaussians' colours and the dense language input (order-independent);
+// bit 0 of word 2 flags a non-finite value.  Blocks [0, nbd) read the three
+// arrays as one float4 index space, 8 loads in flight per lane (a strided loop
+// per array left a chain of dependent rounds); blocks below gridDim - nbd take
 // one visible Gaussian's row per thread.
 __device__ __forceinline__ void det_max4(float4 v, float& m, bool& bad)
 {
@@ -2416,38 +2417,56 @@ __global__ void __launch_bounds__(256) k_det_bounds(const float* __restrict__ dc
 {
     float md = 0.f, mf = 0.f;
     bool bad = false;
-    // a flat float array's max |v| (float4 where aligned)
-    auto scan = [&](const float* src, uint32_t n, uint32_t b0, uint32_t stride, float& m) {
-        if (!src || n == 0) return;
-        const bool al = ((uintptr_t)src & 15u) == 0;
-        const uint32_t n4 = al ? n / 4 : 0;
-        const float4* s4 = reinterpret_cast<const float4*>(src);
-        uint32_t e = b0;
-        // 8 independent loads in flight per lane
-        for (; e + 7 * stride < n4; e += 8 * stride) {
-            float4 v[8];
+    // the colour blocks first (their dependent radius -> colour loads then
+    // overlap the stream instead of trailing it)
+    const int nbf = (int)gridDim.x - nbd;
+    const int blk = (int)blockIdx.x - nbf;
+    if (blk >= 0) {
+        // float4 parts of the aligned arrays: [colour planes | language planes | language input]
+        auto n4 = [](const float* p, uint32_t n) { return (p && ((uintptr_t)p & 15u) == 0) ? n / 4 : 0u; };
+        const uint32_t N1 = n4(dc, ncol), N2 = N1 + n4(dl, nlang), N3 = N2 + n4(lang, nfeat);
+        const float4* c4 = reinterpret_cast<const float4*>(dc);
+        const float4* l4 = reinterpret_cast<const float4*>(dl);
+        const float4* f4 = reinterpret_cast<const float4*>(lang);
+        // block chunks of 4 x 256 consecutive float4 (a copy's access pattern)
+        const uint32_t nch = (N3 + 1023) / 1024;
+        for (uint32_t ch = (uint32_t)blk; ch < nch; ch += (uint32_t)nbd) {
+            float4 v[4];
+            uint32_t ec[4];
 #pragma unroll
-            for (int k = 0; k < 8; k++) v[k] = s4[e + k * stride];
+            for (int k = 0; k < 4; k++) {
+                // branch-free: past the end, lanes re-read the last element (a
+                // real one, counted where it belongs)
+                ec[k] = min(ch * 1024u + (uint32_t)k * 256u + threadIdx.x, N3 - 1);
+                const float4* q = ec[k] < N1 ? c4 + ec[k] : (ec[k] < N2 ? l4 + (ec[k] - N1) : f4 + (ec[k] - N2));
+                v[k] = *q;
+            }
 #pragma unroll
-            for (int k = 0; k < 8; k++) det_max4(v[k], m, bad);
+            for (int k = 0; k < 4; k++) {
+                const bool isd = ec[k] < N2;
+                float m = isd ? md : mf;
+                det_max4(v[k], m, bad);
+                md = isd ? m : md;
+                mf = isd ? mf : m;
+            }
         }
-        for (; e < n4; e += stride) det_max4(s4[e], m, bad);
-        for (uint32_t e = 4 * n4 + b0; e < n; e += stride) {
-            const float v = src[e];
-            bad |= !isfinite(v);
-            m = fmaxf(m, fabsf(v));
-        }
-    };
-    if ((int)blockIdx.x < nbd) {
-        // the upstream planes (colour, then language) and the dense language input
-        const uint32_t stride = (uint32_t)nbd * blockDim.x, b0 = blockIdx.x * blockDim.x + threadIdx.x;
-        scan(dc, ncol, b0, stride, md);
-        scan(dl, nlang, b0, stride, md);
-        scan(lang, nfeat, b0, stride, mf);
+        const uint32_t stride = (uint32_t)nbd * blockDim.x, b0 = (uint32_t)blk * blockDim.x + threadIdx.x;
+        // the scalar rest: tails past the float4 parts, or a whole misaligned array
+        auto rest = [&](const float* p, uint32_t n, float& m) {
+            if (!p) return;
+            for (uint32_t e = 4 * n4(p, n) + b0; e < n; e += stride) {
+                const float x = p[e];
+                bad |= !isfinite(x);
+                m = fmaxf(m, fabsf(x));
+            }
+        };
+        rest(dc, ncol, md);
+        rest(dl, nlang, md);
+        rest(lang, nfeat, mf);
     } else {
         // the colours of the visible Gaussians (a culled Gaussian's colour is never written)
-        const int stride = ((int)gridDim.x - nbd) * (int)blockDim.x;
-        for (int i = ((int)blockIdx.x - nbd) * (int)blockDim.x + (int)threadIdx.x; i < P; i += stride) {
+        const int stride = nbf * (int)blockDim.x;
+        for (int i = (int)blockIdx.x * (int)blockDim.x + (int)threadIdx.x; i < P; i += stride) {
             if (radii[i] <= 0) continue;
             for (int c = 0; c < 3; c++) {
                 const float v = rgb[3 * (size_t)i + c];
@@ -2541,10 +2560,10 @@ hipError_t launch_det_bounds(const RenderBwdArgs& b, float* bounds, hipStream_t 
     if (!b.det_sh || !b.radii) return hipErrorInvalidValue;
     const size_t nf = (size_t)b.f.P * (size_t)(D > 0 ? D : 0);
     if (3 * HW >= (1ull << 32) || (size_t)D * HW >= (1ull << 32) || nf >= (1ull << 32)) return hipErrorInvalidValue;
-    // one Gaussian per colour thread: a strided loop over P there is a chain of
-    // dependent radius -> colour loads (256 blocks of it measured 0.096 ms)
-    const int nbd = 1024;
-    const int nbf = std::max(1, std::min((b.f.P + 255) / 256, LSR_DET_BLOCKS - nbd));
+    // one 16-KB chunk per scan block; one Gaussian per colour thread
+    const size_t n4 = (3 * HW + (size_t)D * HW + nf) / 4;
+    const int nbd = (int)std::max<size_t>(1, std::min<size_t>((n4 + 1023) / 1024, LSR_DET_BLOCKS - LSR_DET_BLOCKS / 4));
+    const int nbf = std::max(1, std::min((b.f.P + 255) / 256, LSR_DET_BLOCKS / 4));
     k_det_bounds<<<nbd + nbf, 256, 0, st>>>(b.dout_color, D > 0 ? b.dout_lang : nullptr, (uint32_t)(3 * HW),
                                             (uint32_t)((size_t)D * HW), nbd, D > 0 ? b.f.lang : nullptr,
                                             (uint32_t)nf, b.f.rgb, b.radii, b.f.P, bounds);

@@ -1,4 +1,5 @@
-"""Minimal workload for PMC collection: a few cfg3 fwd+bwd steps, or (LSR_QUICK=1)
+"""Minimal workload for PMC collection: a few cfg3 fwd+bwd steps (LSR_DET=1: with the
+deterministic backward), or (LSR_QUICK=1)
 quick-path forwards at 1280x800 with 1M Gaussians (K=12 sparse codes, Dq=192), each followed
 by the 3 x 64 x 512 codebook decode + L2 norm."""
 import os
@@ -48,6 +49,9 @@ g["means2D"] = torch.zeros_like(g["means3D"], requires_grad=True)
 r = GaussianRasterizer(bench.settings(cam, dev, 3, True))
 dc = torch.randn(3, cfg["H"], cfg["W"], device=dev)
 dl = torch.randn(D, cfg["H"], cfg["W"], device=dev)
+if os.environ.get("LSR_DET", "0") == "1":   # the deterministic backward (LSR_OPT_DETERMINISTIC)
+    from langsplatv2_amd import _lib
+    _lib.set_deterministic(True)
 for _ in range(steps):
     with torch.set_grad_enabled(cfg["backward"]):   # cfg5 is forward-only
         c, l, _ = r(means3D=g["means3D"], means2D=g["means2D"], opacities=g["opacities"], shs=g["shs"],
