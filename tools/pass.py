@@ -16,7 +16,8 @@ Steps (run in order; outputs under gpurun_out/, named TAG_*):
     profq          the same over the quick path only (tools/pmc_step.py LSR_QUICK=1)
     pmc            cfg3: two SQ issue passes + FETCH_SIZE / WRITE_SIZE passes over
                    tools/pmc_step.py -> TAG_pmc_issue.json, TAG_pmc_traffic.json
-    pmcdet         pmc's four passes with the deterministic backward -> TAG_det_pmc_*.json
+    pmcdet         pmc's four passes with the deterministic backward -> det_TAG_pmc_*.json
+                   (named apart from the r* files bench.py reads)
     pmc2 pmc5      FETCH / WRITE passes at cfg2 / cfg5 -> cfgN_TAG_pmc_traffic.json
     rehearse2      bench.py --gpus 2 on the one-GPU box (gloo exchange, both ranks on cuda:0)
     ab:NAME=LIB,.. tools/ab.py A/B of library variants (tools/variant.py builds them)
@@ -151,14 +152,14 @@ def step(tag, s):
         s2 = rocprof(tag, "dsq2", SQ2, prog, env=env)
         fF = rocprof(tag, "dpmcF", "FETCH_SIZE", prog, env=env)
         fW = rocprof(tag, "dpmcW", "WRITE_SIZE", prog, env=env)
-        with open(os.path.join(OUT, f"{tag}_det_pmc_issue.txt"), "w") as f:
-            subprocess.call([PY, "tools/pmc_issue.py", s1, s2, os.path.join(OUT, f"{tag}_det_pmc_issue.json")],
+        with open(os.path.join(OUT, f"det_{tag}_pmc_issue.txt"), "w") as f:
+            subprocess.call([PY, "tools/pmc_issue.py", s1, s2, os.path.join(OUT, f"det_{tag}_pmc_issue.json")],
                             cwd=ROOT, stdout=f)
-        with open(os.path.join(OUT, f"{tag}_det_pmc_traffic.txt"), "w") as f:
-            subprocess.call([PY, "tools/pmc_traffic.py", fF, fW, os.path.join(OUT, f"{tag}_det_pmc_traffic.json")],
+        with open(os.path.join(OUT, f"det_{tag}_pmc_traffic.txt"), "w") as f:
+            subprocess.call([PY, "tools/pmc_traffic.py", fF, fW, os.path.join(OUT, f"det_{tag}_pmc_traffic.json")],
                             cwd=ROOT, stdout=f)
-        tail(os.path.join(OUT, f"{tag}_det_pmc_issue.txt"), 12)
-        tail(os.path.join(OUT, f"{tag}_det_pmc_traffic.txt"), 12)
+        tail(os.path.join(OUT, f"det_{tag}_pmc_issue.txt"), 12)
+        tail(os.path.join(OUT, f"det_{tag}_pmc_traffic.txt"), 12)
     elif s in ("pmc2", "pmc5"):
         n = s[3:]
         prog = ["python3", os.path.join(ROOT, "tools", "pmc_step.py")]
