@@ -784,7 +784,8 @@ void lso_render_bwd(const lso_settings* s, const lso_inputs* in, const lso_geom*
 static void render_tile_bwd_bound(const lso_settings* s, const lso_inputs* in, const lso_geom* g,
                                   const uint32_t* point_list, const uint32_t* ranges, int tile,
                                   const float* final_Ts, const uint32_t* n_contrib,
-                                  const float* dout_color, const float* dout_lang, dacc_t* A, int atomic)
+                                  const float* dout_color, const float* dout_lang, dacc_t* A, dacc_t* M,
+                                  int32_t* seen_tile, uint8_t* seen_mask, double* nblk, int atomic)
 {
     const int W = s->W, H = s->H;
     const int gx = (W + TILE - 1) / TILE;
@@ -845,6 +846,18 @@ static void render_tile_bwd_bound(const lso_settings* s, const lso_inputs* in, c
                 last_alpha = alpha;
                 last_dot = dot;
                 last_dabs = dabs;
+                if (nblk) {
+                    /* the 8x8 blocks j has a contributing pixel in (the cross-block sum's terms) */
+                    const uint8_t bit = (uint8_t)(1u << (((py >> 3) & 1) * 2 + ((px >> 3) & 1)));
+                    if (seen_tile[j] != tile) {
+                        seen_tile[j] = tile;
+                        seen_mask[j] = 0;
+                    }
+                    if (!(seen_mask[j] & bit)) {
+                        seen_mask[j] |= bit;
+                        acc_add(&nblk[j], 1.0, atomic);
+                    }
+                }
                 const double eaT = eT + 16.0 + 72.0;   /* + the product and the block sum */
                 for (int ch = 0; ch < 3; ch++) acc_add(&A->dcolor[3 * (size_t)j + ch], eaT * fabs(aT * Gc[ch]), atomic);
                 for (int k = 0; k < D; k++) acc_add(&A->dlang[(size_t)j * D + k], eaT * fabs(aT * Gl[k]), atomic);
@@ -862,45 +875,81 @@ static void render_tile_bwd_bound(const lso_settings* s, const lso_inputs* in, c
                 acc_add(&A->dconic[3 * (size_t)j + 0], 0.5 * (VE * adx * adx + 72.0 * o * Ub * AX * AX), atomic);
                 acc_add(&A->dconic[3 * (size_t)j + 1], VE * adx * ady + 72.0 * o * Ub * AX * AY, atomic);
                 acc_add(&A->dconic[3 * (size_t)j + 2], 0.5 * (VE * ady * ady + 72.0 * o * Ub * AY * AY), atomic);
+                if (M) {
+                    /* the terms' magnitudes (geometry: factorised forms), in units of 1 */
+                    for (int ch = 0; ch < 3; ch++) acc_add(&M->dcolor[3 * (size_t)j + ch], fabs(aT * Gc[ch]), atomic);
+                    for (int k = 0; k < D; k++) acc_add(&M->dlang[(size_t)j * D + k], fabs(aT * Gl[k]), atomic);
+                    acc_add(&M->dopacity[j], Ub, atomic);
+                    acc_add(&M->dmean2D[3 * (size_t)j + 0], hW * o * Ub * (ca * AX + cb * AY), atomic);
+                    acc_add(&M->dmean2D[3 * (size_t)j + 1], hH * o * Ub * (cb * AX + cc * AY), atomic);
+                    acc_add(&M->dconic[3 * (size_t)j + 0], 0.5 * o * Ub * AX * AX, atomic);
+                    acc_add(&M->dconic[3 * (size_t)j + 1], o * Ub * AX * AY, atomic);
+                    acc_add(&M->dconic[3 * (size_t)j + 2], 0.5 * o * Ub * AY * AY, atomic);
+                }
             }
         }
     free(Gl);
+}
+
+static void dacc_alloc(dacc_t* A, int N, int D)
+{
+    A->dmean2D = (double*)calloc((size_t)N * 3 + 1, sizeof(double));
+    A->dconic = (double*)calloc((size_t)N * 3 + 1, sizeof(double));
+    A->dopacity = (double*)calloc((size_t)N + 1, sizeof(double));
+    A->dcolor = (double*)calloc((size_t)N * 3 + 1, sizeof(double));
+    A->dlang = (double*)calloc((size_t)N * (D > 0 ? D : 1) + 1, sizeof(double));
+}
+
+static void dacc_store(const dacc_t* A, int N, int D, double scale, lso_render_grads* out)
+{
+    for (size_t i = 0; i < (size_t)N * 3; i++) {
+        out->dmean2D[i] = (i % 3 == 2) ? 0.f : (float)(scale * A->dmean2D[i]);
+        out->dconic[i] = (float)(scale * A->dconic[i]);
+        out->dcolor[i] = (float)(scale * A->dcolor[i]);
+    }
+    for (int i = 0; i < N; i++) out->dopacity[i] = (float)(scale * A->dopacity[i]);
+    if (out->dlang && D)
+        for (size_t i = 0; i < (size_t)N * D; i++) out->dlang[i] = (float)(scale * A->dlang[i]);
+    free(A->dmean2D); free(A->dconic); free(A->dopacity); free(A->dcolor); free(A->dlang);
 }
 
 void lso_render_bwd_bound_tiles_mt(const lso_settings* s, const lso_inputs* in, const lso_geom* g,
                                    const uint32_t* point_list, const uint32_t* ranges, const int32_t* tiles,
                                    int ntiles, const float* final_T, const uint32_t* n_contrib,
                                    const float* dout_color, const float* dout_lang, lso_render_grads* bound,
-                                   int nthreads)
+                                   lso_render_grads* mag, float* nblocks, int nthreads)
 {
     const int N = in->N;
     const int D = s->include_feature ? in->D : 0;
     const double u = 5.9604644775390625e-08; /* 2^-24 */
-    dacc_t A;
-    A.dmean2D = (double*)calloc((size_t)N * 3 + 1, sizeof(double));
-    A.dconic = (double*)calloc((size_t)N * 3 + 1, sizeof(double));
-    A.dopacity = (double*)calloc((size_t)N + 1, sizeof(double));
-    A.dcolor = (double*)calloc((size_t)N * 3 + 1, sizeof(double));
-    A.dlang = (double*)calloc((size_t)N * (D > 0 ? D : 1) + 1, sizeof(double));
-    if (nthreads <= 1) {
+    dacc_t A, M;
+    dacc_alloc(&A, N, D);
+    if (mag) dacc_alloc(&M, N, D);
+    double* nb = nblocks ? (double*)calloc((size_t)N + 1, sizeof(double)) : NULL;
+    const int nt = nthreads <= 1 ? 1 : nthreads;
+#pragma omp parallel num_threads(nt) if (nt > 1)
+    {
+        /* per thread: the tile and 4-block mask j was last counted in */
+        int32_t* seen_tile = NULL;
+        uint8_t* seen_mask = NULL;
+        if (nb) {
+            seen_tile = (int32_t*)malloc(sizeof(int32_t) * ((size_t)N + 1));
+            seen_mask = (uint8_t*)calloc((size_t)N + 1, 1);
+            for (int i = 0; i < N; i++) seen_tile[i] = -1;
+        }
+#pragma omp for schedule(dynamic, 4)
         for (int k = 0; k < ntiles; k++)
             render_tile_bwd_bound(s, in, g, point_list, ranges, tiles[k], final_T, n_contrib, dout_color, dout_lang,
-                                  &A, 0);
-    } else {
-#pragma omp parallel for schedule(dynamic, 4) num_threads(nthreads)
-        for (int k = 0; k < ntiles; k++)
-            render_tile_bwd_bound(s, in, g, point_list, ranges, tiles[k], final_T, n_contrib, dout_color, dout_lang,
-                                  &A, 1);
+                                  &A, mag ? &M : NULL, seen_tile, seen_mask, nb, nt > 1);
+        free(seen_tile);
+        free(seen_mask);
     }
-    for (size_t i = 0; i < (size_t)N * 3; i++) {
-        bound->dmean2D[i] = (i % 3 == 2) ? 0.f : (float)(u * A.dmean2D[i]);
-        bound->dconic[i] = (float)(u * A.dconic[i]);
-        bound->dcolor[i] = (float)(u * A.dcolor[i]);
+    dacc_store(&A, N, D, u, bound);
+    if (mag) dacc_store(&M, N, D, 1.0, mag);
+    if (nb) {
+        for (int i = 0; i < N; i++) nblocks[i] = (float)nb[i];
+        free(nb);
     }
-    for (int i = 0; i < N; i++) bound->dopacity[i] = (float)(u * A.dopacity[i]);
-    if (bound->dlang && D)
-        for (size_t i = 0; i < (size_t)N * D; i++) bound->dlang[i] = (float)(u * A.dlang[i]);
-    free(A.dmean2D); free(A.dconic); free(A.dopacity); free(A.dcolor); free(A.dlang);
 }
 
 /* ------------------------------------------------------ preprocess bwd -- */

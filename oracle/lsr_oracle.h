@@ -153,12 +153,15 @@ void lso_render_bwd_tiles_mt(const lso_settings* s, const lso_inputs* in, const 
 /* A-priori bound of |product deterministic backward - this oracle| per
  * render-gradient element (the same fields as lso_render_grads); see the
  * derivation at its definition.  Excludes the fixed-point rounding and the
- * two final fp32 roundings, which the caller adds. */
+ * two final fp32 roundings, which the caller adds.  Optional (NULL: skipped):
+ * mag = each element's sum of |term| (geometry terms in their factorised form),
+ * nblocks = per Gaussian, the 8x8 blocks it has a contributing pixel in; the
+ * default float-atomic cross-block sum adds at most nblocks u mag. */
 void lso_render_bwd_bound_tiles_mt(const lso_settings* s, const lso_inputs* in, const lso_geom* g,
                                    const uint32_t* point_list, const uint32_t* ranges, const int32_t* tiles,
                                    int ntiles, const float* final_T, const uint32_t* n_contrib,
                                    const float* dout_color, const float* dout_lang, lso_render_grads* bound,
-                                   int nthreads);
+                                   lso_render_grads* mag, float* nblocks, int nthreads);
 
 typedef struct {
     float* dmeans3D;  /* N*3 */

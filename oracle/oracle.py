@@ -244,27 +244,42 @@ def backward(pb: Problem, fwd: dict, dout_color: np.ndarray, dout_lang: np.ndarr
 
 
 def backward_bound(pb: Problem, fwd: dict, dout_color: np.ndarray, dout_lang: np.ndarray | None = None,
-                   nthreads: int = 1) -> dict:
+                   nthreads: int = 1, with_mag: bool = False) -> dict:
     """A-priori bound of |product deterministic backward - oracle| per render-gradient
     element (lso_render_bwd_bound_tiles_mt; dense language input): dmean2D (N,3),
     dconic (N,3), dopacity (N,), dcolor (N,3), dlang (N,D).  Excludes the fixed-point
-    rounding of the block partials and the two final fp32 roundings."""
+    rounding of the block partials and the two final fp32 roundings.  with_mag: also
+    "mag" (the same keys: each element's sum of |term|) and "nblocks" (N,): the 8x8
+    blocks each Gaussian contributes in, for the default float-atomic cross-block sum
+    (at most nblocks u mag more)."""
     lib = load()
     N, D = pb.N, pb.D
     g, geom = fwd["_keep"]
     s, i = pb._structs()
     dcol = _np(dout_color)
     dlang = _np(dout_lang) if (D and dout_lang is not None) else None
-    b = dict(dmean2D=np.zeros((N, 3), np.float32), dconic=np.zeros((N, 3), np.float32),
-             dopacity=np.zeros(N, np.float32), dcolor=np.zeros((N, 3), np.float32),
-             dlang=np.zeros((N, max(D, 1)), np.float32))
-    bs = _RGrads(_p(b["dmean2D"]), _p(b["dconic"]), _p(b["dopacity"]), _p(b["dcolor"]), _p(b["dlang"]) if D else None)
+
+    def grads():
+        b = dict(dmean2D=np.zeros((N, 3), np.float32), dconic=np.zeros((N, 3), np.float32),
+                 dopacity=np.zeros(N, np.float32), dcolor=np.zeros((N, 3), np.float32),
+                 dlang=np.zeros((N, max(D, 1)), np.float32))
+        st = _RGrads(_p(b["dmean2D"]), _p(b["dconic"]), _p(b["dopacity"]), _p(b["dcolor"]), _p(b["dlang"]) if D else None)
+        return b, st
+
+    b, bs = grads()
+    m, ms = grads() if with_mag else (None, None)
+    nbk = np.zeros(N, np.float32) if with_mag else None
     pl = np.ascontiguousarray(fwd["point_list"] if fwd["num_rendered"] > 0 else np.zeros(1, np.uint32))
     tl = np.arange(pb.gx * pb.gy, dtype=np.int32)
     lib.lso_render_bwd_bound_tiles_mt(ctypes.byref(s), ctypes.byref(i), ctypes.byref(geom), _p(pl), _p(fwd["ranges"]),
                                       _p(tl), len(tl), _p(fwd["final_T"]), _p(fwd["n_contrib"]), _p(dcol), _p(dlang),
-                                      ctypes.byref(bs), int(nthreads))
+                                      ctypes.byref(bs), ctypes.byref(ms) if with_mag else None,
+                                      _p(nbk) if with_mag else None, int(nthreads))
     b["dlang"] = b["dlang"][:, :D] if D else None
+    if with_mag:
+        m["dlang"] = m["dlang"][:, :D] if D else None
+        b["mag"] = m
+        b["nblocks"] = nbk
     return b
 
 

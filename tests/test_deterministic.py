@@ -17,7 +17,10 @@ Two levels, both against the C restatement (oracle/lsr_oracle.c):
                  64 bounds the fp32 operations on its longest path; kappa =
                  (|a c| + b^2) / |a c - b^2| of the 2D conic covers the one
                  cancellation in it, the determinant and 1/det^2).
-Together they bound every gradient the rasterizer returns.  u = 2^-24."""
+Together they bound every gradient the rasterizer returns.  u = 2^-24.
+The default backward (fp32 atomics) is held to the same analysis with the
+any-order summation bound nblocks u sum|term| in place of the fixed-point term
+(check_rows(deterministic=False))."""
 import json
 import os
 
@@ -96,24 +99,40 @@ def _check(name, got, ref, tol):
                 median_bound=float(np.median(tol)) if tol.size else 0.0)
 
 
-def check_rows(case, got, oracle_lib, dcol, dlang, nthreads=1):
+def check_rows(case, got, oracle_lib, dcol, dlang, nthreads=1, deterministic=True):
     """The render rows of `got` (run_gpu_bwd_rows) against the oracle within the
-    derived bound; returns the per-quantity max |err| and max |err| / bound."""
+    derived bound; returns the per-quantity max |err| and max |err| / bound.
+    deterministic=False: rows from the default backward, whose cross-block sums
+    are fp32 atomics in arbitrary order -- in place of the fixed-point rounding,
+    the recursive-summation bound of nb partials in any order, nb u sum_b |partial_b|
+    <= nblocks u mag (mag = the element's sum of |term|, nblocks = the 8x8 blocks
+    the Gaussian contributes in; both from the oracle's bound pass)."""
     pb = oracle_problem(case)
     ref = oracle_lib.forward(pb, nthreads=nthreads)
     rb = oracle_lib.backward(pb, ref, dcol, dlang, nthreads=max(nthreads, 2))
-    bd = oracle_lib.backward_bound(pb, ref, dcol, dlang, nthreads=nthreads)
+    bd = oracle_lib.backward_bound(pb, ref, dcol, dlang, nthreads=nthreads, with_mag=not deterministic)
     Dm, Am, WH = _scales(pb, ref, dcol, dlang)
     rows, radii = got["rows"], got["radii"]
     np.testing.assert_array_equal(radii, ref["radii"])
-    qm, qc, qo, q0 = (_quant(radii, c, Dm, Am, WH) for c in (2, 3, 1, 0))
-    res = {"mean2D": _check("mean2D", rows[:, 0:2], rb["dmean2D"][:, :2], bd["dmean2D"][:, :2] + qm[:, None]),
-           "conic": _check("conic", rows[:, 2:5], rb["dconic"], bd["dconic"] + qc[:, None]),
+    if deterministic:
+        qm, qc, qo, q0 = (_quant(radii, c, Dm, Am, WH) for c in (2, 3, 1, 0))
+        ql = q0
+    else:
+        nbu = U * bd["nblocks"].astype(np.float64)
+        mg = bd["mag"]
+        qm = nbu[:, None] * mg["dmean2D"][:, :2]
+        qc = nbu[:, None] * mg["dconic"]
+        qo = nbu * mg["dopacity"]
+        q0 = nbu[:, None] * mg["dcolor"]
+        ql = nbu[:, None] * mg["dlang"] if pb.D else None
+    col = (lambda q: q[:, None]) if deterministic else (lambda q: q)   # per Gaussian / per element
+    res = {"mean2D": _check("mean2D", rows[:, 0:2], rb["dmean2D"][:, :2], bd["dmean2D"][:, :2] + col(qm)),
+           "conic": _check("conic", rows[:, 2:5], rb["dconic"], bd["dconic"] + col(qc)),
            "opacity": _check("opacity", rows[:, 5], rb["dopacity"], bd["dopacity"] + qo),
-           "colour": _check("colour", rows[:, 6:9], rb["dcolor"], bd["dcolor"] + q0[:, None])}
+           "colour": _check("colour", rows[:, 6:9], rb["dcolor"], bd["dcolor"] + col(q0))}
     if pb.D:
         gl = got["grad_language_feature_precomp"]
-        res["language"] = _check("language", gl, rb["dlang"], bd["dlang"] + q0[:, None])
+        res["language"] = _check("language", gl, rb["dlang"], bd["dlang"] + col(ql))
     return pb, ref, res
 
 
@@ -172,6 +191,20 @@ def test_deterministic_backward_within_analytic_bound(gpu, oracle_lib, name):
     pb, ref, r1 = check_rows(case, got, oracle_lib, dcol, dlang)
     r2 = check_chain(pb, ref, got, oracle_lib)
     record(name, {"rows": r1, "chain": r2})
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_default_backward_within_analytic_bound(gpu, oracle_lib, name):
+    """The DEFAULT backward (fp32 atomic cross-block sums) against the same
+    derived bound with the any-order summation term in place of the fixed-point
+    rounding: its tolerance, too, comes from the analysis, not from a fit."""
+    case = make_case(**CASES[name])
+    D = CASES[name]["lang_dim"]
+    dcol, dlang = _upstream(case["cam"]["H"], case["cam"]["W"], D)
+    got = run_gpu_bwd_rows(case, gpu, dcol, dlang, deterministic=False)
+    pb, ref, r1 = check_rows(case, got, oracle_lib, dcol, dlang, deterministic=False)
+    r2 = check_chain(pb, ref, got, oracle_lib)
+    record("default_" + name, {"rows": r1, "chain": r2})
 
 
 @pytest.mark.parametrize("D", [16, 3])

@@ -151,6 +151,21 @@ def test_cfg3_deterministic_backward_whole_frame(gpu, oracle_lib):
     record("cfg3_whole_frame_bench_upstream", {"rows": r1, "chain": r2})
 
 
+def test_cfg3_default_backward_whole_frame_analytic(gpu, oracle_lib):
+    """The headline step's DEFAULT backward (fp32 atomic cross-block sums) on the
+    whole cfg3 frame within the derived bound (check_rows(deterministic=False):
+    the forward-error analysis + the any-order summation term), beside the
+    fitted GRAD_RTOL_FRAME check above."""
+    from harness import run_gpu_bwd_rows
+    from test_deterministic import check_chain, check_rows, record
+    case = _case(3)
+    dcol, dlang = _bench_upstream(1080, 1920, 16)
+    a = run_gpu_bwd_rows(case, gpu, dcol, dlang, deterministic=False)
+    pb, ref, r1 = check_rows(case, a, oracle_lib, dcol, dlang, nthreads=_threads(), deterministic=False)
+    r2 = check_chain(pb, ref, a, oracle_lib)
+    record("default_cfg3_whole_frame_bench_upstream", {"rows": r1, "chain": r2})
+
+
 def test_cfg2_whole_frame(gpu, oracle_lib):
     case = _case(2)
     assert case["g"]["means3D"].shape[0] == 100_000 and case["cam"]["W"] == 800 and case["cam"]["H"] == 800
