@@ -212,7 +212,7 @@ def test_deterministic_language_only_backward(gpu, oracle_lib, D):
     """Feature-mode shape (geometry frozen, only the language input requires
     grad): the language-only kernel in fixed point, bit-reproducible and within
     the bound (D = 3: a width that is not a multiple of the conversion's column
-    quads)."""
+    quads); the default language-only kernel within its derived bound."""
     from diff_gaussian_rasterization import GaussianRasterizer
     from langsplatv2_amd import _lib
     case = make_case(N=20000, W=256, H=192, sh_degree=3, lang_dim=D, seed=7)
@@ -232,10 +232,13 @@ def test_deterministic_language_only_backward(gpu, oracle_lib, D):
     pb = oracle_problem(case)
     ref = oracle_lib.forward(pb)
     rb = oracle_lib.backward(pb, ref, dcol, dlang, nthreads=2)
-    bd = oracle_lib.backward_bound(pb, ref, dcol, dlang)
+    bd = oracle_lib.backward_bound(pb, ref, dcol, dlang, with_mag=True)
     Dm, Am, WH = _scales(pb, ref, dcol, dlang)
     tol = bd["dlang"] + _quant(ref["radii"], 0, Dm, Am, WH)[:, None]
     _check("language (deterministic)", g1, rb["dlang"], tol)
+    # the default (float-atomic) language-only kernel: the any-order summation term
+    tol_f = bd["dlang"] + U * bd["nblocks"].astype(np.float64)[:, None] * bd["mag"]["dlang"]
+    _check("language (default)", gf, rb["dlang"], tol_f)
 
 
 def test_deterministic_quick_weights_only(gpu):
