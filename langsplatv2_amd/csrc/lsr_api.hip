@@ -778,7 +778,8 @@ static GradWs grad_ws_layout(int P, int Dd, bool geom, bool lang, bool lang_alig
 
 // The backward's per-block candidate lists (RenderArgs::listA/B/lcount): A and
 // B arrays of 4 M entries (block b = 4 tile + sub owns [4 tile_start + sub n_tile,
-// + n_tile)), then the 4 T per-block counts.
+// + n_tile)), then the 4 T per-block counts.  The forward that writes them also
+// writes the backward's block order (RenderArgs::border, ImageLayout::border).
 static size_t block_lists_bytes(size_t M, size_t T)
 {
     if (M == 0 || T == 0) return 0;
@@ -790,6 +791,13 @@ static void set_block_lists(RenderArgs& ra, void* lb, size_t M)
     ra.listA = (float4*)p;
     ra.listB = (float4*)(p + align256(4 * M * 16));
     ra.lcount = (uint32_t*)(p + 2 * align256(4 * M * 16));
+}
+// the backward's view of the lists, with the block order the same forward wrote
+static void set_block_lists_bwd(RenderArgs& ra, const void* lb, const void* img, size_t M)
+{
+    set_block_lists(ra, (void*)lb, M);
+    const size_t T = (size_t)ra.cam.gx * ra.cam.gy;
+    if (LSR_BWD_ORDER) ra.border = (const uint32_t*)((const uint8_t*)img + image_layout((size_t)ra.cam.W * ra.cam.H, T).border);
 }
 
 int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, lsr_alloc_fn alloc, void* ctx,
@@ -1004,6 +1012,8 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     }
     LSR_HIP(join.wait());   // the SH colours of a split preprocess
     { StageScope sc(ST_RENDER, st); LSR_HIP(launch_render_fwd(ra, st)); }
+    // the backward's block order from the lists the render just counted
+    if (LSR_BWD_ORDER && ra.lcount) LSR_HIP(launch_bwd_order(ra, (uint32_t*)(img + IL.border), st));
     LSR_DEBUG_SYNC(s, st, "render");
     LSR_GUARD(guard, "out_color", out->out_color, 3 * NPIX);
     LSR_GUARD(guard, "out_lang", out->out_lang, (size_t)(s->quick_render ? quick_dim(s) : Dd) * NPIX);
@@ -1217,7 +1227,7 @@ static int backward_dense(const lsr_settings* s, const lsr_inputs* in, const lsr
         RenderBwdArgs rb;
         rb.f = make_render_args(s, in, c, (const uint8_t*)b->geom, (const uint8_t*)b->binning,
                                 (const uint8_t*)b->image, b->num_rendered);
-        if (b->lists) set_block_lists(rb.f, (void*)b->lists, (size_t)b->num_rendered);
+        if (b->lists) set_block_lists_bwd(rb.f, b->lists, b->image, (size_t)b->num_rendered);
         rb.f.qw = nullptr;
         rb.f.D = Dd;
         rb.f.lang = in->language_feature_precomp;
@@ -1258,7 +1268,7 @@ static int backward_dense(const lsr_settings* s, const lsr_inputs* in, const lsr
     RenderBwdArgs rb;
     rb.f = make_render_args(s, in, c, (const uint8_t*)b->geom, (const uint8_t*)b->binning, (const uint8_t*)b->image,
                             b->num_rendered);
-    if (b->lists) set_block_lists(rb.f, (void*)b->lists, (size_t)b->num_rendered);
+    if (b->lists) set_block_lists_bwd(rb.f, b->lists, b->image, (size_t)b->num_rendered);
     rb.f.qw = nullptr;
     rb.f.D = Dd;
     rb.f.lang = Dd ? in->language_feature_precomp : nullptr;

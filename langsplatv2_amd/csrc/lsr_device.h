@@ -555,7 +555,7 @@ __host__ __device__ inline int table_stride(int T) { return (T + 3) & ~3; }
 
 // Image workspace (per pixel + per tile).
 struct ImageLayout {
-    size_t final_T, n_contrib, tile_cnt, tile_start, tile_part, cls_cnt, cls_list, total;
+    size_t final_T, n_contrib, tile_cnt, tile_start, tile_part, cls_cnt, cls_list, border, total;
 };
 
 __host__ __device__ inline ImageLayout image_layout(size_t P, size_t T)
@@ -570,6 +570,7 @@ __host__ __device__ inline ImageLayout image_layout(size_t P, size_t T)
     L.cls_cnt = o;    o += 512;                        // per-class tile counts (tile-sort classes); word 32: ticket;
                                                        // words 64-65: the tile count's total + arrivals
     L.cls_list = o;   o += align256(T * 6 * 4);        // per-class tile lists, T slots each
+    L.border = o;     o += align256(T * 4 * 4);        // the list-driven backward's block order (k_bwd_order)
     L.total = o;
     return L;
 }

@@ -99,8 +99,16 @@ struct RenderArgs {
     float4* listA = nullptr;   // the candidate's splat record A {x, y, conic.a, conic.b}
     float4* listB = nullptr;   // {conic.c, opacity, id bits, 0-based tile-list position bits}
     uint32_t* lcount = nullptr;
+    // backward only: the blocks in dispatch order, heaviest list first inside
+    // each XCD's range (k_bwd_order; null = band order)
+    const uint32_t* border = nullptr;
 };
 hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st);
+// the backward's block order (RenderArgs::border, 4 T entries) from the forward's lcount
+#ifndef LSR_BWD_ORDER
+#define LSR_BWD_ORDER 1   // list-driven backward: heaviest block lists dispatched first (0: band order)
+#endif
+hipError_t launch_bwd_order(const RenderArgs& a, uint32_t* border, hipStream_t st);
 
 struct RenderBwdArgs {
     RenderArgs f;

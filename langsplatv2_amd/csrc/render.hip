@@ -36,6 +36,9 @@
 #ifndef LSR_BWD_LO_RREG
 #define LSR_BWD_LO_RREG 1   // language-only bwd: atomics straight from the MFMA accumulators (no LDS row tile)
 #endif
+#ifndef LSR_BWD16_WAVES
+#define LSR_BWD16_WAVES 4  // the headline D = 16 list-driven backward: waves per SIMD it is compiled for
+#endif
 #ifndef LSR_MF_WAVES
 #define LSR_MF_WAVES 2      // MFMA render kernels: min waves per SIMD (caps VGPRs at 256)
 #endif
@@ -123,13 +126,99 @@ __device__ __forceinline__ int band_tile(int t, int gx, int gy)
 }
 struct WaveTile {
     int tile, sub;
-    __device__ WaveTile(const RenderArgs& a)
+    // order (the backward's RenderArgs::border): dispatch slot -> block 4 tile + sub
+    __device__ WaveTile(const RenderArgs& a, const uint32_t* order = nullptr)
     {
         const int o = xcd_remap(blockIdx.x, gridDim.x);
-        tile = band_tile(o >> 2, a.cam.gx, a.cam.gy);
-        sub = o & 3;
+        if (order) {
+            const int v = (int)order[o];
+            tile = v >> 2;
+            sub = v & 3;
+        } else {
+            tile = band_tile(o >> 2, a.cam.gx, a.cam.gy);
+            sub = o & 3;
+        }
     }
 };
+
+// The list-driven backward's dispatch order.  A backward wave lasts about
+// 5-8 us per 16-candidate group of its block list at cfg3, and with the
+// blocks in band order the last waves to be dispatched are as heavy as any:
+// the launch ended in a ~70 us drain with the machine less and less occupied
+// (profiles/r06s_wtl.json: 86 % of the wave slots busy over the launch).
+// XCD x's dispatch range (xcd_remap) now holds the blocks with the same
+// range of NATURAL indices 4 tile + sub (a horizontal strip of tiles, so a
+// tile's four blocks and most of a Gaussian's tiles still share that XCD's
+// L2), in descending order of their list length in 16-candidate groups (the
+// forward's lcount): the drain is made of the lightest blocks.  One
+// workgroup per XCD range, an LDS counting sort, launched right after the
+// forward render.  Speed only: every block is still processed exactly once.
+// (Keyed by the tile's instance count instead -- known before the render, so
+// the sort could run on the colour stream during the binning -- it gained
+// nothing: a block's list length does not follow its tile's count.)
+#define LSR_ORD_NB 64
+#ifndef LSR_ORD_THREADS
+#define LSR_ORD_THREADS 1024
+#endif
+#define LSR_ORD_KPT 16   // keys held per thread (ranges up to 16 x LSR_ORD_THREADS blocks in one pass)
+__global__ void __launch_bounds__(LSR_ORD_THREADS) k_bwd_order(const uint32_t* __restrict__ lcount, int n,
+                                                    uint32_t* __restrict__ border)
+{
+    __shared__ uint32_t cnt[LSR_ORD_NB];
+    const int q = n / 8, r = n % 8, x = blockIdx.x;
+    const int lo = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+    const int len = q + (x < r ? 1 : 0);
+    const int tid = threadIdx.x;
+    if (tid < LSR_ORD_NB) cnt[tid] = 0u;
+    __syncthreads();
+    auto key = [&](int i) { return min((int)((lcount[lo + i] + 15u) >> 4), LSR_ORD_NB - 1); };
+    constexpr int STEP = LSR_ORD_THREADS * LSR_ORD_KPT;
+    int kr[LSR_ORD_KPT];
+    for (int c = 0; c < len; c += STEP) {
+#pragma unroll
+        for (int j = 0; j < LSR_ORD_KPT; j++) {
+            const int i = c + tid + LSR_ORD_THREADS * j;
+            kr[j] = i < len ? key(i) : -1;
+        }
+#pragma unroll
+        for (int j = 0; j < LSR_ORD_KPT; j++)
+            if (kr[j] >= 0) atomicAdd(&cnt[kr[j]], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) {   // range offsets, heaviest bucket first: one wave's prefix sum (lane k: bucket 63 - k)
+        static_assert(LSR_ORD_NB == 64, "one bucket per lane");
+        const uint32_t v = cnt[63 - tid];
+        uint32_t incl = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t u = __shfl_up(incl, d, 64);
+            if (tid >= d) incl += u;
+        }
+        cnt[63 - tid] = (uint32_t)lo + incl - v;
+    }
+    __syncthreads();
+    for (int c = 0; c < len; c += STEP) {
+        if (len > STEP) {   // (one pass holds the whole range otherwise)
+#pragma unroll
+            for (int j = 0; j < LSR_ORD_KPT; j++) {
+                const int i = c + tid + LSR_ORD_THREADS * j;
+                kr[j] = i < len ? key(i) : -1;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < LSR_ORD_KPT; j++)
+            if (kr[j] >= 0) border[atomicAdd(&cnt[kr[j]], 1u)] = (uint32_t)(lo + c + tid + LSR_ORD_THREADS * j);
+    }
+}
+
+hipError_t launch_bwd_order(const RenderArgs& a, uint32_t* border, hipStream_t st)
+{
+    const int n = 4 * a.cam.gx * a.cam.gy;
+    if (n == 0) return hipSuccess;
+    k_bwd_order<<<8, LSR_ORD_THREADS, 0, st>>>(a.lcount, n, border);
+    return hipGetLastError();
+}
+
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -1508,7 +1597,7 @@ struct WaveStageL {
 // waves per SIMD the MFMA backward is compiled for: 4 for the list-driven
 // D = 16 kernel (the headline's), the launch-bounds floor otherwise
 template <int NL, bool LD, bool LST, bool DET = false>
-constexpr int bwd_waves() { return (LST && LD && NL == 16 && !DET) ? 4 : LSR_MF_WAVES; }
+constexpr int bwd_waves() { return (LST && LD && NL == 16 && !DET) ? LSR_BWD16_WAVES : LSR_MF_WAVES; }
 
 // LDS-DMA of one 16-B row part per lane: lane l's bytes land at lds + 16 l (an
 // LDS-DMA writes wave-uniform M0 + lane x size).  Inline asm with M0 saved and
@@ -1731,7 +1820,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_wav
 
     const RenderArgs& a = b.f;
     const Cam& c = a.cam;
-    const WaveTile wt(a);
+    const WaveTile wt(a, LST ? a.border : nullptr);
     const int lane = threadIdx.x;
     const int lg = lane >> 4, li = lane & 15;
     const PixMap pm(c, wt.tile, lane + (wt.sub << 6));
