@@ -108,6 +108,11 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st);
 #ifndef LSR_BWD_ORDER
 #define LSR_BWD_ORDER 1   // list-driven backward: heaviest block lists dispatched first (0: band order)
 #endif
+// from this many 8x8 blocks (4 T) up: four or more generations of the
+// backward's 4,096 resident waves, where its drain is worth the order
+// kernel's ~7.5 us (cfg3: 32,640 blocks)
+#define LSR_BWD_ORDER_MIN_BLOCKS 16384
+inline bool bwd_order_on(int T) { return LSR_BWD_ORDER && 4 * (int64_t)T >= LSR_BWD_ORDER_MIN_BLOCKS; }
 hipError_t launch_bwd_order(const RenderArgs& a, uint32_t* border, hipStream_t st);
 
 struct RenderBwdArgs {
