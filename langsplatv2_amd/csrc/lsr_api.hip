@@ -797,7 +797,7 @@ static void set_block_lists_bwd(RenderArgs& ra, const void* lb, const void* img,
 {
     set_block_lists(ra, (void*)lb, M);
     const size_t T = (size_t)ra.cam.gx * ra.cam.gy;
-    if (bwd_order_on((int)T)) ra.border = (const uint32_t*)((const uint8_t*)img + image_layout((size_t)ra.cam.W * ra.cam.H, T).border);
+    if (bwd_order_on((int)T)) ra.border = (const uint4*)((const uint8_t*)img + image_layout((size_t)ra.cam.W * ra.cam.H, T).border);
 }
 
 int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, lsr_alloc_fn alloc, void* ctx,
@@ -1013,7 +1013,7 @@ int lsr_forward(const lsr_settings* s, const lsr_inputs* in, lsr_fwd_out* out, l
     LSR_HIP(join.wait());   // the SH colours of a split preprocess
     { StageScope sc(ST_RENDER, st); LSR_HIP(launch_render_fwd(ra, st)); }
     // the backward's block order from the lists the render just counted
-    if (bwd_order_on(T) && ra.lcount) LSR_HIP(launch_bwd_order(ra, (uint32_t*)(img + IL.border), st));
+    if (bwd_order_on(T) && ra.lcount) LSR_HIP(launch_bwd_order(ra, (uint4*)(img + IL.border), st));
     LSR_DEBUG_SYNC(s, st, "render");
     LSR_GUARD(guard, "out_color", out->out_color, 3 * NPIX);
     LSR_GUARD(guard, "out_lang", out->out_lang, (size_t)(s->quick_render ? quick_dim(s) : Dd) * NPIX);

@@ -570,7 +570,7 @@ __host__ __device__ inline ImageLayout image_layout(size_t P, size_t T)
     L.cls_cnt = o;    o += 512;                        // per-class tile counts (tile-sort classes); word 32: ticket;
                                                        // words 64-65: the tile count's total + arrivals
     L.cls_list = o;   o += align256(T * 6 * 4);        // per-class tile lists, T slots each
-    L.border = o;     o += align256(T * 4 * 4);        // the list-driven backward's block order (k_bwd_order)
+    L.border = o;     o += align256(T * 4 * 16);       // the list-driven backward's block order (k_bwd_order)
     L.total = o;
     return L;
 }

@@ -101,7 +101,7 @@ struct RenderArgs {
     uint32_t* lcount = nullptr;
     // backward only: the blocks in dispatch order, heaviest list first inside
     // each XCD's range (k_bwd_order; null = band order)
-    const uint32_t* border = nullptr;
+    const uint4* border = nullptr;   // {block 4 tile + sub, tile_start[tile], tile_start[tile + 1], lcount[block]}
 };
 hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st);
 // the backward's block order (RenderArgs::border, 4 T entries) from the forward's lcount
@@ -113,7 +113,7 @@ hipError_t launch_render_fwd(const RenderArgs& a, hipStream_t st);
 // kernel's ~7.5 us (cfg3: 32,640 blocks)
 #define LSR_BWD_ORDER_MIN_BLOCKS 16384
 inline bool bwd_order_on(int T) { return LSR_BWD_ORDER && 4 * (int64_t)T >= LSR_BWD_ORDER_MIN_BLOCKS; }
-hipError_t launch_bwd_order(const RenderArgs& a, uint32_t* border, hipStream_t st);
+hipError_t launch_bwd_order(const RenderArgs& a, uint4* border, hipStream_t st);
 
 struct RenderBwdArgs {
     RenderArgs f;

@@ -126,14 +126,22 @@ __device__ __forceinline__ int band_tile(int t, int gx, int gy)
 }
 struct WaveTile {
     int tile, sub;
+    // with an order: the block's tile range and list count from the same entry
+    // (one load before the wave can start its list DMA and fragment loads)
+    uint32_t rs = 0u, re = 0u, lc = 0u;
+    bool ent = false;
     // order (the backward's RenderArgs::border): dispatch slot -> block 4 tile + sub
-    __device__ WaveTile(const RenderArgs& a, const uint32_t* order = nullptr)
+    __device__ WaveTile(const RenderArgs& a, const uint4* order = nullptr)
     {
         const int o = xcd_remap(blockIdx.x, gridDim.x);
         if (order) {
-            const int v = (int)order[o];
-            tile = v >> 2;
-            sub = v & 3;
+            const uint4 e = order[o];
+            tile = (int)(e.x >> 2);
+            sub = (int)(e.x & 3u);
+            rs = e.y;
+            re = e.z;
+            lc = e.w;
+            ent = true;
         } else {
             tile = band_tile(o >> 2, a.cam.gx, a.cam.gy);
             sub = o & 3;
@@ -165,8 +173,9 @@ struct WaveTile {
 #define LSR_ORD_THREADS 1024
 #endif
 #define LSR_ORD_KPT 16   // keys held per thread (ranges up to 16 x LSR_ORD_THREADS blocks in one pass)
-__global__ void __launch_bounds__(LSR_ORD_THREADS) k_bwd_order(const uint32_t* __restrict__ lcount, int n,
-                                                    uint32_t* __restrict__ border)
+__global__ void __launch_bounds__(LSR_ORD_THREADS) k_bwd_order(const uint32_t* __restrict__ lcount,
+                                                    const uint32_t* __restrict__ tile_start, int n,
+                                                    uint4* __restrict__ border)
 {
     __shared__ uint32_t cnt[LSR_ORD_NB];
     const int q = n / 8, r = n % 8, x = blockIdx.x;
@@ -211,15 +220,19 @@ __global__ void __launch_bounds__(LSR_ORD_THREADS) k_bwd_order(const uint32_t* _
         }
 #pragma unroll
         for (int j = 0; j < LSR_ORD_KPT; j++)
-            if (kr[j] >= 0) border[atomicAdd(&cnt[kr[j]], 1u)] = (uint32_t)(lo + c + tid + LSR_ORD_THREADS * j);
+            if (kr[j] >= 0) {
+                const uint32_t blk = (uint32_t)(lo + c + tid + LSR_ORD_THREADS * j);
+                border[atomicAdd(&cnt[kr[j]], 1u)] =
+                    make_uint4(blk, tile_start[blk >> 2], tile_start[(blk >> 2) + 1], lcount[blk]);
+            }
     }
 }
 
-hipError_t launch_bwd_order(const RenderArgs& a, uint32_t* border, hipStream_t st)
+hipError_t launch_bwd_order(const RenderArgs& a, uint4* border, hipStream_t st)
 {
     const int n = 4 * a.cam.gx * a.cam.gy;
     if (n == 0) return hipSuccess;
-    k_bwd_order<<<8, LSR_ORD_THREADS, 0, st>>>(a.lcount, n, border);
+    k_bwd_order<<<8, LSR_ORD_THREADS, 0, st>>>(a.lcount, a.tile_start, n, border);
     return hipGetLastError();
 }
 
@@ -1831,7 +1844,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_wav
     const bool inside = pm.px < c.W && pm.py < c.H;
     const float pfx = (float)pm.px, pfy = (float)pm.py;
     const float cx = (float)pm.bx + 3.5f, cy = (float)pm.by + 3.5f;
-    const uint32_t rs = a.tile_start[wt.tile];
+    const uint32_t rs = wt.ent ? wt.rs : a.tile_start[wt.tile];
     const size_t HW = (size_t)c.H * c.W;
     const size_t pix = (size_t)pm.py * c.W + pm.px;
     const int D = a.D;
@@ -1866,8 +1879,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(bwd_wav
     uint32_t gid1 = 0u, gid2 = 0u;
     float4 A1 = make_float4(0.f, 0.f, 0.f, 0.f), B1 = A1;
     // LST: entries [lbase, lbase + cnt) of the block's list, back to front
-    const uint32_t lcnt = LST ? a.lcount[4 * wt.tile + wt.sub] : 0u;
-    const size_t lbase = LST ? (size_t)4 * rs + (size_t)wt.sub * (a.tile_start[wt.tile + 1] - rs) : 0;
+    const uint32_t lcnt = LST ? (wt.ent ? wt.lc : a.lcount[4 * wt.tile + wt.sub]) : 0u;
+    const size_t lbase = LST ? (size_t)4 * rs + (size_t)wt.sub * ((wt.ent ? wt.re : a.tile_start[wt.tile + 1]) - rs) : 0;
     if constexpr (!LST) {
         gid1 = pl_at(wmax - 1 - lane);
         if constexpr (SPF) {

@@ -26,7 +26,7 @@ def image_layout(P: int, T: int) -> dict:
     o, L = 0, {}
     for name, nb in (("final_T", P * 4), ("n_contrib", P * 4), ("tile_cnt", T * 4), ("tile_start", (T + 1) * 4),
                      ("tile_part", ((T + 63) // 64 + 1) * 8), ("cls_cnt", 512), ("cls_list", T * 6 * 4),
-                     ("border", T * 4 * 4)):
+                     ("border", T * 4 * 16)):
         L[name] = o
         o += _a(nb)
     L["total"] = o

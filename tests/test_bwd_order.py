@@ -6,7 +6,8 @@ A training forward ends by sorting the 8x8 blocks of each XCD dispatch range
 in 16-candidate groups, heaviest first.  The backward's wave in slot o then
 runs block border[o].  Every block must be run exactly once, so the order is
 checked as a permutation that keeps each range's natural block strip, in
-non-increasing group count; the gradients it produces are covered by the
+non-increasing group count, each entry carrying its block's tile range and
+list count; the gradients it produces are covered by the
 whole-frame and deterministic tests (each block's partial sums are the same
 whatever the dispatch order).  Frames below LSR_BWD_ORDER_MIN_BLOCKS blocks
 (lsr_internal.h) keep the band order; the cases here are above it.
@@ -54,7 +55,13 @@ def test_block_order_is_a_heavy_first_permutation_per_xcd_range(N, W, H):
     lcount = lists[2 * a256(4 * M * 16):2 * a256(4 * M * 16) + 4 * n].view(torch.int32).cpu().numpy()
     L = layout.image_layout(W * H, T)
     img = bufs[_lib.LSR_BUF_IMAGE]
-    border = img[L["border"]:L["border"] + 4 * n].view(torch.int32).cpu().numpy().astype(np.int64)
+    ent = img[L["border"]:L["border"] + 16 * n].view(torch.int32).cpu().numpy().astype(np.int64).reshape(n, 4)
+    border = ent[:, 0]
+    tile_start = img[L["tile_start"]:L["tile_start"] + 4 * (T + 1)].view(torch.int32).cpu().numpy().astype(np.int64)
+    # each entry carries its block's tile range and list count (the backward's first load)
+    assert np.array_equal(ent[:, 1], tile_start[border >> 2])
+    assert np.array_equal(ent[:, 2], tile_start[(border >> 2) + 1])
+    assert np.array_equal(ent[:, 3], lcount.astype(np.int64)[border])
     groups = np.minimum((lcount.astype(np.int64) + 15) // 16, 63)
     assert sorted(border.tolist()) == list(range(n)), "every block exactly once"
     for lo, ln in xcd_ranges(n):
